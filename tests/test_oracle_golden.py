@@ -1,0 +1,135 @@
+"""Pin the CPU oracle against golden vectors produced by running the reference.
+
+CPU-only (no GPU): these tests are what makes the oracle trustworthy as the
+parity checker for the HIP kernels.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import irc_oracle as O
+from oracle import train_oracle
+
+
+def test_nce_known_answers():
+    g = load_golden("nce.npz")
+    # SURVEY.md 8c known answers (reference run, torch.manual_seed(0), N=4 C=8 K=16)
+    assert abs(float(g["n4_d8_k16_noq_loss"]) - 48.34416198730469) < 1e-9
+    assert abs(float(g["n4_d8_k16_q_loss"]) - 64.79255676269531) < 1e-9
+
+
+@pytest.mark.parametrize("tag", ["n4_d8_k16_noq", "n4_d8_k16_q", "n32_d128_k0_noq",
+                                 "n32_d128_k512_noq", "n32_d128_k512_q", "n64_d128_k1024_q",
+                                 "n64_d128_k1024_noq", "n8_d32_k64_q"])
+def test_nce_loss_and_grad(tag):
+    g = load_golden("nce.npz")
+    queue = g.get(f"{tag}_queue")
+    loss, dq = O.nce_info_loss(g[f"{tag}_q"], g[f"{tag}_k"], queue, 0.05)
+    ref = float(g[f"{tag}_loss"])
+    assert abs(loss - ref) <= 2e-6 * abs(ref) + 1e-5
+    np.testing.assert_allclose(dq, g[f"{tag}_dq"], rtol=1e-4, atol=2e-5)
+
+
+def _lstm_params(g, tag):
+    pre = f"{tag}_param_"
+    return {k[len(pre):]: np.asarray(v, np.float64) for k, v in g.items() if k.startswith(pre)}
+
+
+@pytest.mark.parametrize("tag", ["a", "b"])
+def test_seq2vec_and_head_grads(tag):
+    g = load_golden("seq2vec.npz")
+    B, L, inp, hid, layers, outd, kq = (int(x) for x in g[f"{tag}_dims"])
+    p = _lstm_params(g, tag)
+    a = np.asarray(g[f"{tag}_anchor"], np.float64)
+    pos = np.asarray(g[f"{tag}_positive"], np.float64)
+    y, _ = O.lstm_head_fwd(a, p, layers)
+    np.testing.assert_allclose(y, g[f"{tag}_head_out"], rtol=1e-4, atol=1e-5)
+    eq, cache = O.seq2vec(a, p, layers)
+    ek, _ = O.seq2vec(pos, p, layers)  # encoder_k == encoder_q at init
+    np.testing.assert_allclose(eq, g[f"{tag}_emb_q"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(ek, g[f"{tag}_emb_k"], rtol=1e-4, atol=1e-5)
+    loss, dq = O.nce_info_loss(eq, ek, g[f"{tag}_queue"], 0.05)
+    assert abs(loss - float(g[f"{tag}_loss"])) < 1e-4
+    grads = O.seq2vec_bwd(dq, p, cache, layers)
+    for name, gv in grads.items():
+        ref = g[f"{tag}_grad_{name}"]
+        np.testing.assert_allclose(gv, ref, rtol=2e-3, atol=2e-5 * max(1.0, np.abs(ref).max()),
+                                   err_msg=name)
+
+
+def test_bert_forward():
+    g = load_golden("bert_tiny.npz")
+    w = {k[2:]: v for k, v in g.items() if k.startswith("w_")}
+    vocab, hid, nl, nh, inter, maxpos = (int(x) for x in g["cfg"])
+    out = O.bert_forward(g["input_ids"], g["attention_mask"], w, nl, nh)
+    np.testing.assert_allclose(out, g["last_hidden_state"], rtol=1e-4, atol=1e-4)
+
+
+def test_scan_grid_matches_reference_closest_docs():
+    g = load_golden("scan.npz")
+    q = g["grid_q"].astype(np.float32) / 128
+    d = g["grid_d"].astype(np.float32) / 128
+    k = int(g["grid_k"])
+    idx, sc = O.scan_topk(q, d, k)
+    np.testing.assert_array_equal(idx, g["grid_idx"])
+    np.testing.assert_array_equal(sc, g["grid_score"])
+
+
+def test_scan_ties_rule():
+    g = load_golden("scan.npz")
+    q = g["tie_q"].astype(np.float32) / 128
+    d = g["tie_d"].astype(np.float32) / 128
+    k = int(g["tie_k"])
+    idx, sc = O.scan_topk(q, d, k, chunk=700)  # chunked merge must not change ties
+    np.testing.assert_array_equal(sc, g["tie_score"])  # reference's score multiset/order
+    full = O.scan_scores(q, d)
+    for r in range(q.shape[0]):
+        assert np.all(full[r, idx[r]] == sc[r])
+        # tie rule: equal scores -> ascending index
+        for j in range(k - 1):
+            assert sc[r, j] > sc[r, j + 1] or idx[r, j] < idx[r, j + 1]
+        # completeness at the boundary: no excluded doc beats the last one
+        rest = np.setdiff1d(np.arange(d.shape[0]), idx[r])
+        last_s, last_i = sc[r, -1], idx[r, -1]
+        assert not np.any((full[r, rest] > last_s) | ((full[r, rest] == last_s) & (rest < last_i)))
+
+
+def test_scan_edge_cases():
+    rng = np.random.default_rng(0)
+    q = rng.integers(-3, 4, (3, 128)).astype(np.float32) / 128
+    d = rng.integers(-3, 4, (5, 128)).astype(np.float32) / 128
+    idx, sc = O.scan_topk(q, d, 8, doc_offset=100)  # k > N: padded
+    assert (idx[:, 5:] == -1).all() and np.isneginf(sc[:, 5:]).all()
+    assert set(idx[0, :5]) == set(range(100, 105))
+    idx0, _ = O.scan_topk(q, d[:0], 4)
+    assert (idx0 == -1).all()
+
+
+def test_merge_equals_global():
+    rng = np.random.default_rng(1)
+    q = rng.integers(-2, 3, (4, 128)).astype(np.float32) / 128
+    d = rng.integers(-2, 3, (999, 128)).astype(np.float32) / 128
+    full_i, full_s = O.scan_topk(q, d, 50)
+    parts = [(0, 250), (250, 600), (600, 999)]
+    li, ls = zip(*[O.scan_topk(q, d[a:b], 50, doc_offset=a) for a, b in parts])
+    mi, ms = O.merge_topk(li, ls, 50)
+    np.testing.assert_array_equal(mi, full_i)
+    np.testing.assert_array_equal(ms, full_s)
+
+
+def test_train_trajectory_matches_reference():
+    fx = load_golden("train_traj.npz")
+    losses, final = train_oracle.run_trajectory(fx)
+    np.testing.assert_allclose(losses, fx["mb_loss"], rtol=2e-5, atol=1e-4)
+    for k, v in final.items():
+        ref = fx["final_" + k]
+        np.testing.assert_allclose(np.asarray(v).reshape(ref.shape), ref, rtol=1e-4, atol=2e-6,
+                                   err_msg=k)
+
+
+def test_enqueue_rule():
+    queue = np.zeros((4, 12))
+    q2, ptr = O.dequeue_and_enqueue(queue, 8, np.ones((4, 4)))
+    assert ptr == 0 and (q2[:, 8:] == 1).all()
+    q3, ptr = O.dequeue_and_enqueue(queue, 0, np.ones((5, 4)))  # 12 % 5 != 0: no update
+    assert ptr == 0 and (q3 == 0).all()
