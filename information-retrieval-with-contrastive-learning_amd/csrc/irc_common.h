@@ -1,0 +1,108 @@
+// Shared device/host helpers for libirc_hip.so (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "irc.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define IRC_LDS_BYTES (160 * 1024)
+
+namespace irc {
+
+// ---- host-side error plumbing (irc_runtime.hip) ----
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define IRC_REQUIRE(cond, ...)          \
+  do {                                  \
+    if (!(cond)) {                      \
+      ::irc::set_error(__VA_ARGS__);    \
+      return IRC_E_INVALID;             \
+    }                                   \
+  } while (0)
+
+bool prof_on();
+void prof_begin(hipStream_t st);
+void prof_end(const char* name, hipStream_t st);
+
+static inline hipStream_t as_stream(irc_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- device helpers ----
+
+// s_waitcnt that waits only on vmcnt <= N (gfx9 encoding: vmcnt lo [3:0], hi [15:14];
+// expcnt [6:4] and lgkmcnt [11:8] left at their maxima so they do not wait).
+// Counts above the 6-bit maximum clamp to 63 (waiting for MORE ops is always safe).
+template <int N0>
+__device__ __forceinline__ void wait_vmcnt() {
+  constexpr int N = N0 > 63 ? 63 : N0;
+  static_assert(N >= 0, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// Raw workgroup barrier that does NOT drain vmcnt (so LDS-DMA prefetches stay in
+// flight across it); the empty asm statements stop the compiler moving memory
+// operations across the barrier.
+__device__ __forceinline__ void wg_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// 16-byte global -> LDS DMA (global_load_lds_dwordx4).  The LDS destination of
+// lane l is (wave-uniform lds_base) + 16*l; the global source is per lane.
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)gsrc,
+      (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// Order-preserving map fp32 -> uint32 (larger float -> larger uint).  -0.0 is
+// folded to +0.0 and NaN to 0 (lowest), matching oracle.canon_scores.
+__device__ __forceinline__ uint32_t orderable_f32(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) == 0) u = 0;
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return 0u;  // NaN
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ float unorderable_f32(uint32_t h) {
+  uint32_t u = (h & 0x80000000u) ? (h & 0x7fffffffu) : ~h;
+  return __uint_as_float(u);
+}
+
+// Distinct 64-bit ranking key: score in the high word, bitwise-NOT of the global
+// doc index in the low word, so a larger key = higher score, then LOWER index.
+__device__ __forceinline__ uint64_t make_key(float score, uint32_t gidx) {
+  return ((uint64_t)orderable_f32(score) << 32) | (uint64_t)(uint32_t)(~gidx);
+}
+
+__device__ __forceinline__ float bf16_to_f32(unsigned short b) {
+  return __uint_as_float(((uint32_t)b) << 16);
+}
+
+__device__ __forceinline__ unsigned short f32_to_bf16(float f) {
+  __bf16 h = (__bf16)f;  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return __builtin_bit_cast(unsigned short, h);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace irc

@@ -1,0 +1,81 @@
+"""ctypes binding of libirc_hip.so (the C ABI declared in include/irc.h).
+
+The product path has NO fallback: if the library is missing or the device is not
+a HIP GPU, every op raises.  Build the library with ``__graft_entry__.build()``
+(or ``make -C information-retrieval-with-contrastive-learning_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libirc_hip.so")
+
+_c = ctypes
+P = _c.c_void_p
+I64 = _c.c_int64
+I32 = _c.c_int
+F32 = _c.c_float
+
+# name -> (restype, argtypes).  Keep in sync with include/irc.h
+# (tests/test_abi.py checks every declared symbol is exported and bound here).
+SIGNATURES = {
+    "irc_last_error": (_c.c_char_p, []),
+    "irc_abi_version": (I32, []),
+    "irc_scan_topk_workspace": (I64, [I64, I64, I64, I64]),
+    "irc_scan_topk": (I32, [P, P, I64, I64, I64, I64, I64, P, I64, P, P, P]),
+    "irc_topk_merge": (I32, [P, P, I64, I64, I64, I64, P, P, P]),
+    "irc_scan_scores": (I32, [P, P, I64, I64, I64, P, P]),
+    "irc_prof_enable": (I32, [I32]),
+    "irc_prof_query": (I32, [_c.c_char_p, _c.POINTER(_c.c_double), _c.POINTER(I64)]),
+    "irc_prof_reset": (I32, []),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class IRCError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the library; raises IRCError if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise IRCError(
+                f"libirc_hip.so not found at {LIB_PATH}: build it first "
+                "(python -c 'import __graft_entry__ as g; g.build()'). "
+                "There is no CPU fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def call(name: str, *args):
+    """Call an IRC entry point; raise on a non-zero status with the library's
+    thread-local message ("out of memory" is kept in the text so the
+    reference's OOM handler, src/train.py:190-195, still matches)."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.irc_last_error().decode(errors="replace")
+        if rc == 2:  # hipErrorOutOfMemory
+            msg = "HIP out of memory: " + msg
+        raise IRCError(f"{name} failed (rc={rc}): {msg}")
+    return rc
+
+
+def fn(name: str):
+    return getattr(load(), name)

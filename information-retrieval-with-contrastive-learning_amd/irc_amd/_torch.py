@@ -1,0 +1,48 @@
+"""Thin torch plumbing for the C ABI: device checks, raw pointers, the current
+HIP stream, and the workspace allocator.  PyTorch is plumbing only here: memory,
+streams, autograd bookkeeping and torch.distributed -- never the compute."""
+from __future__ import annotations
+
+import torch
+
+from ._lib import IRCError
+
+
+def require_hip(*tensors: torch.Tensor) -> None:
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise IRCError(
+                "irc_amd kernels run on a HIP device (MI355X / gfx950) only; got a tensor on "
+                f"{t.device}. There is no CPU fallback in the product path.")
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr(device: torch.device | None = None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def contig(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    if t.dtype != dtype:
+        t = t.to(dtype)
+    return t.contiguous()
+
+
+_ws_cache: dict = {}
+
+
+def workspace(nbytes: int, device: torch.device, tag: str = "default") -> torch.Tensor:
+    """Grow-only per-(device, tag) scratch buffer from the caching allocator.
+
+    Stream-ordered reuse is safe because every IRC call on a tag is issued on the
+    same (current) stream; callers on other streams must pass their own tag."""
+    key = (device.index if device.index is not None else torch.cuda.current_device(), tag)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf

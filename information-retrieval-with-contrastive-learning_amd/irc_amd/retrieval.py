@@ -1,0 +1,122 @@
+"""Dense retrieval: corpus-wide cosine top-k over a (sharded) document corpus.
+
+Semantics: scores = <e_q, e_n> of L2-normalised
+``ctx2vec`` embeddings (src/evaluation.py:110-112, src/contrastor/
+contrastive_module.py:96-100), per-query top-k by descending score as in
+``TfidfDocRanker.closest_docs`` (preprocessing/drqa/retriever/
+tfidf_doc_ranker.py:60-75); equal scores -> lower global doc index.
+
+Multi-GPU: the corpus is split into contiguous shards, one per
+rank, resident in HBM.  A search all-gathers the query embeddings over RCCL,
+scans the local shard (global indices via the shard offset), all-gathers the
+per-shard top-k lists and merges them with the same exact rule.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._torch import contig, ptr, require_hip, stream_ptr, workspace
+
+
+def scan_topk(queries: torch.Tensor, docs: torch.Tensor, k: int, doc_offset: int = 0):
+    """Exact top-k of queries @ docs.T (bf16 inputs, fp32 scores).
+
+    queries [Q, D], docs [N, D] on the same HIP device.  Returns
+    (scores fp32 [Q, k], idx int64 [Q, k]) sorted by (score desc, idx asc);
+    slots past N are (-inf, -1).
+    """
+    require_hip(queries, docs)
+    q = contig(queries, torch.bfloat16)
+    d = contig(docs, torch.bfloat16)
+    Q, D = q.shape
+    N = d.shape[0]
+    if d.shape[1] != D:
+        raise ValueError(f"dim mismatch: queries D={D}, docs D={d.shape[1]}")
+    out_s = torch.empty((Q, k), dtype=torch.float32, device=q.device)
+    out_i = torch.empty((Q, k), dtype=torch.int64, device=q.device)
+    nbytes = int(_lib.fn("irc_scan_topk_workspace")(Q, N, D, k))
+    ws = workspace(nbytes, q.device, "scan")
+    _lib.call("irc_scan_topk", ptr(q), ptr(d), Q, N, D, k, doc_offset, ptr(ws), ws.numel(),
+              ptr(out_s), ptr(out_i), stream_ptr(q.device))
+    return out_s, out_i
+
+
+def scan_scores(queries: torch.Tensor, docs: torch.Tensor) -> torch.Tensor:
+    """Raw fp32 score matrix from the same MFMA path (tests / diagnostics)."""
+    require_hip(queries, docs)
+    q = contig(queries, torch.bfloat16)
+    d = contig(docs, torch.bfloat16)
+    out = torch.empty((q.shape[0], d.shape[0]), dtype=torch.float32, device=q.device)
+    _lib.call("irc_scan_scores", ptr(q), ptr(d), q.shape[0], d.shape[0], q.shape[1], ptr(out),
+              stream_ptr(q.device))
+    return out
+
+
+def topk_merge(scores: torch.Tensor, idx: torch.Tensor, k: int):
+    """Merge [P, Q, kin] per-shard lists into [Q, k] with the exact rule."""
+    require_hip(scores, idx)
+    s = contig(scores, torch.float32)
+    i = contig(idx, torch.int64)
+    P, Q, kin = s.shape
+    out_s = torch.empty((Q, k), dtype=torch.float32, device=s.device)
+    out_i = torch.empty((Q, k), dtype=torch.int64, device=s.device)
+    _lib.call("irc_topk_merge", ptr(s), ptr(i), P, Q, kin, k, ptr(out_s), ptr(out_i),
+              stream_ptr(s.device))
+    return out_s, out_i
+
+
+def shard_bounds(n_docs: int, world: int, rank: int):
+    """Contiguous shard [start, stop) of rank `rank` (first n % world ranks get +1)."""
+    base, rem = divmod(n_docs, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+class ShardedDenseIndex:
+    """One rank's HBM-resident shard of the corpus embedding matrix.
+
+    ``docs`` is this rank's shard [N_local, D] (bf16), ``doc_offset`` its first
+    global index.  ``search`` is collective over ``group`` when one is given:
+    every rank passes its local query slice (may be empty) and receives the
+    global top-k for ALL gathered queries (queries ordered by rank).
+    """
+
+    def __init__(self, docs: torch.Tensor, doc_offset: int = 0, group=None):
+        self.docs = docs.to(torch.bfloat16).contiguous()
+        self.doc_offset = int(doc_offset)
+        self.group = group
+
+    # The two device steps are methods so the collective orchestration can be
+    # exercised on CPU (gloo) with a test double in tests/test_dist_cpu.py.
+    def _local_topk(self, queries, k):
+        return scan_topk(queries, self.docs, k, self.doc_offset)
+
+    def _merge(self, scores, idx, k):
+        return topk_merge(scores, idx, k)
+
+    def search(self, queries: torch.Tensor, k: int):
+        import torch.distributed as dist
+
+        if self.group is None or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return self._local_topk(queries, k)
+        world = dist.get_world_size(self.group)
+        # (1) all-gather query embeddings (ragged: exchange counts first)
+        n_local = torch.tensor([queries.shape[0]], dtype=torch.int64, device=queries.device)
+        counts = [torch.zeros_like(n_local) for _ in range(world)]
+        dist.all_gather(counts, n_local, group=self.group)
+        counts = [int(c.item()) for c in counts]
+        qmax = max(counts)
+        qpad = torch.zeros((qmax, queries.shape[1]), dtype=queries.dtype, device=queries.device)
+        qpad[: queries.shape[0]] = queries
+        gathered = [torch.empty_like(qpad) for _ in range(world)]
+        dist.all_gather(gathered, qpad, group=self.group)
+        allq = torch.cat([g[:c] for g, c in zip(gathered, counts)], dim=0)
+        # (2) local exact top-k over this shard (global indices)
+        s, i = self._local_topk(allq, k)
+        # (3) exchange per-shard lists and merge (every rank gets the result)
+        ss = [torch.empty_like(s) for _ in range(world)]
+        ii = [torch.empty_like(i) for _ in range(world)]
+        dist.all_gather(ss, s.contiguous(), group=self.group)
+        dist.all_gather(ii, i.contiguous(), group=self.group)
+        return self._merge(torch.stack(ss), torch.stack(ii), k)

@@ -1,0 +1,154 @@
+"""Parity of the HIP corpus scan + top-k (irc_scan_topk) with the CPU oracle.
+
+Bit-exact on integer-grid embeddings (every fp32 dot product is exact in any
+accumulation order) and on the reference-generated golden fixtures; margin-aware
+on Gaussian data; size-independent properties at the full C2 size.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import irc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _grid(rng, shape, lim=127):
+    return rng.integers(-lim, lim + 1, shape).astype(np.float32) / 128
+
+
+def _dev(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+@pytest.mark.parametrize("D", [64, 128, 256, 384, 512, 768, 1024])
+def test_scores_exact_on_grid(gpu, D):
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(D)
+    q = _grid(rng, (70, D))
+    d = _grid(rng, (517, D))
+    s = retrieval.scan_scores(_dev(q, gpu), _dev(d, gpu)).cpu().numpy()
+    np.testing.assert_array_equal(s, O.scan_scores(q, d))
+
+
+def test_golden_grid_reference_order(gpu):
+    from irc_amd import retrieval
+
+    g = load_golden("scan.npz")
+    q = g["grid_q"].astype(np.float32) / 128
+    d = g["grid_d"].astype(np.float32) / 128
+    s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), int(g["grid_k"]))
+    np.testing.assert_array_equal(i.cpu().numpy(), g["grid_idx"])
+    np.testing.assert_array_equal(s.cpu().numpy(), g["grid_score"])
+
+
+def test_golden_ties(gpu):
+    from irc_amd import retrieval
+
+    g = load_golden("scan.npz")
+    q = g["tie_q"].astype(np.float32) / 128
+    d = g["tie_d"].astype(np.float32) / 128
+    k = int(g["tie_k"])
+    s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), k)
+    ri, rs = O.scan_topk(q, d, k)
+    np.testing.assert_array_equal(s.cpu().numpy(), g["tie_score"])
+    np.testing.assert_array_equal(i.cpu().numpy(), ri)
+
+
+@pytest.mark.parametrize("Q,N,D,k,off", [
+    (1, 1, 128, 1, 0),          # single doc
+    (3, 5, 128, 8, 11),         # k > N -> padded
+    (33, 31, 64, 10, 0),        # partial tile, Q not a multiple of 32
+    (257, 4099, 128, 100, 5),   # two query blocks, ragged tail
+    (16, 60000, 128, 100, 0),   # two-phase (sampled threshold) path
+    (64, 40000, 768, 1024, 3),  # maximum k
+    (8, 20000, 128, 1, 0),      # k = 1
+])
+def test_topk_exact_vs_oracle(gpu, Q, N, D, k, off):
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(Q * 7 + N)
+    q = _grid(rng, (Q, D), 3)  # small range -> many exact ties
+    d = _grid(rng, (N, D), 3)
+    s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), k, off)
+    ri, rs = O.scan_topk(q, d, k, doc_offset=off)
+    np.testing.assert_array_equal(i.cpu().numpy(), ri)
+    np.testing.assert_array_equal(s.cpu().numpy(), rs)
+
+
+def test_adversarial_sorted_corpus(gpu):
+    """Later docs strictly better than the sample: nearly every doc survives the
+    threshold, the selection must still be exact."""
+    from irc_amd import retrieval
+
+    N, D, k = 50000, 128, 100
+    q = np.zeros((4, D), np.float32)
+    q[:, 0] = 1.0
+    d = np.zeros((N, D), np.float32)
+    d[:, 0] = (np.arange(N) % 256) / 128.0 - 1.0  # ramp, repeated -> huge tie groups
+    s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), k)
+    ri, rs = O.scan_topk(q, d, k)
+    np.testing.assert_array_equal(i.cpu().numpy(), ri)
+    np.testing.assert_array_equal(s.cpu().numpy(), rs)
+
+
+def test_gaussian_margin_aware(gpu):
+    from irc_amd import retrieval
+
+    torch.manual_seed(2024)
+    Q, N, D, k = 64, 30000, 768, 100
+    q = torch.nn.functional.normalize(torch.randn(Q, D)).bfloat16()
+    d = torch.nn.functional.normalize(torch.randn(N, D)).bfloat16()
+    s, i = retrieval.scan_topk(q.to(gpu), d.to(gpu), k)
+    s, i = s.cpu().numpy(), i.cpu().numpy()
+    full = O.scan_scores(q.float().numpy(), d.float().numpy())
+    ri, rs = O.topk_rows(full, k)
+    tol = 1e-5  # fp32 accumulation-order difference on unit vectors, D=768
+    for r in range(Q):
+        # returned scores are the true scores of the returned docs (to fp32 rounding)
+        np.testing.assert_allclose(s[r], full[r, i[r]], atol=tol)
+        # same set except where the oracle's boundary score is within tol
+        diff = set(i[r]) ^ set(ri[r])
+        for doc in diff:
+            assert abs(full[r, doc] - rs[r, -1]) <= 2 * tol
+        assert np.all(np.diff(s[r]) <= 0)
+
+
+def test_merge_matches_unsharded(gpu):
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(3)
+    q = _grid(rng, (40, 128), 2)
+    d = _grid(rng, (7001, 128), 2)
+    k = 64
+    bounds = [retrieval.shard_bounds(7001, 3, r) for r in range(3)]
+    parts = [retrieval.scan_topk(_dev(q, gpu), _dev(d[a:b], gpu), k, a) for a, b in bounds]
+    ms, mi = retrieval.topk_merge(torch.stack([p[0] for p in parts]),
+                                  torch.stack([p[1] for p in parts]), k)
+    ri, rs = O.scan_topk(q, d, k)
+    np.testing.assert_array_equal(mi.cpu().numpy(), ri)
+    np.testing.assert_array_equal(ms.cpu().numpy(), rs)
+
+
+def test_full_c2_size_properties(gpu):
+    """C2: Q=256, N=100k, D=768, k=100 -- properties that do not need the oracle."""
+    from irc_amd import retrieval
+
+    g = torch.Generator(device="cpu").manual_seed(2024)
+    Q, N, D, k = 256, 100_000, 768, 100
+    d = torch.nn.functional.normalize(torch.randn(N, D, generator=g)).bfloat16().to(gpu)
+    q = torch.nn.functional.normalize(torch.randn(Q, D, generator=g)).bfloat16().to(gpu)
+    s, i = retrieval.scan_topk(q, d, k)
+    full = retrieval.scan_scores(q, d)  # same MFMA arithmetic
+    assert bool((i >= 0).all()) and bool((i < N).all())
+    assert torch.equal(s, torch.gather(full, 1, i))  # scores belong to their docs, bit-exact
+    assert bool((s[:, 1:] <= s[:, :-1]).all())
+    # completeness: nothing outside the list beats the k-th entry
+    masked = full.clone()
+    masked.scatter_(1, i, float("-inf"))
+    assert bool((masked.max(dim=1).values <= s[:, -1]).all())
+    # idempotence: a second call returns the same bits
+    s2, i2 = retrieval.scan_topk(q, d, k)
+    assert torch.equal(i, i2) and torch.equal(s, s2)
