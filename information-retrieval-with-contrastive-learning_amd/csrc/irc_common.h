@@ -47,6 +47,37 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
+// vmcnt(ahead*PW + extra) with ahead in {0,1,2} and a run-time extra in [0, 32]:
+// s_waitcnt takes an immediate, so dispatch over the small range (counts above
+// 63 clamp, which only waits for more).
+template <int PW>
+__device__ __forceinline__ void wait_vmcnt_dyn(int ahead, int extra) {
+  if (ahead == 0) {
+    wait_vmcnt<0>();
+    return;
+  }
+#define IRC_VM_CASE(E)                     \
+  case E:                                  \
+    if (ahead == 2)                        \
+      wait_vmcnt<2 * PW + E>();            \
+    else                                   \
+      wait_vmcnt<PW + E>();                \
+    return;
+  switch (extra) {
+    IRC_VM_CASE(0) IRC_VM_CASE(1) IRC_VM_CASE(2) IRC_VM_CASE(3) IRC_VM_CASE(4)
+    IRC_VM_CASE(5) IRC_VM_CASE(6) IRC_VM_CASE(7) IRC_VM_CASE(8) IRC_VM_CASE(9)
+    IRC_VM_CASE(10) IRC_VM_CASE(11) IRC_VM_CASE(12) IRC_VM_CASE(13) IRC_VM_CASE(14)
+    IRC_VM_CASE(15) IRC_VM_CASE(16) IRC_VM_CASE(17) IRC_VM_CASE(18) IRC_VM_CASE(19)
+    IRC_VM_CASE(20) IRC_VM_CASE(21) IRC_VM_CASE(22) IRC_VM_CASE(23) IRC_VM_CASE(24)
+    IRC_VM_CASE(25) IRC_VM_CASE(26) IRC_VM_CASE(27) IRC_VM_CASE(28) IRC_VM_CASE(29)
+    IRC_VM_CASE(30) IRC_VM_CASE(31) IRC_VM_CASE(32)
+    default:
+      if (ahead == 2) wait_vmcnt<2 * PW>(); else wait_vmcnt<PW>();  // conservative
+      return;
+  }
+#undef IRC_VM_CASE
+}
+
 // Raw workgroup barrier that does NOT drain vmcnt (so LDS-DMA prefetches stay in
 // flight across it); the empty asm statements stop the compiler moving memory
 // operations across the barrier.

@@ -34,146 +34,228 @@ struct Geo {
   static constexpr int SWZ = (LOWBIT < 16 ? LOWBIT : 16) - 1;
   static constexpr int TILE_BYTES = TD * D * 2;
   static constexpr int GLDS_PER_TILE = TD * CH / 64;  // wave-instructions per tile
-  static constexpr int NBUF = ((IRC_LDS_BYTES - 2048) / TILE_BYTES) >= 3 ? 3 : 2;
+  static constexpr int XBUF_BYTES = (D > 512) ? 4 * 4096 : 0;  // KS=2 exchange (NQ <= 4)
+  static constexpr int NBUF = ((IRC_LDS_BYTES - XBUF_BYTES) / TILE_BYTES) >= 3 ? 3 : 2;
   static constexpr int KK = D / 16;                  // MFMA k-steps
 };
 
 enum Mode { KEYS = 0, SCORES = 1 };
 
-// grid: x = worker (contiguous range of tiles), y = query block of NW*32 queries.
-template <int D, int NW, int MODE>
-__global__ __launch_bounds__(NW * 64) void scan_tile_kernel(
+// Opaque copy: stops LICM from hoisting per-lane address math out of the tile
+// loop (keeping 12+ 64-bit DMA addresses live costs more VGPRs than recomputing).
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// grid (1-D): G workers x GY query blocks, decoded XCD-aware so the GY blocks
+// that scan the SAME doc range are consecutive in dispatch order on the same XCD
+// (blocks b and b+8 share an XCD under round-robin placement): the corpus tile is
+// fetched from HBM once and re-read from that XCD's L2 by the partner block.
+// Placement only affects speed, never results.
+//
+// Waves: NQ query groups (32 queries each) x KS k-slices.  Wave (g, kh) keeps
+// the B fragments of its 32 queries for dims [kh*D/KS, (kh+1)*D/KS) in VGPRs;
+// with KS = 2 the partial 32x32 accumulators of the two k-slices are exchanged
+// through LDS (each wave finishes half of the 16 accumulator rows).
+//
+// Survivors: lane (r32, h) of wave (g, kh) finishes rows {(j&3) + 8(j>>2) + 4h}
+// for j in its half of [0, 16) of every tile, for query (g, r32).  It owns the
+// private slice (kh*2 + h) of the (worker, query) region and counts in a
+// register -- no atomics, nothing that could drain the LDS-DMA ring.
+template <int D, int NQ, int KS, int MODE>
+__global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
     const unsigned short* __restrict__ queries, const unsigned short* __restrict__ docs, int Q,
-    int Qpad, int64_t NS, int64_t stride, int tiles_per_worker, uint32_t idx_base,
+    int Qpad, int GY, int NS, int stride, int tiles_per_worker, uint32_t idx_base,
     const uint64_t* __restrict__ thr, uint64_t* __restrict__ keys, uint32_t* __restrict__ counts,
     int64_t cap, float* __restrict__ scores_out) {
   using G = Geo<D>;
+  constexpr int NW = NQ * KS;
+  constexpr int KKW = G::KK / KS;  // k-steps per wave
+  constexpr int JPW = 16 / KS;     // accumulator registers each wave finishes
+  constexpr int PW = (G::GLDS_PER_TILE + NW - 1) / NW;  // glds per wave per tile (upper bound)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint32_t* lds_cnt = reinterpret_cast<uint32_t*>(smem + G::NBUF * G::TILE_BYTES);
+  float* xbuf = reinterpret_cast<float*>(smem + G::NBUF * G::TILE_BYTES);
 
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = wave % NQ;
+  const int kh = wave / NQ;
   const int h = lane >> 5;
   const int r32 = lane & 31;
-  const int worker = blockIdx.x;
-  const int q = blockIdx.y * (NW * 32) + wave * 32 + r32;
+  const int b = blockIdx.x;
+  const int qblock = (b >> 3) % GY;
+  const int worker = ((b >> 3) / GY) * 8 + (b & 7);
+  const int q = qblock * (NQ * 32) + g * 32 + r32;
 
-  const int64_t ntiles_total = (NS + TD - 1) / TD;
-  const int64_t t_begin = (int64_t)worker * tiles_per_worker;
-  int64_t t_end = t_begin + tiles_per_worker;
+  const int ntiles_total = (NS + TD - 1) / TD;
+  const int t_begin = worker * tiles_per_worker;
+  int t_end = t_begin + tiles_per_worker;
   if (t_end > ntiles_total) t_end = ntiles_total;
-  const int my_tiles = t_end > t_begin ? (int)(t_end - t_begin) : 0;
+  const int my_tiles = t_end > t_begin ? t_end - t_begin : 0;
 
-  if (MODE == KEYS && threadIdx.x < NW * 32) lds_cnt[threadIdx.x] = 0;
-
-  // Stage one tile of TD logical docs into LDS buffer `buf` (lane-linear image;
-  // swizzle applied on the global source address, read with the same XOR).
-  auto issue_tile = [&](int64_t tile, int buf) {
-    char* base = smem + buf * G::TILE_BYTES;
+  // Per-lane byte offsets (within a tile) of this wave's PW DMA pieces; a piece
+  // i covers LDS bytes [1024 i, 1024 i + 1024) of the lane-linear image, lane l
+  // the 16 bytes at 1024 i + 16 l, sourced from (row, chunk ^ (row & SWZ)).
+  const int64_t row_bytes = (int64_t)stride * D * 2;
+  uint32_t goff[PW];
+  int grow[PW];
 #pragma unroll
-    for (int i0 = 0; i0 < G::GLDS_PER_TILE; i0 += NW) {
-      const int i = i0 + wave;
+  for (int t = 0; t < PW; ++t) {
+    const int i = t * NW + wave;
+    const int p = i * 64 + lane;
+    const int row = p / G::CH;
+    const int cp = p - row * G::CH;
+    const int c = cp ^ (row & G::SWZ);
+    grow[t] = row;
+    goff[t] = (uint32_t)(row * row_bytes + c * 16);
+  }
+  auto issue_tile = [&](int tile, int buf) {
+    char* base = smem + buf * G::TILE_BYTES;
+    const char* src0 = reinterpret_cast<const char*>(docs) + (int64_t)tile * TD * row_bytes;
+    const bool tail = (tile + 1) * TD > NS;  // uniform
+#pragma unroll
+    for (int t = 0; t < PW; ++t) {
+      const int i = t * NW + wave;
       if (G::GLDS_PER_TILE % NW == 0 || i < G::GLDS_PER_TILE) {
-        const int p = i * 64 + lane;
-        const int row = p / G::CH;
-        const int cp = p % G::CH;
-        const int c = cp ^ (row & G::SWZ);
-        int64_t s = tile * TD + row;
-        if (s >= NS) s = NS - 1;  // clamp: rows past the end are loaded but never kept
-        const unsigned short* src = docs + (s * stride) * (int64_t)D + c * 8;
-        glds16(src, base + i * 1024);
+        uint32_t off = goff[t];
+        if (tail && tile * TD + grow[t] >= NS)  // clamp: loaded but never kept
+          off -= (uint32_t)((tile * TD + grow[t] - (NS - 1)) * row_bytes);
+        glds16(src0 + off, base + i * 1024);
       }
     }
   };
 
-  // Prologue: start the LDS ring before touching the query fragments.
-  constexpr int PW = (G::GLDS_PER_TILE + NW - 1) / NW;  // glds per wave per tile (upper bound)
 #pragma unroll
-  for (int b = 0; b < G::NBUF - 1; ++b)
-    if (b < my_tiles) issue_tile(t_begin + b, b);
+  for (int bb = 0; bb < G::NBUF - 1; ++bb)
+    if (bb < my_tiles) issue_tile(t_begin + bb, bb);
 
-  // Stationary B fragments: lane holds Q[q][kk*16 + 8h .. +8] for every k-step.
-  bf16x8 bq[G::KK];
+  // Stationary B fragments: lane holds Q[q][kk*16 + 8h .. +8] for its k-steps.
+  bf16x8 bq[KKW];
   {
     const bool qv = q < Q;
-    const unsigned short* qrow = queries + (int64_t)(qv ? q : 0) * D + 8 * h;
+    const unsigned short* qrow = queries + (int64_t)(qv ? q : 0) * D + 8 * h + kh * (D / KS);
 #pragma unroll
-    for (int kk = 0; kk < G::KK; ++kk) {
+    for (int kk = 0; kk < KKW; ++kk) {
       u16x8 v = *reinterpret_cast<const u16x8*>(qrow + kk * 16);
       if (!qv) v = (u16x8)0;
       bq[kk] = __builtin_bit_cast(bf16x8, v);
     }
   }
-  const uint64_t qthr = (MODE == KEYS && thr != nullptr) ? thr[q] : 0ull;
+  const uint64_t qthr = (MODE == KEYS && thr != nullptr && q < Q) ? thr[q] : 0ull;
+  // LDS read offsets: chunk c = 2kk + h of row r32 lives at 16*(c ^ (r32 & SWZ));
+  // the XOR only touches the low 4 bits, so 8 per-lane offsets + an immediate
+  // 256*(kk>>3) cover all k-steps.
+  int lo[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int cj = 2 * j + h;
+    lo[j] = r32 * (G::CH * 16) + (((cj & 15) ^ (r32 & G::SWZ)) * 16);
+  }
+  uint32_t nsurv = 0;
+  // Survivor store instructions issued by this wave in the last two tiles
+  // (wave-uniform).  They sit between the ring's DMAs in vmcnt order, so the
+  // wait for tile `it` allows them as extra younger operations.
+  int nst1 = 0, nst2 = 0;
+  const int slice = kh * 2 + h;  // private output slice (of 2*KS)
+  uint64_t* myreg = keys + ((int64_t)worker * Qpad + q) * cap + slice * (cap / (2 * KS));
 
   for (int it = 0; it < my_tiles; ++it) {
-    const int64_t tile = t_begin + it;
+    const int tile = t_begin + it;
     if (it + G::NBUF - 1 < my_tiles) issue_tile(tile + G::NBUF - 1, (it + G::NBUF - 1) % G::NBUF);
-    // Wait for THIS wave's DMA of tile `it`: later tiles' DMAs may stay in flight.
     const int after = my_tiles - 1 - it;
-    if (G::NBUF == 3 && after >= 2)
-      wait_vmcnt<2 * PW>();
-    else if (after >= 1)
-      wait_vmcnt<PW>();
-    else
-      wait_vmcnt<0>();
+    const int ahead = (G::NBUF == 3 && after >= 2) ? 2 : (after >= 1 ? 1 : 0);
+    int extra = G::NBUF == 3 ? nst1 + nst2 : nst1;
+    extra = __builtin_amdgcn_readfirstlane(extra < 15 ? extra : 15);  // smaller = safe
+    wait_vmcnt_dyn<PW>(ahead, extra);
     wg_barrier();  // every wave's share of the tile has landed
 
-    const char* tb = smem + (it % G::NBUF) * G::TILE_BYTES;
+    const char* tb = smem + (it % G::NBUF) * G::TILE_BYTES + kh * (D / KS) * 2;
     f32x16 acc = (f32x16)0.0f;
 #pragma unroll
-    for (int kk = 0; kk < G::KK; ++kk) {
-      const int c = kk * 2 + h;
-      const int off = r32 * (G::CH * 16) + ((c ^ (r32 & G::SWZ)) * 16);
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(tb + off);
+    for (int kk = 0; kk < KKW; ++kk) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(tb + lo[kk & 7] + 256 * (kk >> 3));
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[kk], acc, 0, 0, 0);
+    }
+    if (KS == 2) {
+      // exchange: wave kh sends the half it does NOT finish, adds the partner's.
+      float* xo = xbuf + ((g * 2 + kh) * 64 + lane) * 8;
+      float* xi = xbuf + ((g * 2 + (kh ^ 1)) * 64 + lane) * 8;
+      f32x4 s0, s1;
+      if (kh == 0) {
+        s0 = (f32x4){acc[8], acc[9], acc[10], acc[11]};
+        s1 = (f32x4){acc[12], acc[13], acc[14], acc[15]};
+      } else {
+        s0 = (f32x4){acc[0], acc[1], acc[2], acc[3]};
+        s1 = (f32x4){acc[4], acc[5], acc[6], acc[7]};
+      }
+      reinterpret_cast<f32x4*>(xo)[0] = s0;
+      reinterpret_cast<f32x4*>(xo)[1] = s1;
+      wg_barrier();
+      const f32x4 t0 = reinterpret_cast<const f32x4*>(xi)[0];
+      const f32x4 t1 = reinterpret_cast<const f32x4*>(xi)[1];
+      if (kh == 0) {
+        acc[0] += t0[0]; acc[1] += t0[1]; acc[2] += t0[2]; acc[3] += t0[3];
+        acc[4] += t1[0]; acc[5] += t1[1]; acc[6] += t1[2]; acc[7] += t1[3];
+      } else {
+        acc[8] += t0[0]; acc[9] += t0[1]; acc[10] += t0[2]; acc[11] += t0[3];
+        acc[12] += t1[0]; acc[13] += t1[1]; acc[14] += t1[2]; acc[15] += t1[3];
+      }
     }
 
     // Epilogue: C[doc row][query col]; col = lane&31, row = (j&3) + 8(j>>2) + 4h.
-    if (q < Q) {
+    int nst = 0;
+    const int s0row = tile * TD;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int row = (j & 3) + 8 * (j >> 2) + 4 * h;
-        const int64_t s = tile * TD + row;
-        if (s < NS) {
-          if (MODE == SCORES) {
-            scores_out[(int64_t)q * NS + s] = acc[j];
-          } else {
-            const uint32_t gidx = idx_base + (uint32_t)(s * stride);
-            const uint64_t key = make_key(acc[j], gidx);
-            if (key >= qthr) {
-              const uint32_t slot = atomicAdd(&lds_cnt[wave * 32 + r32], 1u);
-              keys[((int64_t)worker * Qpad + q) * cap + slot] = key;
-            }
-          }
+    for (int jj = 0; jj < JPW; ++jj) {
+      const int j = (KS == 2 && kh == 1) ? jj + 8 : jj;
+      const int s = s0row + (j & 3) + 8 * (j >> 2) + 4 * h;
+      const float v = (KS == 2 && kh == 1) ? acc[jj + 8] : acc[jj];
+      const bool ok = (q < Q) && (s < NS);
+      if (MODE == SCORES) {
+        if (ok) scores_out[(int64_t)q * NS + s] = v;
+      } else {
+        const uint32_t gidx = idx_base + (uint32_t)s * (uint32_t)stride;
+        const uint64_t key = make_key(v, gidx);
+        const bool keep = ok && key >= qthr;
+        if (__ballot(keep)) {  // one store instruction when any lane keeps
+          ++nst;
+          if (keep) myreg[nsurv++] = key;
         }
       }
     }
-    wg_barrier();  // all reads of this buffer done before it is refilled
+    nst2 = nst1;
+    nst1 = nst;
+    wg_barrier();  // all reads of this buffer (and of xbuf) done before reuse
   }
 
-  if (MODE == KEYS) {
-    __syncthreads();
-    if (threadIdx.x < NW * 32) {
-      const int qq = blockIdx.y * (NW * 32) + threadIdx.x;
-      counts[(int64_t)worker * Qpad + qq] = lds_cnt[threadIdx.x];
-    }
-  }
+  if (MODE == KEYS && q < Qpad)
+    counts[((int64_t)worker * Qpad + q) * (2 * KS) + slice] = nsurv;
 }
 
 // ----------------------------------------------------------------- selection
 // Key sources for the select kernel.
-struct RegionSource {  // scan workspace: G regions per query, counts[g][q]
+struct RegionSource {  // scan workspace: G regions per query, NSL slices each
   const uint64_t* keys;
   const uint32_t* counts;
   int G;
   int Qpad;
   int64_t cap;
+  int NSL;
+  static constexpr bool kRegions = true;
+  __device__ __forceinline__ int nregions() const { return NSL * G; }
+  __device__ __forceinline__ uint32_t count(int q, int r) const {
+    return counts[((int64_t)(r / NSL) * Qpad + q) * NSL + (r % NSL)];
+  }
+  __device__ __forceinline__ const uint64_t* region(int q, int r) const {
+    return keys + ((int64_t)(r / NSL) * Qpad + q) * cap + (r % NSL) * (cap / NSL);
+  }
   template <class F>
   __device__ __forceinline__ void for_each(int q, int tid, int nt, F&& f) const {
-    for (int g = tid; g < G; g += nt) {
-      const uint32_t n = counts[(int64_t)g * Qpad + q];
-      const uint64_t* p = keys + ((int64_t)g * Qpad + q) * cap;
+    for (int gs = tid; gs < NSL * G; gs += nt) {
+      const int g = gs / NSL, sl = gs % NSL;
+      const uint32_t n = counts[((int64_t)g * Qpad + q) * NSL + sl];
+      const uint64_t* p = keys + ((int64_t)g * Qpad + q) * cap + sl * (cap / NSL);
       for (uint32_t j = 0; j < n; ++j) f(p[j]);
     }
   }
@@ -185,6 +267,10 @@ struct ListSource {  // merge input: [P][Q][kin] scores + global idx (-1 = empty
   int P;
   int Q;
   int kin;
+  static constexpr bool kRegions = false;
+  __device__ __forceinline__ int nregions() const { return 0; }
+  __device__ __forceinline__ uint32_t count(int, int) const { return 0; }
+  __device__ __forceinline__ const uint64_t* region(int, int) const { return nullptr; }
   template <class F>
   __device__ __forceinline__ void for_each(int q, int tid, int nt, F&& f) const {
     const int64_t M = (int64_t)P * kin;
@@ -200,9 +286,17 @@ struct ListSource {  // merge input: [P][Q][kin] scores + global idx (-1 = empty
 constexpr int SEL_NT = 256;
 constexpr int SEL_NW = SEL_NT / 64;
 constexpr int SEL_MAXK = 1024;
+constexpr int SEL_STAGE = 8192;  // candidates staged in LDS when they fit (64 KB)
+constexpr int SEL_MAXR = 2048;   // region table size for the parallel staging path
 
 enum SelMode { SEL_THRESHOLD = 0, SEL_FINAL = 1 };
 
+// One workgroup per query.  Exact radix select (8-bit digits, MSB first) of the
+// k-th largest distinct key among the query's candidates, then collect + bitonic
+// sort of the winners.  SEL_THRESHOLD only needs a LOWER BOUND of the k-th key
+// (the filter keeps key >= bound), so it stops after the top 16 bits: bound =
+// (16-bit prefix of the k-th key) << 48 -- exact top-k is still guaranteed
+// because the FINAL pass selects exactly among everything >= bound.
 template <class Src>
 __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode,
                                                          uint64_t* __restrict__ thr_out,
@@ -210,49 +304,110 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
                                                          int64_t* __restrict__ out_idx) {
   __shared__ uint32_t hist[SEL_NW][256];
   __shared__ uint64_t cand[SEL_MAXK];
+  __shared__ uint64_t stage[SEL_STAGE];
   __shared__ uint32_t s_misc[4];  // 0: total count, 1: kr, 2: selected digit, 3: collect ctr
+  __shared__ uint32_t roff[SEL_MAXR + 1];
 
   const int q = blockIdx.x;
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
 
-  // total candidate count
   if (tid == 0) {
     s_misc[0] = 0;
     s_misc[3] = 0;
   }
   __syncthreads();
-  {
+  bool table = false;
+  uint32_t M;
+  if constexpr (Src::kRegions) {
+    const int R = src.nregions();
+    table = R <= SEL_MAXR;
+    if (table) {
+      // counts of all regions in parallel, then an exclusive scan (one wave)
+      for (int r = tid; r < R; r += SEL_NT) roff[r + 1] = src.count(q, r);
+      __syncthreads();
+      if (wave == 0) {
+        uint32_t carry = 0;
+        for (int base = 0; base < R; base += 64) {
+          const int r = base + lane;
+          uint32_t v = r < R ? roff[r + 1] : 0;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(v, o, 64);
+            if (lane >= o) v += t;
+          }
+          if (r < R) roff[r + 1] = carry + v;
+          carry += __shfl(v, 63, 64);
+        }
+        if (lane == 0) {
+          roff[0] = 0;
+          s_misc[0] = carry;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (!table) {
     uint32_t c = 0;
     src.for_each(q, tid, SEL_NT, [&](uint64_t) { ++c; });
     atomicAdd(&s_misc[0], c);
+    __syncthreads();
   }
-  __syncthreads();
-  const uint32_t M = s_misc[0];
+  M = s_misc[0];
+  const bool staged = M <= (uint32_t)SEL_STAGE;
+  if (staged) {
+    if (table) {
+      // flat index -> region by binary search: every load independent (high MLP)
+      const int R = src.nregions();
+      for (uint32_t i = tid; i < M; i += SEL_NT) {
+        int lo = 0, hi = R - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (roff[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        stage[i] = src.region(q, lo)[i - roff[lo]];
+      }
+    } else {
+      if (tid == 0) s_misc[3] = 0;
+      __syncthreads();
+      src.for_each(q, tid, SEL_NT, [&](uint64_t key) { stage[atomicAdd(&s_misc[3], 1u)] = key; });
+    }
+    __syncthreads();
+    if (tid == 0) s_misc[3] = 0;
+    __syncthreads();
+  }
+  auto visit = [&](auto&& f) {
+    if (staged) {
+      for (uint32_t i = tid; i < M; i += SEL_NT) f(stage[i]);
+    } else {
+      src.for_each(q, tid, SEL_NT, f);
+    }
+  };
 
   uint64_t kth = 0;  // 0 = keep everything
   if (M > (uint32_t)k) {
     if (tid == 0) s_misc[1] = (uint32_t)k;
     uint64_t prefix = 0, pmask = 0;
-    for (int shift = 56; shift >= 0; shift -= 8) {
+    const int last_shift = (mode == SEL_THRESHOLD) ? 48 : 0;
+    for (int shift = 56; shift >= last_shift; shift -= 8) {
       for (int i = tid; i < SEL_NW * 256; i += SEL_NT) (&hist[0][0])[i] = 0;
       __syncthreads();
-      src.for_each(q, tid, SEL_NT, [&](uint64_t key) {
+      visit([&](uint64_t key) {
         if ((key & pmask) == prefix) atomicAdd(&hist[wave][(key >> shift) & 255], 1u);
       });
       __syncthreads();
       if (wave == 0) {
         // lane covers digits 4*lane .. 4*lane+3; suffix-scan from the top digit.
-        uint32_t b[4];
+        uint32_t bb[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          uint32_t s = 0;
+          uint32_t t = 0;
 #pragma unroll
-          for (int w = 0; w < SEL_NW; ++w) s += hist[w][4 * lane + j];
-          b[j] = s;
+          for (int w = 0; w < SEL_NW; ++w) t += hist[w][4 * lane + j];
+          bb[j] = t;
         }
-        const uint32_t mine = b[0] + b[1] + b[2] + b[3];
+        const uint32_t mine = bb[0] + bb[1] + bb[2] + bb[3];
         uint32_t suf = mine;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -265,11 +420,11 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
           uint32_t acc = above;
           int sel = 4 * lane;
           for (int j = 3; j >= 0; --j) {
-            if (acc + b[j] >= kr) {
+            if (acc + bb[j] >= kr) {
               sel = 4 * lane + j;
               break;
             }
-            acc += b[j];
+            acc += bb[j];
           }
           s_misc[2] = (uint32_t)sel;
           s_misc[1] = kr - acc;
@@ -279,7 +434,7 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
       prefix |= (uint64_t)s_misc[2] << shift;
       pmask |= (uint64_t)0xff << shift;
     }
-    kth = prefix;
+    kth = prefix;  // THRESHOLD: low 48 bits are zero -> a lower bound of the k-th key
   }
 
   if (mode == SEL_THRESHOLD) {
@@ -293,7 +448,7 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
   while (npow < cnt) npow <<= 1;
   for (int i = tid; i < npow; i += SEL_NT) cand[i] = 0;
   __syncthreads();
-  src.for_each(q, tid, SEL_NT, [&](uint64_t key) {
+  visit([&](uint64_t key) {
     if (key >= kth) {
       const uint32_t slot = atomicAdd(&s_misc[3], 1u);
       if (slot < (uint32_t)SEL_MAXK) cand[slot] = key;
@@ -307,10 +462,10 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
         const int j = i ^ stride;
         if (j > i) {
           const bool desc = ((i & size) == 0);
-          const uint64_t a = cand[i], b = cand[j];
-          if (desc ? (a < b) : (a > b)) {
-            cand[i] = b;
-            cand[j] = a;
+          const uint64_t x = cand[i], y = cand[j];
+          if (desc ? (x < y) : (x > y)) {
+            cand[i] = y;
+            cand[j] = x;
           }
         }
       }
@@ -318,21 +473,23 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
     }
   }
   for (int i = tid; i < k; i += SEL_NT) {
-    float s = -__builtin_huge_valf();
+    float sc = -__builtin_huge_valf();
     int64_t id = -1;
     if (i < cnt) {
       const uint64_t key = cand[i];
-      s = unorderable_f32((uint32_t)(key >> 32));
+      sc = unorderable_f32((uint32_t)(key >> 32));
       id = (int64_t)(uint32_t)(~(uint32_t)key);
     }
-    out_score[(int64_t)q * k + i] = s;
+    out_score[(int64_t)q * k + i] = sc;
     out_idx[(int64_t)q * k + i] = id;
   }
 }
 
 // ------------------------------------------------------------------ planning
 struct Plan {
-  int nw;
+  int nw;  // waves = nq * ks
+  int nq;  // 32-query groups per workgroup
+  int ks;  // k-slices (D split across a wave pair)
   int qpad;
   int gy;
   bool two_phase;
@@ -345,30 +502,58 @@ struct Plan {
   size_t off_thr, off_cnt, off_keys, bytes;
 };
 
-static int pick_nw(int64_t D, int64_t Q) {
-  int nw = D <= 256 ? 8 : 4;  // B fragments: D/16 * 4 VGPRs per lane
-  int need = (int)((Q + 31) / 32);
+static int pick_ks(int64_t D) { return D > 512 ? 2 : 1; }  // <= 128 fragment VGPRs/wave
+
+static int pick_nq(int64_t D, int64_t Q) {
+  const int nqmax = 8 / pick_ks(D);
+  const int need = (int)((Q + 31) / 32);
   int p = 1;
-  while (p < need && p < nw) p <<= 1;
-  return p < nw ? p : nw;
+  while (p < need && p < nqmax) p <<= 1;
+  return p;
 }
 
-static void plan_workers(int64_t ntiles, int gy, int* g, int* tpw) {
-  const int64_t target = 256 * 2;  // ~2 waves of workgroups over 256 CUs
+template <int D>
+static size_t tile_lds_bytes() {
+  return (size_t)Geo<D>::NBUF * Geo<D>::TILE_BYTES + Geo<D>::XBUF_BYTES;
+}
+
+static size_t lds_bytes_for(int64_t D) {
+  switch (D) {
+    case 64: return tile_lds_bytes<64>();
+    case 128: return tile_lds_bytes<128>();
+    case 256: return tile_lds_bytes<256>();
+    case 384: return tile_lds_bytes<384>();
+    case 512: return tile_lds_bytes<512>();
+    case 768: return tile_lds_bytes<768>();
+    default: return tile_lds_bytes<1024>();
+  }
+}
+
+// Workers own contiguous tile ranges; the worker count is a multiple of 8 so the
+// XCD-aware block decode in scan_tile_kernel is a bijection.
+static void plan_workers(int64_t ntiles, int gy, int64_t D, int nw, int* g, int* tpw) {
+  int per_cu = (int)(IRC_LDS_BYTES / lds_bytes_for(D));
+  const int by_waves = 16 / nw > 0 ? 16 / nw : 1;  // keep <= 16 waves per CU
+  if (per_cu > by_waves) per_cu = by_waves;
+  if (per_cu < 1) per_cu = 1;
+  const int64_t target = 256LL * per_cu;
   int64_t want = (target + gy - 1) / gy;
   if (want < 1) want = 1;
   if (want > ntiles) want = ntiles > 0 ? ntiles : 1;
   int64_t per = (ntiles + want - 1) / want;
   if (per < 1) per = 1;
   *tpw = (int)per;
-  *g = (int)((ntiles + per - 1) / per);
-  if (*g < 1) *g = 1;
+  int64_t gg = (ntiles + per - 1) / per;
+  gg = (gg + 7) / 8 * 8;
+  *g = (int)gg;
 }
 
 static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k) {
   Plan p{};
-  p.nw = pick_nw(D, Q);
-  const int qb = p.nw * 32;
+  p.ks = pick_ks(D);
+  p.nq = pick_nq(D, Q);
+  p.nw = p.nq * p.ks;
+  const int qb = p.nq * 32;
   p.gy = (int)((Q + qb - 1) / qb);
   if (p.gy < 1) p.gy = 1;
   p.qpad = p.gy * qb;
@@ -378,60 +563,46 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k) {
   if (p.stride < 1) p.stride = 1;
   p.two_phase = p.stride > 1;
   p.S = p.two_phase ? (N + p.stride - 1) / p.stride : N;
-  plan_workers((p.S + TD - 1) / TD, p.gy, &p.g_s, &p.tpw_s);
+  plan_workers((p.S + TD - 1) / TD, p.gy, D, p.nw, &p.g_s, &p.tpw_s);
   p.cap_s = (int64_t)p.tpw_s * TD;
-  plan_workers((N + TD - 1) / TD, p.gy, &p.g_f, &p.tpw_f);
+  plan_workers((N + TD - 1) / TD, p.gy, D, p.nw, &p.g_f, &p.tpw_f);
   p.cap_f = (int64_t)p.tpw_f * TD;
   const int gmax = p.g_s > p.g_f ? p.g_s : p.g_f;
-  int64_t kmax = (int64_t)p.g_s * p.cap_s;
-  if (p.two_phase && (int64_t)p.g_f * p.cap_f > kmax) kmax = (int64_t)p.g_f * p.cap_f;
+  int64_t kmax = (int64_t)p.g_f * p.cap_f;
+  if (p.two_phase && (int64_t)p.g_s * p.cap_s > kmax) kmax = (int64_t)p.g_s * p.cap_s;
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   p.off_thr = 0;
   p.off_cnt = al(p.off_thr + (size_t)p.qpad * 8);
-  p.off_cnt = al(p.off_cnt);
-  p.off_keys = al(p.off_cnt + (size_t)gmax * p.qpad * 4);
+  p.off_keys = al(p.off_cnt + (size_t)gmax * p.qpad * 2 * p.ks * 4);
   p.bytes = al(p.off_keys + (size_t)kmax * p.qpad * 8);
   return p;
 }
 
-template <int D, int NW, int MODE>
-static void launch_tile(const Plan& p, dim3 grid, const unsigned short* qs,
-                        const unsigned short* docs, int Q, int64_t NS, int64_t stride, int tpw,
-                        uint32_t idx_base, const uint64_t* thr, uint64_t* keys, uint32_t* counts,
-                        int64_t cap, float* scores, hipStream_t st) {
-  using G = Geo<D>;
-  const size_t lds = (size_t)G::NBUF * G::TILE_BYTES + NW * 32 * 4;
-  hipLaunchKernelGGL((scan_tile_kernel<D, NW, MODE>), grid, dim3(NW * 64), lds, st, qs, docs, Q,
-                     p.qpad, NS, stride, tpw, idx_base, thr, keys, counts, cap, scores);
+template <int D, int NQ, int MODE>
+static void launch_tile(const Plan& p, int g, const unsigned short* qs, const unsigned short* docs,
+                        int Q, int64_t NS, int64_t stride, int tpw, uint32_t idx_base,
+                        const uint64_t* thr, uint64_t* keys, uint32_t* counts, int64_t cap,
+                        float* scores, hipStream_t st) {
+  const size_t lds = tile_lds_bytes<D>();
+  constexpr int KS = D > 512 ? 2 : 1;
+  static_assert(NQ * KS <= 8 || KS == 1, "wave budget");
+  hipLaunchKernelGGL((scan_tile_kernel<D, NQ, KS, MODE>), dim3(g * p.gy), dim3(NQ * KS * 64), lds, st, qs,
+                     docs, Q, p.qpad, p.gy, (int)NS, (int)stride, tpw, idx_base, thr, keys, counts,
+                     cap, scores);
 }
 
 template <int MODE>
-static int dispatch_tile(int64_t D, const Plan& p, dim3 grid, const unsigned short* qs,
+static int dispatch_tile(int64_t D, const Plan& p, int g, const unsigned short* qs,
                          const unsigned short* docs, int Q, int64_t NS, int64_t stride, int tpw,
                          uint32_t idx_base, const uint64_t* thr, uint64_t* keys, uint32_t* counts,
                          int64_t cap, float* scores, hipStream_t st) {
-#define IRC_SCAN_CASE(DD)                                                                       \
-  case DD:                                                                                      \
-    switch (p.nw) {                                                                             \
-      case 1:                                                                                   \
-        launch_tile<DD, 1, MODE>(p, grid, qs, docs, Q, NS, stride, tpw, idx_base, thr, keys,   \
-                                 counts, cap, scores, st);                                      \
-        break;                                                                                  \
-      case 2:                                                                                   \
-        launch_tile<DD, 2, MODE>(p, grid, qs, docs, Q, NS, stride, tpw, idx_base, thr, keys,   \
-                                 counts, cap, scores, st);                                      \
-        break;                                                                                  \
-      case 4:                                                                                   \
-        launch_tile<DD, 4, MODE>(p, grid, qs, docs, Q, NS, stride, tpw, idx_base, thr, keys,   \
-                                 counts, cap, scores, st);                                      \
-        break;                                                                                  \
-      default:                                                                                  \
-        if (DD <= 256)                                                                          \
-          launch_tile<DD, (DD <= 256 ? 8 : 4), MODE>(p, grid, qs, docs, Q, NS, stride, tpw,     \
-                                                     idx_base, thr, keys, counts, cap, scores,  \
-                                                     st);                                       \
-        break;                                                                                  \
-    }                                                                                           \
+#define IRC_SCAN_ARGS p, g, qs, docs, Q, NS, stride, tpw, idx_base, thr, keys, counts, cap, scores, st
+#define IRC_SCAN_CASE(DD)                                          \
+  case DD:                                                         \
+    if (p.nq == 1) launch_tile<DD, 1, MODE>(IRC_SCAN_ARGS);        \
+    else if (p.nq == 2) launch_tile<DD, 2, MODE>(IRC_SCAN_ARGS);   \
+    else if (p.nq == 4) launch_tile<DD, 4, MODE>(IRC_SCAN_ARGS);   \
+    else launch_tile<DD, (DD > 512 ? 4 : 8), MODE>(IRC_SCAN_ARGS); \
     break;
   switch (D) {
     IRC_SCAN_CASE(64)
@@ -447,6 +618,7 @@ static int dispatch_tile(int64_t D, const Plan& p, dim3 grid, const unsigned sho
       return IRC_E_INVALID;
   }
 #undef IRC_SCAN_CASE
+#undef IRC_SCAN_ARGS
   return check_launch("scan_tile_kernel");
 }
 
@@ -476,6 +648,7 @@ extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, i
   IRC_REQUIRE(doc_offset >= 0 && doc_offset + N <= (int64_t)0xFFFFFFFFll,
               "scan_topk: global doc index must fit 32 bits");
   IRC_REQUIRE(Q < (1 << 24), "scan_topk: Q too large");
+  IRC_REQUIRE(N < (1ll << 31) - 64, "scan_topk: shard too large (N < 2^31)");
   hipStream_t st = as_stream(stream);
   if (Q == 0) return IRC_OK;
   if (N == 0) {
@@ -499,20 +672,20 @@ extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, i
   const uint32_t base = (uint32_t)doc_offset;
   int rc;
   if (p.two_phase) {
-    rc = dispatch_tile<KEYS>(D, p, dim3(p.g_s, p.gy), qs, ds, (int)Q, p.S, p.stride, p.tpw_s,
+    rc = dispatch_tile<KEYS>(D, p, p.g_s, qs, ds, (int)Q, p.S, p.stride, p.tpw_s,
                              base, nullptr, keys, cnt, p.cap_s, nullptr, st);
     if (rc) return rc;
-    RegionSource s1{keys, cnt, p.g_s, p.qpad, p.cap_s};
+    RegionSource s1{keys, cnt, p.g_s, p.qpad, p.cap_s, 2 * p.ks};
     hipLaunchKernelGGL((select_kernel<RegionSource>), dim3(Q), dim3(SEL_NT), 0, st, s1, (int)k,
                        (int)SEL_THRESHOLD, thr, nullptr, nullptr);
     if ((rc = check_launch("select_kernel(threshold)"))) return rc;
   }
   prof_begin(st);
-  rc = dispatch_tile<KEYS>(D, p, dim3(p.g_f, p.gy), qs, ds, (int)Q, N, 1, p.tpw_f, base,
+  rc = dispatch_tile<KEYS>(D, p, p.g_f, qs, ds, (int)Q, N, 1, p.tpw_f, base,
                            p.two_phase ? thr : nullptr, keys, cnt, p.cap_f, nullptr, st);
   prof_end("scan_filter", st);
   if (rc) return rc;
-  RegionSource s2{keys, cnt, p.g_f, p.qpad, p.cap_f};
+  RegionSource s2{keys, cnt, p.g_f, p.qpad, p.cap_f, 2 * p.ks};
   hipLaunchKernelGGL((select_kernel<RegionSource>), dim3(Q), dim3(SEL_NT), 0, st, s2, (int)k,
                      (int)SEL_FINAL, nullptr, out_score, out_idx);
   return check_launch("select_kernel(final)");
@@ -536,7 +709,7 @@ extern "C" int irc_scan_scores(const void* queries, const void* docs, int64_t Q,
   IRC_REQUIRE(supported_d(D), "scan_scores: unsupported D=%lld", (long long)D);
   if (Q == 0 || N == 0) return IRC_OK;
   Plan p = make_plan(Q, N, D, 1);
-  return dispatch_tile<SCORES>(D, p, dim3(p.g_f, p.gy), static_cast<const unsigned short*>(queries),
+  return dispatch_tile<SCORES>(D, p, p.g_f, static_cast<const unsigned short*>(queries),
                                static_cast<const unsigned short*>(docs), (int)Q, N, 1, p.tpw_f, 0,
                                nullptr, nullptr, nullptr, 0, out, as_stream(stream));
 }
