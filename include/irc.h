@@ -66,6 +66,83 @@ int irc_topk_merge(const float* in_score, const int64_t* in_idx, int64_t P, int6
 int irc_scan_scores(const void* queries, const void* docs, int64_t Q, int64_t N, int64_t D,
                     float* out, irc_stream_t stream);
 
+/* ---------------------------------------------------------------- GEMM
+ * C[M,N] (=|+=) alpha * op(A) . op(B) (+bias[N]) (->GELU) (+R[M,N]), batched.
+ * Replaces the cuBLAS GEMMs behind nn.Linear / torch.matmul on the path: BERT
+ * QKV/out/FFN (contrastive_module.py:39 -> HF modeling_bert), the LSTM
+ * projections and the head Linear (src/model.py:16-26, 39-40), and the InfoNCE
+ * logits (contrastive_loss.py:61-62, 79).
+ * in_dtype/out_dtype: 0 = bf16, 1 = fp32 (fp32 inputs use the exact f32 MFMA).
+ * a_layout: 0 = A is [M][K], 1 = A is [K][M];  b_layout: 0 = B is [N][K]
+ * (nn.Linear weight), 1 = B is [K][N].  epilogue: 0 none, 1 +bias, 2 +bias->GELU(erf),
+ * 3 +bias+R, 4 +R.  accumulate (fp32 C only): C += result. */
+int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue, int64_t M,
+             int64_t N, int64_t K, float alpha, const void* A, int64_t lda, int64_t strideA,
+             const void* B, int64_t ldb, int64_t strideB, const float* bias, int64_t strideBias,
+             const void* R, int64_t ldr, int64_t strideR, void* C, int64_t ldc, int64_t strideC,
+             int accumulate, int64_t batch, irc_stream_t stream);
+
+/* ------------------------------------------------------------- BERT encoder
+ * Frozen BERT forward pieces (contrastive_module.py:36-41 -> HF BertModel):
+ * fused embedding gather + LayerNorm, LayerNorm (residual fused in the GEMM),
+ * masked multi-head self-attention over the fused [B*L, 3H] QKV projection.
+ * dtype: 0 = bf16 activations/tables, 1 = fp32.  gamma/beta fp32. */
+int irc_embed_ln(int dtype, const int64_t* ids, const void* word, const void* pos,
+                 const void* type0, const float* gamma, const float* beta, void* y, int64_t rows,
+                 int64_t L, int64_t H, float eps, irc_stream_t stream);
+int irc_layernorm(int dtype, const void* x, void* y, const float* gamma, const float* beta,
+                  int64_t rows, int64_t H, float eps, irc_stream_t stream);
+int irc_attention(int dtype, const void* qkv, const int64_t* mask, void* ctx, int64_t B,
+                  int64_t L, int64_t H, int64_t heads, irc_stream_t stream);
+
+/* --------------------------------------------------------------- BiLSTM head
+ * nn.LSTM recurrences (src/model.py:16-22, 39), gate order i,f,g,o, zero state,
+ * padded sequences processed as is.  xp = x W_ih^T + b_ih + b_hh comes from
+ * irc_gemm.  dtype: type of W_hh / h (0 bf16, 1 fp32); state math is fp32.
+ * lstm_fwd saves activated gates, c and the consumed h_{t-1} for BPTT (any of
+ * gsave/csave/hprev may be NULL for the no-grad momentum encoder);
+ * lstm_bwd turns dL/dh (dy) into dL/d(gate pre-activations). */
+int irc_lstm_fwd(int dtype, const float* xp, const void* whh, void* hout, float* gsave,
+                 float* csave, void* hprev, int64_t B, int64_t L, int64_t H, int64_t ndir,
+                 irc_stream_t stream);
+int irc_lstm_bwd(int dtype, const float* dy, const void* whh, const float* gsave,
+                 const float* csave, float* dgates, int64_t B, int64_t L, int64_t H,
+                 int64_t ndir, irc_stream_t stream);
+
+/* ------------------------------------------------- seq2vec tail + InfoNCE + optimizer
+ * seq2vec mean-over-L (PAD included) + F.normalize (contrastive_module.py:102-112);
+ * InfoNCE row log-sum-exp / NLL and softmax gradients (contrastive_loss.py:56-93,
+ * the k-rows reuse q's queue logits); deterministic sums; clip_grad_norm_ +
+ * Adam (train.py:155-165, model.py:52-57); momentum update and enqueue
+ * (contrastive_module.py:43-68); casts and column sums for bias gradients. */
+int irc_mean_rows(int dtype, const void* x, float* out, int64_t B, int64_t L, int64_t C,
+                  int64_t ldx, irc_stream_t stream);
+int irc_bcast_rows(const float* g, float* y, int64_t B, int64_t L, int64_t C, float scale,
+                   irc_stream_t stream);
+int irc_l2norm_fwd(const float* x, float* y, float* nrm, int64_t B, int64_t D, float eps,
+                   irc_stream_t stream);
+int irc_l2norm_bwd(const float* dy, const float* y, const float* nrm, float* dx, int64_t B,
+                   int64_t D, float eps, irc_stream_t stream);
+int irc_nce_lse(const float* S, const float* LQ, int64_t N, int64_t K, float T, float* lse,
+                float* loss_row, irc_stream_t stream);
+int irc_nce_grads(const float* S, const float* LQ, const float* lse, int64_t N, int64_t K,
+                  float T, const float* gscale, float* GS, float* GQ, irc_stream_t stream);
+int irc_sum(const float* x, int64_t n, float scale, float* partial, float* out,
+            irc_stream_t stream);
+int irc_grad_norm_clip(const float* g, int64_t n, float max_norm, float* partial, float* out,
+                       irc_stream_t stream);
+int irc_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* coef,
+                  float b1, float b2, float step_size, float bc2_sqrt, float eps,
+                  irc_stream_t stream);
+int irc_momentum_update(float* pk, const float* pq, int64_t n, float mom, irc_stream_t stream);
+int irc_enqueue(float* queue, const float* keys, int64_t* ptr, int64_t D, int64_t K, int64_t B,
+                irc_stream_t stream);
+int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t stream);
+int irc_axpby(float* out, const float* x, const float* y, float a, float b, int64_t n,
+              irc_stream_t stream);
+int irc_colsum(const float* x, float* out, int64_t R, int64_t C, int64_t ldx, int accumulate,
+               float* partial, irc_stream_t stream);
+
 /* ------------------------------------------------------------------ profiling
  * HIP-event timing of the dominant kernel of each entry point, recorded on the
  * caller's stream (bench.py's roofline "achieved" figure).  Names: "scan_filter". */

@@ -1,0 +1,349 @@
+// General MFMA GEMM for gfx950 with fused epilogues.
+//
+//   C[M, N] (=|+=) alpha * op(A)[M, K] . op(B)[K, N]  (+ bias[N]) (-> GELU) (+ R[M, N])
+//
+// Replaces the cuBLAS GEMMs the reference reaches through nn.Linear /
+// torch.matmul: BERT QKV / out-proj / FFN (HF modeling_bert, called from
+// src/contrastor/contrastive_module.py:39), the LSTM input projections and their
+// backward products (src/model.py:16-26, 39-40), the BiLSTM head's Linear
+// 512->128, and the InfoNCE logits (src/contrastor/contrastive_loss.py:61-62,79).
+//
+// Operand layouts (all row-major in memory):
+//   A: ROW = [M][K] (lda)            COL = [K][M] (lda)
+//   B: NK  = [N][K] (ldb, nn.Linear) KN  = [K][N] (ldb)
+// Input types: bf16 (v_mfma_f32_32x32x16_bf16, fp32 accumulate) or fp32
+// (v_mfma_f32_32x32x2_f32: exact fp32 products, the parity mode).
+//
+// Structure: 128x128 block tile, 4 waves (2x2) of 64x64, BK k-slab staged
+// global -> registers -> LDS (double buffered; the next slab's global loads are
+// issued before the current slab's MFMAs).  LDS rows are padded by 16 B so the
+// row-wise ds_read_b128 fragment reads are conflict free.  K-major (ROW / NK)
+// slabs move as 16-byte vectors; the transposed layouts (COL / KN) are loaded
+// along M/N and scattered into the [row][k] LDS image.  Blocks are remapped so
+// each XCD walks a contiguous band of output tiles (neighbours share A/B panels
+// in that XCD's L2).
+#include "irc_common.h"
+
+namespace irc {
+namespace gemm {
+
+enum Layout { ROW = 0, COL = 1 };  // A: ROW=[M][K], COL=[K][M]; B: ROW=[N][K] (NK), COL=[K][N] (KN)
+enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RESID = 3, EPI_RESID = 4 };
+
+constexpr int BM = 128, BN = 128, NT = 256;
+
+template <typename T>
+struct TT;
+template <>
+struct TT<unsigned short> {  // bf16
+  static constexpr int BK = 32;
+  static constexpr int VEC = 8;  // elements per 16-byte vector
+  static constexpr int PITCH = BK * 2 + 16;  // bytes per LDS row (64 + 16 pad)
+};
+template <>
+struct TT<float> {
+  static constexpr int BK = 16;
+  static constexpr int VEC = 4;
+  static constexpr int PITCH = BK * 4 + 16;  // 64 + 16 pad
+};
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+struct Args {
+  const void* A;
+  const void* B;
+  void* C;
+  const float* bias;
+  const void* R;  // residual, same type/ld as C
+  int M, N, K;
+  int64_t lda, ldb, ldc, ldr;
+  int64_t sA, sB, sC, sR, sBias;  // batch strides (elements)
+  float alpha;
+  int accumulate;  // C += result (fp32 C only)
+};
+
+// Load one [rows x BK] slab of an operand into registers (as 16-byte vectors).
+// For K-major storage (ROW) each vector = 8 (bf16) / 4 (f32) consecutive k of one
+// row; for transposed storage (COL) each vector = consecutive rows at one k.
+template <typename T, int LAYOUT>
+struct Slab {
+  static constexpr int BK = TT<T>::BK;
+  static constexpr int VEC = TT<T>::VEC;
+  static constexpr int NVEC = (128 * BK) / VEC;  // vectors per slab
+  static constexpr int PER_T = NVEC / NT;
+  u16x8 v[PER_T];
+
+  __device__ __forceinline__ void load(const T* base, int64_t ld, int row0, int nrows, int k0,
+                                       int K) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int e = i * NT + tid;
+      int r, kk;
+      if (LAYOUT == ROW) {
+        r = e / (BK / VEC);
+        kk = (e % (BK / VEC)) * VEC;
+      } else {
+        kk = e / (128 / VEC);
+        r = (e % (128 / VEC)) * VEC;
+      }
+      const int gr = row0 + r, gk = k0 + kk;
+      u16x8 val = (u16x8)0;
+      if (LAYOUT == ROW) {
+        if (gr < nrows && gk + VEC <= K) {
+          val = *reinterpret_cast<const u16x8*>(base + (int64_t)gr * ld + gk);
+        } else if (gr < nrows) {
+          T tmp[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) tmp[j] = (gk + j < K) ? base[(int64_t)gr * ld + gk + j] : T(0);
+          val = *reinterpret_cast<u16x8*>(tmp);
+        }
+      } else {
+        if (gk < K && gr + VEC <= nrows) {
+          val = *reinterpret_cast<const u16x8*>(base + (int64_t)gk * ld + gr);
+        } else if (gk < K) {
+          T tmp[VEC];
+#pragma unroll
+          for (int j = 0; j < VEC; ++j)
+            tmp[j] = (gr + j < nrows) ? base[(int64_t)gk * ld + gr + j] : T(0);
+          val = *reinterpret_cast<u16x8*>(tmp);
+        }
+      }
+      v[i] = val;
+    }
+  }
+
+  __device__ __forceinline__ void store(char* lds) const {
+    const int tid = threadIdx.x;
+    constexpr int PITCH = TT<T>::PITCH;
+#pragma unroll
+    for (int i = 0; i < PER_T; ++i) {
+      const int e = i * NT + tid;
+      if (LAYOUT == ROW) {
+        const int r = e / (BK / VEC);
+        const int kk = (e % (BK / VEC)) * VEC;
+        *reinterpret_cast<u16x8*>(lds + r * PITCH + kk * (int)sizeof(T)) = v[i];
+      } else {
+        const int kk = e / (128 / VEC);
+        const int r = (e % (128 / VEC)) * VEC;
+        const T* t = reinterpret_cast<const T*>(&v[i]);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+          *reinterpret_cast<T*>(lds + (r + j) * PITCH + kk * (int)sizeof(T)) = t[j];
+      }
+    }
+  }
+};
+
+template <typename TI, typename TO, int LA, int LB, int EPI>
+__global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
+  constexpr int BK = TT<TI>::BK;
+  constexpr int PITCH = TT<TI>::PITCH;
+  constexpr int SLAB = 128 * PITCH;
+  __shared__ __attribute__((aligned(16))) char lds[2][2][SLAB];  // [buf][A/B]
+
+  const int tiles_m = (g.M + BM - 1) / BM;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  // XCD-aware bijective remap of the linear block id (blocks b and b+8 share an XCD)
+  int bid = blockIdx.x;
+  {
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int batch = blockIdx.y;
+  const TI* A = reinterpret_cast<const TI*>(g.A) + batch * g.sA;
+  const TI* B = reinterpret_cast<const TI*>(g.B) + batch * g.sB;
+  TO* C = reinterpret_cast<TO*>(g.C) + batch * g.sC;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, r32 = lane & 31;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16)0.0f;
+
+  Slab<TI, LA> sa;
+  Slab<TI, LB> sb;
+  const int nk = (g.K + BK - 1) / BK;
+  sa.load(A, g.lda, m0, g.M, 0, g.K);
+  sb.load(B, g.ldb, n0, g.N, 0, g.K);
+  sa.store(lds[0][0]);
+  sb.store(lds[0][1]);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      sa.load(A, g.lda, m0, g.M, (kt + 1) * BK, g.K);
+      sb.load(B, g.ldb, n0, g.N, (kt + 1) * BK, g.K);
+    }
+    const char* la = lds[cur][0];
+    const char* lb = lds[cur][1];
+    if constexpr (sizeof(TI) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bf16x8 fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = wm * 64 + i * 32 + r32;
+          fa[i] = *reinterpret_cast<const bf16x8*>(la + row * PITCH + (ks * 16 + 8 * h) * 2);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = wn * 64 + j * 32 + r32;
+          fb[j] = *reinterpret_cast<const bf16x8*>(lb + row * PITCH + (ks * 16 + 8 * h) * 2);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // fp32: lane half h owns k = 8h .. 8h+7 of the 16-deep slab (same k pairing
+      // for A and B), read as two 16-byte vectors; 8 MFMAs of K=2 (one k-slot per half).
+      f32x4 fa[2][2], fb[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 32 + r32;
+        fa[i][0] = *reinterpret_cast<const f32x4*>(la + row * PITCH + (8 * h) * 4);
+        fa[i][1] = *reinterpret_cast<const f32x4*>(la + row * PITCH + (8 * h + 4) * 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wn * 64 + j * 32 + r32;
+        fb[j][0] = *reinterpret_cast<const f32x4*>(lb + row * PITCH + (8 * h) * 4);
+        fb[j][1] = *reinterpret_cast<const f32x4*>(lb + row * PITCH + (8 * h + 4) * 4);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][kk >> 2][kk & 3],
+                                                             fb[j][kk >> 2][kk & 3], acc[i][j],
+                                                             0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      __syncthreads();  // everyone done reading the other buffer
+      sa.store(lds[cur ^ 1][0]);
+      sb.store(lds[cur ^ 1][1]);
+      __syncthreads();
+    }
+  }
+
+  // Epilogue: acc[i][j] reg e -> row = m0 + wm*64 + i*32 + (e&3) + 8(e>>2) + 4h,
+  //                              col = n0 + wn*64 + j*32 + r32.
+  const float* bias = g.bias ? g.bias + batch * g.sBias : nullptr;
+  const TO* R = g.R ? reinterpret_cast<const TO*>(g.R) + batch * g.sR : nullptr;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 64 + j * 32 + r32;
+    if (col >= g.N) continue;
+    const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESID) ? bias[col]
+                                                                                        : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row >= g.M) continue;
+        float v = acc[i][j][e] * g.alpha + bv;
+        if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+        if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
+          if constexpr (sizeof(TO) == 2)
+            v += bf16_to_f32(reinterpret_cast<const unsigned short*>(R)[(int64_t)row * g.ldr + col]);
+          else
+            v += reinterpret_cast<const float*>(R)[(int64_t)row * g.ldr + col];
+        }
+        TO* dst = C + (int64_t)row * g.ldc + col;
+        if constexpr (sizeof(TO) == 2) {
+          *reinterpret_cast<unsigned short*>(dst) = f32_to_bf16(v);
+        } else {
+          if (g.accumulate)
+            *reinterpret_cast<float*>(dst) += v;
+          else
+            *reinterpret_cast<float*>(dst) = v;
+        }
+      }
+    }
+  }
+}
+
+template <typename TI, typename TO, int LA, int LB, int EPI>
+static int launch(const Args& g, int batch, hipStream_t st) {
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_kernel<TI, TO, LA, LB, EPI>), dim3(tiles, batch), dim3(NT), 0, st, g);
+  return check_launch("gemm_kernel");
+}
+
+template <typename TI, typename TO, int LA, int LB>
+static int by_epi(int epi, const Args& g, int batch, hipStream_t st) {
+  switch (epi) {
+    case EPI_NONE: return launch<TI, TO, LA, LB, EPI_NONE>(g, batch, st);
+    case EPI_BIAS: return launch<TI, TO, LA, LB, EPI_BIAS>(g, batch, st);
+    case EPI_BIAS_GELU: return launch<TI, TO, LA, LB, EPI_BIAS_GELU>(g, batch, st);
+    case EPI_BIAS_RESID: return launch<TI, TO, LA, LB, EPI_BIAS_RESID>(g, batch, st);
+    case EPI_RESID: return launch<TI, TO, LA, LB, EPI_RESID>(g, batch, st);
+  }
+  set_error("gemm: bad epilogue %d", epi);
+  return IRC_E_INVALID;
+}
+
+template <typename TI, typename TO>
+static int by_layout(int la, int lb, int epi, const Args& g, int batch, hipStream_t st) {
+  if (la == ROW && lb == ROW) return by_epi<TI, TO, ROW, ROW>(epi, g, batch, st);
+  if (la == ROW && lb == COL) return by_epi<TI, TO, ROW, COL>(epi, g, batch, st);
+  if (la == COL && lb == ROW) return by_epi<TI, TO, COL, ROW>(epi, g, batch, st);
+  return by_epi<TI, TO, COL, COL>(epi, g, batch, st);
+}
+
+}  // namespace gemm
+}  // namespace irc
+
+using namespace irc;
+
+// dtype codes: 0 = bf16, 1 = fp32
+extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue,
+                        int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
+                        int64_t strideA, const void* B, int64_t ldb, int64_t strideB,
+                        const float* bias, int64_t strideBias, const void* R, int64_t ldr,
+                        int64_t strideR, void* C, int64_t ldc, int64_t strideC, int accumulate,
+                        int64_t batch, irc_stream_t stream) {
+  IRC_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: bad sizes");
+  IRC_REQUIRE(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31), "gemm: size too large");
+  IRC_REQUIRE(in_dtype == 0 || in_dtype == 1, "gemm: in_dtype must be 0 (bf16) or 1 (fp32)");
+  IRC_REQUIRE(out_dtype == 0 || out_dtype == 1, "gemm: out_dtype must be 0 (bf16) or 1 (fp32)");
+  IRC_REQUIRE(!(accumulate && out_dtype == 0), "gemm: accumulate needs fp32 C");
+  IRC_REQUIRE(epilogue >= 0 && epilogue <= 4, "gemm: bad epilogue");
+  IRC_REQUIRE(!(epilogue >= 1 && epilogue <= 3) || bias, "gemm: epilogue needs bias");
+  IRC_REQUIRE(!(epilogue == 3 || epilogue == 4) || R, "gemm: epilogue needs residual");
+  const int vec = in_dtype == 0 ? 8 : 4;
+  IRC_REQUIRE((a_layout == 0 ? lda : lda) % vec == 0 && ldb % vec == 0,
+              "gemm: leading dimensions must be multiples of %d elements", vec);
+  IRC_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0,
+              "gemm: A and B must be 16-byte aligned");
+  if (M == 0 || N == 0) return IRC_OK;
+  gemm::Args g{A, B, C, bias, R, (int)M, (int)N, (int)K, lda, ldb, ldc, ldr,
+               strideA, strideB, strideC, strideR, strideBias, alpha, accumulate};
+  hipStream_t st = as_stream(stream);
+  if (in_dtype == 0 && out_dtype == 0)
+    return gemm::by_layout<unsigned short, unsigned short>(a_layout, b_layout, epilogue, g,
+                                                           (int)batch, st);
+  if (in_dtype == 0 && out_dtype == 1)
+    return gemm::by_layout<unsigned short, float>(a_layout, b_layout, epilogue, g, (int)batch, st);
+  if (in_dtype == 1 && out_dtype == 1)
+    return gemm::by_layout<float, float>(a_layout, b_layout, epilogue, g, (int)batch, st);
+  set_error("gemm: fp32 inputs with bf16 output is not supported");
+  return IRC_E_INVALID;
+}

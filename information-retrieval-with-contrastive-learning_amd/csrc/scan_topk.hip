@@ -297,6 +297,28 @@ enum SelMode { SEL_THRESHOLD = 0, SEL_FINAL = 1 };
 // (the filter keeps key >= bound), so it stops after the top 16 bits: bound =
 // (16-bit prefix of the k-th key) << 48 -- exact top-k is still guaranteed
 // because the FINAL pass selects exactly among everything >= bound.
+//
+// Fast path (region sources with <= SEL_STAGE candidates): counts of all
+// regions -> exclusive scan -> an LDS region-id map -> every candidate load is
+// independent (no dependent search per element) -> keys staged in LDS; the
+// radix passes start at the first bit where min and max key differ.
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t t = __shfl_xor(v, o, 64);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+
 template <class Src>
 __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode,
                                                          uint64_t* __restrict__ thr_out,
@@ -305,8 +327,10 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
   __shared__ uint32_t hist[SEL_NW][256];
   __shared__ uint64_t cand[SEL_MAXK];
   __shared__ uint64_t stage[SEL_STAGE];
-  __shared__ uint32_t s_misc[4];  // 0: total count, 1: kr, 2: selected digit, 3: collect ctr
+  __shared__ uint16_t rid[SEL_STAGE];
   __shared__ uint32_t roff[SEL_MAXR + 1];
+  __shared__ uint64_t s_mm[2][SEL_NW];
+  __shared__ uint32_t s_misc[4];  // 0: total count, 1: kr, 2: selected digit, 3: collect ctr
 
   const int q = blockIdx.x;
   const int tid = threadIdx.x;
@@ -319,12 +343,10 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
   }
   __syncthreads();
   bool table = false;
-  uint32_t M;
   if constexpr (Src::kRegions) {
     const int R = src.nregions();
     table = R <= SEL_MAXR;
     if (table) {
-      // counts of all regions in parallel, then an exclusive scan (one wave)
       for (int r = tid; r < R; r += SEL_NT) roff[r + 1] = src.count(q, r);
       __syncthreads();
       if (wave == 0) {
@@ -354,23 +376,32 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
     atomicAdd(&s_misc[0], c);
     __syncthreads();
   }
-  M = s_misc[0];
+  const uint32_t M = s_misc[0];
   const bool staged = M <= (uint32_t)SEL_STAGE;
   if (staged) {
     if (table) {
-      // flat index -> region by binary search: every load independent (high MLP)
       const int R = src.nregions();
-      for (uint32_t i = tid; i < M; i += SEL_NT) {
-        int lo = 0, hi = R - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (roff[mid] <= i) lo = mid; else hi = mid - 1;
+      for (int r = tid; r < R; r += SEL_NT)
+        for (uint32_t j = roff[r]; j < roff[r + 1]; ++j) rid[j] = (uint16_t)r;
+      __syncthreads();
+      constexpr int U = 8;  // independent loads in flight per thread
+      for (uint32_t i0 = tid; i0 < M; i0 += SEL_NT * U) {
+        uint64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t i = i0 + u * SEL_NT;
+          if (i < M) {
+            const int r = rid[i];
+            v[u] = src.region(q, r)[i - roff[r]];
+          }
         }
-        stage[i] = src.region(q, lo)[i - roff[lo]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t i = i0 + u * SEL_NT;
+          if (i < M) stage[i] = v[u];
+        }
       }
     } else {
-      if (tid == 0) s_misc[3] = 0;
-      __syncthreads();
       src.for_each(q, tid, SEL_NT, [&](uint64_t key) { stage[atomicAdd(&s_misc[3], 1u)] = key; });
     }
     __syncthreads();
@@ -387,10 +418,34 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
 
   uint64_t kth = 0;  // 0 = keep everything
   if (M > (uint32_t)k) {
-    if (tid == 0) s_misc[1] = (uint32_t)k;
-    uint64_t prefix = 0, pmask = 0;
+    // common prefix of all candidates: start the digits at the first differing bit
+    uint64_t mn = ~0ull, mx = 0;
+    visit([&](uint64_t key) {
+      mn = key < mn ? key : mn;
+      mx = key > mx ? key : mx;
+    });
+    mn = wave_min_u64(mn);
+    mx = wave_max_u64(mx);
+    if (lane == 0) {
+      s_mm[0][wave] = mn;
+      s_mm[1][wave] = mx;
+    }
+    __syncthreads();
+    mn = s_mm[0][0];
+    mx = s_mm[1][0];
+#pragma unroll
+    for (int w = 1; w < SEL_NW; ++w) {
+      mn = s_mm[0][w] < mn ? s_mm[0][w] : mn;
+      mx = s_mm[1][w] > mx ? s_mm[1][w] : mx;
+    }
+    const int top = 63 - __builtin_clzll(mn ^ mx | 1ull);  // highest differing bit
+    const int first_shift = (top / 8) * 8;
     const int last_shift = (mode == SEL_THRESHOLD) ? 48 : 0;
-    for (int shift = 56; shift >= last_shift; shift -= 8) {
+    uint64_t pmask = first_shift >= 56 ? 0ull : (~0ull << (first_shift + 8));
+    uint64_t prefix = mn & pmask;
+    if (tid == 0) s_misc[1] = (uint32_t)k;
+    __syncthreads();
+    for (int shift = first_shift; shift >= last_shift; shift -= 8) {
       for (int i = tid; i < SEL_NW * 256; i += SEL_NT) (&hist[0][0])[i] = 0;
       __syncthreads();
       visit([&](uint64_t key) {
@@ -434,7 +489,9 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
       prefix |= (uint64_t)s_misc[2] << shift;
       pmask |= (uint64_t)0xff << shift;
     }
-    kth = prefix;  // THRESHOLD: low 48 bits are zero -> a lower bound of the k-th key
+    // THRESHOLD: bits below 48 of `prefix` are zero unless the candidates share
+    // their top 16 bits; mask them so the bound is the 16-bit prefix << 48.
+    kth = (mode == SEL_THRESHOLD) ? (prefix & (~0ull << 48)) : prefix;
   }
 
   if (mode == SEL_THRESHOLD) {

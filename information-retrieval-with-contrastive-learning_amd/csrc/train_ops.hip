@@ -1,0 +1,418 @@
+// Training-step kernels other than GEMM / encoder / LSTM (gfx950):
+//  * seq2vec tail (src/contrastor/contrastive_module.py:102-112): mean over ALL L
+//    positions (PAD included) and F.normalize (L2, eps 1e-12), forward + backward.
+//  * InfoNCE row pass (src/contrastor/contrastive_loss.py:56-93): per row of the
+//    [2N, 2N] in-batch logits (+ the q.queue logits, REUSED for rows N..2N-1 as
+//    the reference's .repeat(2, 1) does) the log-sum-exp and NLL of the positive
+//    column (i+N) mod 2N, then the softmax gradients G = 1/2 (P - onehot) / T.
+//    The two logit GEMMs and the dq GEMMs run on gemm.hip in fp32-MFMA mode.
+//  * deterministic reductions (fixed assignment + fixed-order final sum).
+//  * clip_grad_norm_(1.0) + torch.optim.Adam step fused over the flat fp32
+//    parameter buffer (src/train.py:155-165, src/model.py:52-57), momentum update
+//    theta_k = m theta_k + (1-m) theta_q (contrastive_module.py:43-53) and the
+//    queue enqueue with its device-side pointer (contrastive_module.py:55-68).
+#include "irc_common.h"
+
+namespace irc {
+namespace tops {
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, int64_t i) {
+  if constexpr (sizeof(T) == 2)
+    return bf16_to_f32(reinterpret_cast<const unsigned short*>(p)[i]);
+  else
+    return reinterpret_cast<const float*>(p)[i];
+}
+
+// out[b, c] = mean_l x[b, l, c]  (fp32 accumulate in l order)
+template <typename T>
+__global__ void mean_rows_kernel(const T* __restrict__ x, float* __restrict__ out, int B, int L,
+                                 int C, int64_t ldx) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)B * C) return;
+  const int b = (int)(e / C), c = (int)(e % C);
+  float s = 0.f;
+  for (int l = 0; l < L; ++l) s += ldf(x, ((int64_t)b * L + l) * ldx + c);
+  out[e] = s / (float)L;
+}
+
+// y[b, l, c] = g[b, c] * scale  (broadcast of d(mean) over positions)
+__global__ void bcast_rows_kernel(const float* __restrict__ g, float* __restrict__ y, int B, int L,
+                                  int C, float scale) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)B * L * C) return;
+  const int c = (int)(e % C);
+  const int b = (int)(e / ((int64_t)L * C));
+  y[e] = g[(int64_t)b * C + c] * scale;
+}
+
+// one wave per row: y = x / max(||x||, eps); nrm[b] = ||x||
+__global__ void l2norm_fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                  float* __restrict__ nrm, int B, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const float v = x[(int64_t)b * D + c];
+    s += v * v;
+  }
+  const float n = sqrtf(warp_sum(s));
+  const float inv = 1.f / fmaxf(n, eps);
+  for (int c = lane; c < D; c += 64) y[(int64_t)b * D + c] = x[(int64_t)b * D + c] * inv;
+  if (lane == 0 && nrm) nrm[b] = n;
+}
+
+// dx = (dy - e (dy . e)) / n  for n > eps (e = y), else dy / eps
+__global__ void l2norm_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                  const float* __restrict__ nrm, float* __restrict__ dx, int B,
+                                  int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float n = nrm[b];
+  if (n <= eps) {
+    for (int c = lane; c < D; c += 64) dx[(int64_t)b * D + c] = dy[(int64_t)b * D + c] / eps;
+    return;
+  }
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) s += dy[(int64_t)b * D + c] * y[(int64_t)b * D + c];
+  const float dot = warp_sum(s);
+  for (int c = lane; c < D; c += 64)
+    dx[(int64_t)b * D + c] = (dy[(int64_t)b * D + c] - y[(int64_t)b * D + c] * dot) / n;
+}
+
+// ---- InfoNCE ----
+// S [2N, 2N] (ld 2N), LQ [N, K] (ld K) or K == 0.  One workgroup per row i.
+__global__ __launch_bounds__(256) void nce_lse_kernel(const float* __restrict__ S,
+                                                      const float* __restrict__ LQ, int N, int K,
+                                                      float invT, float* __restrict__ lse,
+                                                      float* __restrict__ loss_row) {
+  __shared__ float red[4];
+  const int i = blockIdx.x;
+  const int n2 = 2 * N;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* srow = S + (int64_t)i * n2;
+  const float* qrow = K > 0 ? LQ + (int64_t)(i % N) * K : nullptr;
+  float m = -INFINITY;
+  for (int j = tid; j < n2; j += 256)
+    if (j != i) m = fmaxf(m, srow[j] * invT);
+  for (int j = tid; j < K; j += 256) m = fmaxf(m, qrow[j] * invT);
+  m = warp_max(m);
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float s = 0.f;
+  for (int j = tid; j < n2; j += 256)
+    if (j != i) s += __expf(srow[j] * invT - m);
+  for (int j = tid; j < K; j += 256) s += __expf(qrow[j] * invT - m);
+  s = warp_sum(s);
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  if (tid == 0) {
+    const float tot = (red[0] + red[1]) + (red[2] + red[3]);
+    const float l = m + logf(tot);
+    lse[i] = l;
+    const int p = (i + N) % n2;
+    loss_row[i] = l - srow[p] * invT;
+  }
+}
+
+// GS[i][j] = 0.5/T (exp(S_ij/T - lse_i) - [j == p_i]), GS[i][i] = 0, times the
+// upstream gradient *gscale (read on device: no host sync for loss / acml).
+__global__ void nce_grad_s_kernel(const float* __restrict__ S, const float* __restrict__ lse,
+                                  float* __restrict__ GS, int N, float invT, float scale0,
+                                  const float* __restrict__ gscale) {
+  const int n2 = 2 * N;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n2 * n2) return;
+  const float scale = gscale ? scale0 * gscale[0] : scale0;
+  const int i = (int)(e / n2), j = (int)(e % n2);
+  float g = 0.f;
+  if (j != i) {
+    g = __expf(S[e] * invT - lse[i]);
+    if (j == (i + N) % n2) g -= 1.f;
+  }
+  GS[e] = g * scale;
+}
+
+// GQ[n][m] = 0.5/T (exp(LQ/T - lse_n) + exp(LQ/T - lse_{n+N}))
+__global__ void nce_grad_q_kernel(const float* __restrict__ LQ, const float* __restrict__ lse,
+                                  float* __restrict__ GQ, int N, int K, float invT, float scale0,
+                                  const float* __restrict__ gscale) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)N * K) return;
+  const float scale = gscale ? scale0 * gscale[0] : scale0;
+  const int n = (int)(e / K);
+  const float z = LQ[e] * invT;
+  GQ[e] = (__expf(z - lse[n]) + __expf(z - lse[n + N])) * scale;
+}
+
+// ---- deterministic reductions ----
+constexpr int RED_NT = 256;
+// partial[blk] = sum over a fixed contiguous range of (scale * x)^p, p in {1, 2}
+template <int POW>
+__global__ __launch_bounds__(RED_NT) void partial_sum_kernel(const float* __restrict__ x, int64_t n,
+                                                             int64_t per_blk,
+                                                             float* __restrict__ partial) {
+  __shared__ float red[RED_NT / 64];
+  const int64_t lo = (int64_t)blockIdx.x * per_blk;
+  int64_t hi = lo + per_blk;
+  if (hi > n) hi = n;
+  float s = 0.f;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += RED_NT) {
+    const float v = x[i];
+    s += POW == 2 ? v * v : v;
+  }
+  s = warp_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < RED_NT / 64; ++w) t += red[w];
+    partial[blockIdx.x] = t;
+  }
+}
+
+// out[0] = scale * sum(partial) in fixed order; for the clip variant also
+// out[1] = min(1, max_norm / (sqrt(sum) + 1e-6)) and out[0] = sqrt(sum).
+__global__ void finalize_kernel(const float* __restrict__ partial, int np, float scale,
+                                float max_norm, int clip, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;  // fixed order, wide accumulator
+  for (int i = 0; i < np; ++i) s += (double)partial[i];
+  if (clip) {
+    const float nrm = (float)sqrt(s);
+    out[0] = nrm;
+    const float coef = max_norm / (nrm + 1e-6f);
+    out[1] = coef < 1.f ? coef : 1.f;
+  } else {
+    out[0] = (float)(s * (double)scale);
+  }
+}
+
+// Adam (torch.optim.Adam, weight_decay 0, amsgrad False) with the clip coefficient
+// applied to the gradient: g' = g * coef[1].
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                            float* __restrict__ m, float* __restrict__ v, int64_t n,
+                            const float* __restrict__ coef, float b1, float b2, float step_size,
+                            float bc2_sqrt, float eps) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float c = coef ? coef[1] : 1.f;
+  const float gi = g[i] * c;
+  const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // lerp, as torch
+  const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] = p[i] - step_size * (mi / denom);
+}
+
+__global__ void momentum_kernel(float* __restrict__ pk, const float* __restrict__ pq, int64_t n,
+                                float mom) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) pk[i] = pk[i] * mom + pq[i] * (1.f - mom);
+}
+
+// queue[d, ptr + b] = keys[b, d]
+__global__ void enqueue_kernel(float* __restrict__ queue, const float* __restrict__ keys,
+                               const int64_t* __restrict__ ptr, int D, int K, int B) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)D * B) return;
+  const int d = (int)(e / B), b = (int)(e % B);
+  queue[(int64_t)d * K + ptr[0] + b] = keys[(int64_t)b * D + d];
+}
+
+__global__ void ptr_advance_kernel(int64_t* ptr, int B, int K) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) ptr[0] = (ptr[0] + B) % K;
+}
+
+__global__ void axpby_kernel(float* __restrict__ out, const float* __restrict__ x,
+                             const float* __restrict__ y, float a, float b, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = a * x[i] + b * y[i];
+}
+
+__global__ void cast_bf16_kernel(const float* __restrict__ x, unsigned short* __restrict__ y,
+                                 int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = f32_to_bf16(x[i]);
+}
+
+// Column sums in two deterministic passes: partial[chunk][c] over a fixed row
+// chunk (grid.y), then out[c] (+)= sum over chunks in order.
+constexpr int COLSUM_ROWS = 256;
+__global__ void colsum_partial_kernel(const float* __restrict__ x, float* __restrict__ partial,
+                                      int64_t R, int C, int64_t ldx) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS;
+  int64_t r1 = r0 + COLSUM_ROWS;
+  if (r1 > R) r1 = R;
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += x[r * ldx + c];
+  partial[(int64_t)blockIdx.y * C + c] = s;
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ partial, float* __restrict__ out,
+                                    int nchunks, int C, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int k = 0; k < nchunks; ++k) s += partial[(int64_t)k * C + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+}  // namespace tops
+}  // namespace irc
+
+using namespace irc;
+using namespace irc::tops;
+
+static inline unsigned nblk(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
+
+extern "C" int irc_mean_rows(int dtype, const void* x, float* out, int64_t B, int64_t L, int64_t C,
+                             int64_t ldx, irc_stream_t stream) {
+  IRC_REQUIRE(B >= 0 && L >= 1 && C >= 1, "mean_rows: bad sizes");
+  if (B == 0) return IRC_OK;
+  if (dtype == 0)
+    hipLaunchKernelGGL(mean_rows_kernel<unsigned short>, dim3(nblk(B * C)), dim3(256), 0,
+                       as_stream(stream), (const unsigned short*)x, out, (int)B, (int)L, (int)C,
+                       ldx);
+  else
+    hipLaunchKernelGGL(mean_rows_kernel<float>, dim3(nblk(B * C)), dim3(256), 0,
+                       as_stream(stream), (const float*)x, out, (int)B, (int)L, (int)C, ldx);
+  return check_launch("mean_rows");
+}
+
+extern "C" int irc_bcast_rows(const float* g, float* y, int64_t B, int64_t L, int64_t C,
+                              float scale, irc_stream_t stream) {
+  if (B * L * C == 0) return IRC_OK;
+  hipLaunchKernelGGL(bcast_rows_kernel, dim3(nblk(B * L * C)), dim3(256), 0, as_stream(stream), g,
+                     y, (int)B, (int)L, (int)C, scale);
+  return check_launch("bcast_rows");
+}
+
+extern "C" int irc_l2norm_fwd(const float* x, float* y, float* nrm, int64_t B, int64_t D,
+                              float eps, irc_stream_t stream) {
+  if (B == 0) return IRC_OK;
+  hipLaunchKernelGGL(l2norm_fwd_kernel, dim3(nblk(B, 4)), dim3(256), 0, as_stream(stream), x, y,
+                     nrm, (int)B, (int)D, eps);
+  return check_launch("l2norm_fwd");
+}
+
+extern "C" int irc_l2norm_bwd(const float* dy, const float* y, const float* nrm, float* dx,
+                              int64_t B, int64_t D, float eps, irc_stream_t stream) {
+  if (B == 0) return IRC_OK;
+  hipLaunchKernelGGL(l2norm_bwd_kernel, dim3(nblk(B, 4)), dim3(256), 0, as_stream(stream), dy, y,
+                     nrm, dx, (int)B, (int)D, eps);
+  return check_launch("l2norm_bwd");
+}
+
+extern "C" int irc_nce_lse(const float* S, const float* LQ, int64_t N, int64_t K, float T,
+                           float* lse, float* loss_row, irc_stream_t stream) {
+  IRC_REQUIRE(N >= 1 && K >= 0 && T > 0, "nce_lse: bad sizes");
+  hipLaunchKernelGGL(nce_lse_kernel, dim3((unsigned)(2 * N)), dim3(256), 0, as_stream(stream), S,
+                     LQ, (int)N, (int)K, 1.f / T, lse, loss_row);
+  return check_launch("nce_lse");
+}
+
+extern "C" int irc_nce_grads(const float* S, const float* LQ, const float* lse, int64_t N,
+                             int64_t K, float T, const float* gscale, float* GS, float* GQ,
+                             irc_stream_t stream) {
+  IRC_REQUIRE(N >= 1 && K >= 0 && T > 0, "nce_grads: bad sizes");
+  const float scale = 0.5f / T;
+  hipLaunchKernelGGL(nce_grad_s_kernel, dim3(nblk(4 * N * N)), dim3(256), 0, as_stream(stream), S,
+                     lse, GS, (int)N, 1.f / T, scale, gscale);
+  int rc = check_launch("nce_grad_s");
+  if (rc || K == 0) return rc;
+  hipLaunchKernelGGL(nce_grad_q_kernel, dim3(nblk(N * K)), dim3(256), 0, as_stream(stream), LQ,
+                     lse, GQ, (int)N, (int)K, 1.f / T, scale, gscale);
+  return check_launch("nce_grad_q");
+}
+
+// Deterministic sum: out[0] = scale * sum(x).  partial needs >= 1024 floats.
+extern "C" int irc_sum(const float* x, int64_t n, float scale, float* partial, float* out,
+                       irc_stream_t stream) {
+  const int64_t np = n < 1024 * 4096 ? (n + 4095) / 4096 : 1024;
+  const int64_t per = np > 0 ? (n + np - 1) / np : 1;
+  hipStream_t st = as_stream(stream);
+  if (np > 0)
+    hipLaunchKernelGGL(partial_sum_kernel<1>, dim3((unsigned)np), dim3(RED_NT), 0, st, x, n, per,
+                       partial);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, st, partial, (int)np, scale, 0.f, 0,
+                     out);
+  return check_launch("sum");
+}
+
+// Global grad norm + clip coefficient: out[0] = ||g||, out[1] = min(1, max/(||g||+1e-6)).
+extern "C" int irc_grad_norm_clip(const float* g, int64_t n, float max_norm, float* partial,
+                                  float* out, irc_stream_t stream) {
+  const int64_t np = n < 1024 * 4096 ? (n + 4095) / 4096 : 1024;
+  const int64_t per = np > 0 ? (n + np - 1) / np : 1;
+  hipStream_t st = as_stream(stream);
+  if (np > 0)
+    hipLaunchKernelGGL(partial_sum_kernel<2>, dim3((unsigned)np), dim3(RED_NT), 0, st, g, n, per,
+                       partial);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, st, partial, (int)np, 1.f, max_norm, 1,
+                     out);
+  return check_launch("grad_norm_clip");
+}
+
+extern "C" int irc_adam_step(float* p, const float* g, float* m, float* v, int64_t n,
+                             const float* coef, float b1, float b2, float step_size,
+                             float bc2_sqrt, float eps, irc_stream_t stream) {
+  if (n == 0) return IRC_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), p, g, m, v, n,
+                     coef, b1, b2, step_size, bc2_sqrt, eps);
+  return check_launch("adam");
+}
+
+extern "C" int irc_momentum_update(float* pk, const float* pq, int64_t n, float mom,
+                                   irc_stream_t stream) {
+  if (n == 0) return IRC_OK;
+  hipLaunchKernelGGL(momentum_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), pk, pq, n,
+                     mom);
+  return check_launch("momentum");
+}
+
+extern "C" int irc_enqueue(float* queue, const float* keys, int64_t* ptr, int64_t D, int64_t K,
+                           int64_t B, irc_stream_t stream) {
+  IRC_REQUIRE(B >= 1 && K % B == 0, "enqueue: queue_size %% batch != 0 (caller must skip)");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(enqueue_kernel, dim3(nblk(D * B)), dim3(256), 0, st, queue, keys, ptr,
+                     (int)D, (int)K, (int)B);
+  hipLaunchKernelGGL(ptr_advance_kernel, dim3(1), dim3(64), 0, st, ptr, (int)B, (int)K);
+  return check_launch("enqueue");
+}
+
+extern "C" int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t stream) {
+  if (n == 0) return IRC_OK;
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), x,
+                     (unsigned short*)y, n);
+  return check_launch("cast_bf16");
+}
+
+// partial: workspace of >= ceil(R / 256) * C floats.
+extern "C" int irc_colsum(const float* x, float* out, int64_t R, int64_t C, int64_t ldx,
+                          int accumulate, float* partial, irc_stream_t stream) {
+  if (C == 0) return IRC_OK;
+  const int64_t nch = (R + COLSUM_ROWS - 1) / COLSUM_ROWS;
+  hipStream_t st = as_stream(stream);
+  if (nch > 0)
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nblk(C, 64), (unsigned)nch), dim3(64), 0, st, x,
+                       partial, R, (int)C, ldx);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(nblk(C)), dim3(256), 0, st, partial, out, (int)nch,
+                     (int)C, accumulate);
+  return check_launch("colsum");
+}
+
+extern "C" int irc_axpby(float* out, const float* x, const float* y, float a, float b, int64_t n,
+                         irc_stream_t stream) {
+  if (n == 0) return IRC_OK;
+  hipLaunchKernelGGL(axpby_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), out, x, y, a, b,
+                     n);
+  return check_launch("axpby");
+}

@@ -28,6 +28,27 @@ SIGNATURES = {
     "irc_scan_topk": (I32, [P, P, I64, I64, I64, I64, I64, P, I64, P, P, P]),
     "irc_topk_merge": (I32, [P, P, I64, I64, I64, I64, P, P, P]),
     "irc_scan_scores": (I32, [P, P, I64, I64, I64, P, P]),
+    "irc_gemm": (I32, [I32, I32, I32, I32, I32, I64, I64, I64, F32, P, I64, I64, P, I64, I64,
+                       P, I64, P, I64, I64, P, I64, I64, I32, I64, P]),
+    "irc_embed_ln": (I32, [I32, P, P, P, P, P, P, P, I64, I64, I64, F32, P]),
+    "irc_layernorm": (I32, [I32, P, P, P, P, I64, I64, F32, P]),
+    "irc_attention": (I32, [I32, P, P, P, I64, I64, I64, I64, P]),
+    "irc_lstm_fwd": (I32, [I32, P, P, P, P, P, P, I64, I64, I64, I64, P]),
+    "irc_lstm_bwd": (I32, [I32, P, P, P, P, P, I64, I64, I64, I64, P]),
+    "irc_mean_rows": (I32, [I32, P, P, I64, I64, I64, I64, P]),
+    "irc_bcast_rows": (I32, [P, P, I64, I64, I64, F32, P]),
+    "irc_l2norm_fwd": (I32, [P, P, P, I64, I64, F32, P]),
+    "irc_l2norm_bwd": (I32, [P, P, P, P, I64, I64, F32, P]),
+    "irc_nce_lse": (I32, [P, P, I64, I64, F32, P, P, P]),
+    "irc_nce_grads": (I32, [P, P, P, I64, I64, F32, P, P, P, P]),
+    "irc_axpby": (I32, [P, P, P, F32, F32, I64, P]),
+    "irc_sum": (I32, [P, I64, F32, P, P, P]),
+    "irc_grad_norm_clip": (I32, [P, I64, F32, P, P, P]),
+    "irc_adam_step": (I32, [P, P, P, P, I64, P, F32, F32, F32, F32, F32, P]),
+    "irc_momentum_update": (I32, [P, P, I64, F32, P]),
+    "irc_enqueue": (I32, [P, P, P, I64, I64, I64, P]),
+    "irc_cast_bf16": (I32, [P, P, I64, P]),
+    "irc_colsum": (I32, [P, P, I64, I64, I64, I32, P, P]),
     "irc_prof_enable": (I32, [I32]),
     "irc_prof_query": (I32, [_c.c_char_p, _c.POINTER(_c.c_double), _c.POINTER(I64)]),
     "irc_prof_reset": (I32, []),

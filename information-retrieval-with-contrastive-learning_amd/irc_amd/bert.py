@@ -1,0 +1,273 @@
+"""Frozen BERT encoder on the irc HIP kernels.
+
+Mirrors what the reference reaches through ``BertModel.from_pretrained(
+'bert-base-uncased')(...).last_hidden_state`` in ``bert_extract`` / ``ctx2vec``
+(src/contrastor/contrastive_module.py:32-41, 96-99): eval mode (no dropout),
+token_type 0, positions arange(L), additive key mask, exact-erf GELU, LN eps
+1e-12.  Parameter names are HF's, so ``state_dict()`` round-trips with the
+reference checkpoints' ``bert_model.*`` entries.
+
+Per layer: 1 fused QKV GEMM (+bias) -> attention kernel -> out-proj GEMM with
+bias+residual epilogue -> LayerNorm -> FFN1 GEMM with bias+GELU epilogue ->
+FFN2 GEMM with bias+residual epilogue -> LayerNorm.  Weights are kept fp32 as
+parameters (checkpoint format) and cast once into a cached compute copy.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+from dataclasses import asdict, dataclass
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .precision import compute_dtype
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden_size: int = 768
+    num_hidden_layers: int = 12
+    num_attention_heads: int = 12
+    intermediate_size: int = 3072
+    max_position_embeddings: int = 512
+    type_vocab_size: int = 2
+    layer_norm_eps: float = 1e-12
+    pad_token_id: int = 0
+    initializer_range: float = 0.02
+
+    @classmethod
+    def from_dict(cls, d):
+        keys = cls.__dataclass_fields__.keys()
+        return cls(**{k: v for k, v in d.items() if k in keys})
+
+
+BERT_BASE = BertConfig()
+BERT_LARGE = BertConfig(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16,
+                        intermediate_size=4096)
+PRESETS = {"bert-base-uncased": BERT_BASE, "bert-large-uncased": BERT_LARGE}
+
+
+class _Linear(nn.Module):
+    def __init__(self, i, o):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(o, i), requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(o), requires_grad=False)
+
+
+class _LayerNorm(nn.Module):
+    def __init__(self, h):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(h), requires_grad=False)
+        self.bias = nn.Parameter(torch.zeros(h), requires_grad=False)
+
+
+class _Embeddings(nn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(c.vocab_size, c.hidden_size, _weight=torch.empty(
+            c.vocab_size, c.hidden_size))
+        self.position_embeddings = nn.Embedding(c.max_position_embeddings, c.hidden_size,
+                                                _weight=torch.empty(c.max_position_embeddings,
+                                                                    c.hidden_size))
+        self.token_type_embeddings = nn.Embedding(c.type_vocab_size, c.hidden_size,
+                                                  _weight=torch.empty(c.type_vocab_size,
+                                                                      c.hidden_size))
+        self.LayerNorm = _LayerNorm(c.hidden_size)
+        for e in (self.word_embeddings, self.position_embeddings, self.token_type_embeddings):
+            e.weight.requires_grad_(False)
+
+
+class _SelfAttn(nn.Module):
+    def __init__(self, h):
+        super().__init__()
+        self.query, self.key, self.value = _Linear(h, h), _Linear(h, h), _Linear(h, h)
+
+
+class _AttnOut(nn.Module):
+    def __init__(self, h):
+        super().__init__()
+        self.dense = _Linear(h, h)
+        self.LayerNorm = _LayerNorm(h)
+
+
+class _Attention(nn.Module):
+    def __init__(self, h):
+        super().__init__()
+        self.self = _SelfAttn(h)
+        self.output = _AttnOut(h)
+
+
+class _Intermediate(nn.Module):
+    def __init__(self, h, i):
+        super().__init__()
+        self.dense = _Linear(h, i)
+
+
+class _Output(nn.Module):
+    def __init__(self, i, h):
+        super().__init__()
+        self.dense = _Linear(i, h)
+        self.LayerNorm = _LayerNorm(h)
+
+
+class _Layer(nn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.attention = _Attention(c.hidden_size)
+        self.intermediate = _Intermediate(c.hidden_size, c.intermediate_size)
+        self.output = _Output(c.intermediate_size, c.hidden_size)
+
+
+class _Encoder(nn.Module):
+    def __init__(self, c: BertConfig):
+        super().__init__()
+        self.layer = nn.ModuleList([_Layer(c) for _ in range(c.num_hidden_layers)])
+
+
+class _Pooler(nn.Module):
+    def __init__(self, h):
+        super().__init__()
+        self.dense = _Linear(h, h)
+
+
+class BertModel(nn.Module):
+    """HF-compatible parameter tree; forward runs on the irc kernels only."""
+
+    def __init__(self, config: BertConfig, seed: int | None = 0):
+        super().__init__()
+        self.config = config
+        self.embeddings = _Embeddings(config)
+        self.encoder = _Encoder(config)
+        self.pooler = _Pooler(config.hidden_size)  # kept for checkpoint compatibility
+        self._init_weights(seed)
+        self._cache = {}
+        self.eval()
+
+    # HF _init_weights: normal(0, 0.02) for Linear/Embedding, padding row 0, LN (1, 0)
+    @torch.no_grad()
+    def _init_weights(self, seed):
+        g = torch.Generator().manual_seed(seed) if seed is not None else None
+        std = self.config.initializer_range
+        for name, p in self.named_parameters():
+            if name.endswith("LayerNorm.weight"):
+                p.fill_(1.0)
+            elif name.endswith("LayerNorm.bias") or name.endswith(".bias"):
+                p.zero_()
+            else:
+                p.copy_(torch.randn(p.shape, generator=g) * std)
+        self.embeddings.word_embeddings.weight[self.config.pad_token_id].zero_()
+
+    @classmethod
+    def from_pretrained(cls, name_or_path: str, config: BertConfig | dict | None = None,
+                        seed: int = 0):
+        """Local directory (config.json + model.safetensors / pytorch_model.bin) or a
+        preset name.  Offline: a preset name builds the architecture with seeded
+        random init (HF's initializer); weights are never fetched over a network."""
+        if isinstance(config, dict):
+            config = BertConfig.from_dict(config)
+        if name_or_path and os.path.isdir(name_or_path):
+            with open(os.path.join(name_or_path, "config.json")) as f:
+                cfg = BertConfig.from_dict(json.load(f)) if config is None else config
+            m = cls(cfg, seed=None)
+            st = _load_local_weights(name_or_path)
+            st = {k[5:] if k.startswith("bert.") else k: v for k, v in st.items()}
+            missing = m.load_state_dict(st, strict=False)
+            if missing.missing_keys:
+                raise RuntimeError(f"missing BERT weights: {missing.missing_keys[:5]}")
+            return m
+        cfg = config or PRESETS.get(name_or_path, BERT_BASE)
+        return cls(cfg, seed=seed)
+
+    def _apply(self, fn, *a, **k):
+        self._cache = {}
+        return super()._apply(fn, *a, **k)
+
+    def load_state_dict(self, *a, **k):
+        self._cache = {}
+        return super().load_state_dict(*a, **k)
+
+    def _weights(self):
+        dt = compute_dtype()
+        key = (dt, self.embeddings.word_embeddings.weight.device)
+        w = self._cache.get(key)
+        if w is not None:
+            return w
+        cast = (lambda t: t.detach().to(dt).contiguous())
+        f32 = (lambda t: t.detach().float().contiguous())
+        e = self.embeddings
+        w = {"word": cast(e.word_embeddings.weight), "pos": cast(e.position_embeddings.weight),
+             "type0": cast(e.token_type_embeddings.weight[0]), "ln_g": f32(e.LayerNorm.weight),
+             "ln_b": f32(e.LayerNorm.bias), "layers": []}
+        for lyr in self.encoder.layer:
+            sa = lyr.attention.self
+            w["layers"].append({
+                "wqkv": cast(torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0)),
+                "bqkv": f32(torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0)),
+                "wo": cast(lyr.attention.output.dense.weight),
+                "bo": f32(lyr.attention.output.dense.bias),
+                "ln1_g": f32(lyr.attention.output.LayerNorm.weight),
+                "ln1_b": f32(lyr.attention.output.LayerNorm.bias),
+                "w1": cast(lyr.intermediate.dense.weight), "b1": f32(lyr.intermediate.dense.bias),
+                "w2": cast(lyr.output.dense.weight), "b2": f32(lyr.output.dense.bias),
+                "ln2_g": f32(lyr.output.LayerNorm.weight), "ln2_b": f32(lyr.output.LayerNorm.bias),
+            })
+        self._cache = {key: w}
+        return w
+
+    @torch.no_grad()
+    def encode(self, input_ids: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
+        """last_hidden_state [B, L, H] in the compute dtype (bf16 or fp32)."""
+        c = self.config
+        ids = input_ids.to(torch.int64).contiguous()
+        mask = attention_mask.to(torch.int64).contiguous()
+        B, L = ids.shape
+        if L > c.max_position_embeddings:
+            raise ValueError(f"sequence length {L} > max_position_embeddings")
+        H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
+        w = self._weights()
+        x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
+        for lw in w["layers"]:
+            qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
+            ctx = ops.attention(qkv, mask, B, L, H, heads)
+            a = ops.gemm(ctx, lw["wo"], bias=lw["bo"], residual=x, epilogue=ops.EPI_BIAS_RESID)
+            a = ops.layernorm(a, lw["ln1_g"], lw["ln1_b"], eps, out=a)
+            i = ops.gemm(a, lw["w1"], bias=lw["b1"], epilogue=ops.EPI_BIAS_GELU)
+            x = ops.gemm(i, lw["w2"], bias=lw["b2"], residual=a, epilogue=ops.EPI_BIAS_RESID)
+            x = ops.layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, out=x)
+        return x.view(B, L, H)
+
+    def forward(self, input_ids=None, attention_mask=None, **kw):
+        if attention_mask is None:
+            attention_mask = torch.ones_like(input_ids)
+        return BertOutputs(self.encode(input_ids, attention_mask))
+
+    def flops_per_sequence(self, L: int) -> float:
+        c = self.config
+        H, I = c.hidden_size, c.intermediate_size
+        return c.num_hidden_layers * (2 * L * (4 * H * H + 2 * H * I) + 4 * L * L * H)
+
+    def export_config(self):
+        return asdict(self.config)
+
+
+class BertOutputs:
+    def __init__(self, h):
+        self.last_hidden_state = h
+
+
+def _load_local_weights(path):
+    st_path = os.path.join(path, "model.safetensors")
+    if os.path.exists(st_path):
+        from safetensors.torch import load_file
+
+        return load_file(st_path)
+    bin_path = os.path.join(path, "pytorch_model.bin")
+    return torch.load(bin_path, map_location="cpu", weights_only=True)
+
+
+def attention_scale(c: BertConfig) -> float:
+    return 1.0 / math.sqrt(c.hidden_size // c.num_attention_heads)

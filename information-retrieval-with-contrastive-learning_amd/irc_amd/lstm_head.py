@@ -1,0 +1,265 @@
+"""BiLSTM + Linear encoder head and its seq2vec tail on the irc HIP kernels.
+
+Reference: ``LSTM`` in src/model.py:7-41 (nn.LSTM(input, hidden, num_layers,
+batch_first, bidirectional) -> Linear(2*hidden -> output) -> Identity) and
+``seq2vec`` in src/contrastor/contrastive_module.py:102-112 (mean over ALL L
+positions, PAD included, then F.normalize).
+
+Parameters live in ONE flat fp32 buffer (16-float aligned slices) with
+nn.LSTM-named views, so the optimizer, clipping and the momentum update are
+single fused launches over the buffer, and ``state_dict()`` keeps the
+reference's keys (``lstm.weight_ih_l0`` ... ``scaling_layer.0.bias``).
+Gradients go to a parallel flat buffer (``flat_grad``); each named parameter's
+``.grad`` is a view of it.
+
+Forward (per layer): xp = x W_ih^T + (b_ih + b_hh) for both directions in one
+GEMM -> recurrence kernel -> next layer.  Head: mean over positions of the top
+layer, then the Linear (mean and Linear commute exactly in real arithmetic),
+then L2 normalisation.  Backward: l2norm bwd -> Linear grads -> broadcast /L ->
+per layer BPTT kernel -> weight-gradient GEMMs over all (b, t).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .precision import compute_dtype
+
+ALIGN = 16  # floats (64 B) per slice start: GEMM operands need 16-byte alignment
+
+
+def lstm_param_specs(input_size, hidden, num_layers, bidirectional, output_size):
+    """(name, shape) in nn.LSTM + Linear named_parameters() order."""
+    specs = []
+    dirs = ["", "_reverse"] if bidirectional else [""]
+    for l in range(num_layers):
+        in_l = input_size if l == 0 else hidden * len(dirs)
+        for d in dirs:
+            specs += [(f"lstm.weight_ih_l{l}{d}", (4 * hidden, in_l)),
+                      (f"lstm.weight_hh_l{l}{d}", (4 * hidden, hidden)),
+                      (f"lstm.bias_ih_l{l}{d}", (4 * hidden,)),
+                      (f"lstm.bias_hh_l{l}{d}", (4 * hidden,))]
+    specs += [("scaling_layer.0.weight", (output_size, hidden * len(dirs))),
+              ("scaling_layer.0.bias", (output_size,))]
+    return specs
+
+
+def _layout(specs):
+    """Flat offsets: per layer [W_ih fwd | W_ih rev] and [W_hh fwd | W_hh rev] are
+    adjacent so both directions are one GEMM operand / one kernel argument."""
+    order = []
+    names = [n for n, _ in specs]
+    shapes = dict(specs)
+    layers = sorted({int(n.split("_l")[1].split("_")[0].rstrip("_reverse")) for n in names
+                     if n.startswith("lstm.")})
+    for l in layers:
+        for kind in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
+            for d in ("", "_reverse"):
+                n = f"lstm.{kind}_l{l}{d}"
+                if n in shapes:
+                    order.append(n)
+    order += ["scaling_layer.0.weight", "scaling_layer.0.bias"]
+    offs, o = {}, 0
+    for n in order:
+        numel = math.prod(shapes[n])
+        if not (n.startswith("lstm.") and n.endswith("_reverse")):
+            o = (o + ALIGN - 1) // ALIGN * ALIGN
+        offs[n] = o
+        o += numel
+    total = (o + ALIGN - 1) // ALIGN * ALIGN
+    return offs, total
+
+
+class LSTMHead(nn.Module):
+    """Drop-in for the reference ``LSTM`` module (same config keys and names)."""
+
+    def __init__(self, config, init: bool = True, **kwargs):
+        super().__init__()
+        c = config["model"]["LSTM"]
+        self.input_size = int(c["input_size"])
+        self.hidden = int(c["hidden_size"])
+        self.num_layers = int(c["num_layers"])
+        self.bidirectional = bool(c["bidirectional"])
+        self.output_size = int(c["output_size"])
+        act = c.get("activation", "Identity")
+        if act != "Identity":
+            raise NotImplementedError(f"activation {act!r}: the reference config uses Identity")
+        self.ndir = 2 if self.bidirectional else 1
+        self.specs = lstm_param_specs(self.input_size, self.hidden, self.num_layers,
+                                      self.bidirectional, self.output_size)
+        self.offsets, self.numel_flat = _layout(self.specs)
+        self.flat = nn.Parameter(torch.zeros(self.numel_flat), requires_grad=True)
+        self.register_buffer("flat_grad", torch.zeros(self.numel_flat), persistent=False)
+        if init:
+            self.reset_parameters()
+
+    # ---- parameter plumbing ----
+    def view(self, name, buf=None):
+        buf = self.flat if buf is None else buf
+        shape = dict(self.specs)[name]
+        o = self.offsets[name]
+        return buf.detach()[o:o + math.prod(shape)].view(shape)
+
+    def named_flat_params(self):
+        return [(n, self.view(n)) for n, _ in self.specs]
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        # reference key layout: one entry per nn.LSTM / Linear parameter
+        for n, _ in self.specs:
+            destination[prefix + n] = self.view(n).clone()
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        with torch.no_grad():
+            for n, shape in self.specs:
+                k = prefix + n
+                if k in state_dict:
+                    self.view(n).copy_(state_dict[k].reshape(shape))
+                elif strict:
+                    missing_keys.append(k)
+        for k in state_dict:  # the head has no child modules: every prefixed key is ours
+            if k.startswith(prefix) and k[len(prefix):] not in self.offsets and strict:
+                unexpected_keys.append(k)
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        """nn.LSTM default init then the reference's init_weights (model.py:29-36):
+        xavier_uniform_ (weight_ih*, Linear weight), orthogonal_ (weight_hh*),
+        zero biases -- consuming torch's CPU RNG in the same order."""
+        cpu = {n: torch.empty(s) for n, s in self.specs}
+        stdv = 1.0 / math.sqrt(self.hidden)
+        for n, _ in self.specs:  # nn.LSTM.reset_parameters
+            if n.startswith("lstm."):
+                cpu[n].uniform_(-stdv, stdv)
+        w, b = cpu["scaling_layer.0.weight"], cpu["scaling_layer.0.bias"]  # nn.Linear init
+        nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        bound = 1 / math.sqrt(w.shape[1])
+        nn.init.uniform_(b, -bound, bound)
+        for n, _ in self.specs:  # LSTM.init_weights
+            if "weight_ih" in n or "scaling_layer.0.weight" in n:
+                nn.init.xavier_uniform_(cpu[n])
+            elif "weight_hh" in n:
+                nn.init.orthogonal_(cpu[n])
+            elif "bias" in n:
+                nn.init.constant_(cpu[n], 0)
+        for n, _ in self.specs:
+            self.view(n).copy_(cpu[n])
+
+    # ---- compute ----
+    def _layer_weights(self, l, dt):
+        """(W_ih both dirs [ndir*4H, In], W_hh [ndir, 4H, H], bias [ndir*4H]) in dt."""
+        H, nd = self.hidden, self.ndir
+        wih0 = self.offsets[f"lstm.weight_ih_l{l}"]
+        in_l = self.input_size if l == 0 else H * nd
+        flat = self.flat.detach()
+        wih = flat[wih0:wih0 + nd * 4 * H * in_l].view(nd * 4 * H, in_l)
+        whh0 = self.offsets[f"lstm.weight_hh_l{l}"]
+        whh = flat[whh0:whh0 + nd * 4 * H * H].view(nd, 4 * H, H)
+        bih0 = self.offsets[f"lstm.bias_ih_l{l}"]
+        bhh0 = self.offsets[f"lstm.bias_hh_l{l}"]
+        bias = ops.axpby(flat[bih0:bih0 + nd * 4 * H], flat[bhh0:bhh0 + nd * 4 * H])
+        if dt == torch.bfloat16:
+            wih = ops.cast_bf16(wih)
+            whh = ops.cast_bf16(whh)
+        return wih, whh, bias
+
+    def forward_compute(self, features: torch.Tensor, save: bool):
+        """features [B, L, In] -> (emb [B, D] fp32 unit-norm, saved state or None)."""
+        B, L, In = features.shape
+        if In != self.input_size:
+            raise ValueError(f"feature dim {In} != input_size {self.input_size}")
+        dt = compute_dtype()
+        H, nd = self.hidden, self.ndir
+        x = features.reshape(B * L, In)
+        if x.dtype != dt:
+            x = x.to(dt)  # dtype conversion of the frozen features (copy)
+        x = x.contiguous()
+        layers = []
+        for l in range(self.num_layers):
+            wih, whh, bias = self._layer_weights(l, dt)
+            xp = ops.gemm(x, wih, bias=bias, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
+            hout, gsave, csave, hprev = ops.lstm_fwd(xp, whh, B, L, H, nd, dt, save=save)
+            if save:
+                layers.append((x, wih, whh, gsave, csave, hprev))
+            x = hout
+        mh = ops.mean_rows(x, B, L, nd * H)  # [B, 2H] fp32
+        wl = self.view("scaling_layer.0.weight")
+        bl = self.view("scaling_layer.0.bias")
+        m = ops.gemm(mh, wl, bias=bl, epilogue=ops.EPI_BIAS)
+        emb, nrm = ops.l2norm_fwd(m)
+        saved = (B, L, layers, mh, emb, nrm) if save else None
+        return emb, saved
+
+    def backward_compute(self, saved, demb: torch.Tensor):
+        """Accumulate d(loss)/d(params) into self.flat_grad."""
+        B, L, layers, mh, emb, nrm = saved
+        H, nd = self.hidden, self.ndir
+        g = self.flat_grad
+        dm = ops.l2norm_bwd(demb.contiguous(), emb, nrm)
+        ops.gemm(dm, mh, trans_a=True, b_is_nk=False, accumulate=True,
+                 out=self.view("scaling_layer.0.weight", g))
+        ops.colsum(dm, out=self.view("scaling_layer.0.bias", g), accumulate=True)
+        dmh = ops.gemm(dm, self.view("scaling_layer.0.weight"), b_is_nk=False)  # [B, 2H]
+        dy = ops.bcast_rows(dmh, B, L, 1.0 / L)  # [B*L, 2H] fp32
+        for l in range(self.num_layers - 1, -1, -1):
+            x, wih, whh, gsave, csave, hprev = layers[l]
+            dg = ops.lstm_bwd(dy, whh, gsave, csave, B, L, H, nd)  # [nd, B*L, 4H] fp32
+            dgc = ops.cast_bf16(dg) if x.dtype == torch.bfloat16 else dg
+            in_l = x.shape[1]
+            dx = None
+            for d in range(nd):
+                sfx = f"l{l}" + ("_reverse" if d == 1 else "")
+                ops.gemm(dgc[d], x, trans_a=True, b_is_nk=False, accumulate=True,
+                         out=self.view(f"lstm.weight_ih_{sfx}", g), out_dtype=torch.float32)
+                ops.gemm(dgc[d], hprev[d], trans_a=True, b_is_nk=False, accumulate=True,
+                         out=self.view(f"lstm.weight_hh_{sfx}", g), out_dtype=torch.float32)
+                ops.colsum(dg[d], out=self.view(f"lstm.bias_ih_{sfx}", g), accumulate=True)
+                ops.colsum(dg[d], out=self.view(f"lstm.bias_hh_{sfx}", g), accumulate=True)
+                if l > 0:
+                    w_d = wih[d * 4 * H:(d + 1) * 4 * H]  # [4H, In] = [K][N]
+                    dx = ops.gemm(dgc[d], w_d, b_is_nk=False, out=dx, accumulate=dx is not None,
+                                  out_dtype=torch.float32)
+            dy = dx
+
+    def forward(self, features, **kwargs):
+        """Per-position head output [B, L, D] (reference LSTM.forward semantics);
+        the training path uses the fused ``seq2vec`` instead."""
+        B, L, In = features.shape
+        dt = compute_dtype()
+        x = features.reshape(B * L, In).to(dt).contiguous()
+        for l in range(self.num_layers):
+            wih, whh, bias = self._layer_weights(l, dt)
+            xp = ops.gemm(x, wih, bias=bias, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
+            x, _, _, _ = ops.lstm_fwd(xp, whh, B, L, self.hidden, self.ndir, dt, save=False)
+        wl = self.view("scaling_layer.0.weight")
+        bl = self.view("scaling_layer.0.bias")
+        xf = x if x.dtype == torch.float32 else x.float()
+        return ops.gemm(xf.contiguous(), wl, bias=bl, epilogue=ops.EPI_BIAS).view(B, L, -1)
+
+
+class _Seq2VecFn(torch.autograd.Function):
+    """emb = seq2vec(features) with grads accumulated into head.flat_grad."""
+
+    @staticmethod
+    def forward(ctx, features, flat, head):
+        emb, saved = head.forward_compute(features, save=True)
+        ctx.head = head
+        ctx.saved = saved
+        return emb
+
+    @staticmethod
+    def backward(ctx, demb):
+        ctx.head.backward_compute(ctx.saved, demb)
+        ctx.saved = None
+        return None, None, None
+
+
+def seq2vec(head: LSTMHead, features: torch.Tensor, grad: bool) -> torch.Tensor:
+    if grad and torch.is_grad_enabled():
+        return _Seq2VecFn.apply(features, head.flat, head)
+    with torch.no_grad():
+        emb, _ = head.forward_compute(features, save=False)
+    return emb

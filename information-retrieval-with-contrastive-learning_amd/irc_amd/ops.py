@@ -1,0 +1,224 @@
+"""Typed wrappers over the libirc_hip.so entry points (include/irc.h).
+
+Each wrapper validates devices/dtypes, allocates outputs from the PyTorch
+caching allocator and launches on the current HIP stream.  None of them has a
+fallback: a CPU tensor or a missing library raises.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._torch import ptr, require_hip, stream_ptr
+
+BF16, F32 = torch.bfloat16, torch.float32
+_DT = {BF16: 0, F32: 1}
+
+EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RESID, EPI_RESID = 0, 1, 2, 3, 4
+
+
+def _code(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"irc kernels take bf16 or fp32, got {t.dtype}") from None
+
+
+def gemm(a, b, *, trans_a=False, b_is_nk=True, bias=None, epilogue=EPI_NONE, residual=None,
+         alpha=1.0, out=None, out_dtype=None, accumulate=False):
+    """out[M, N] = alpha * op(a) @ op(b) (+ bias) (-> gelu) (+ residual).
+
+    a: [M, K] (or [K, M] with trans_a); b: [N, K] when b_is_nk (nn.Linear weight
+    layout, i.e. a @ b.T) else [K, N].  Inputs bf16 or fp32 (same dtype);
+    fp32 inputs run the exact fp32 MFMA.  2-D only (see gemm_batched).
+    """
+    require_hip(a, b, bias, residual, out)
+    if a.dtype != b.dtype:
+        raise TypeError(f"gemm operands must share a dtype ({a.dtype} vs {b.dtype})")
+    if a.stride(-1) != 1 or b.stride(-1) != 1:
+        raise ValueError("gemm operands must be contiguous in their last dim")
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    N, Kb = (b.shape[0], b.shape[1]) if b_is_nk else (b.shape[1], b.shape[0])
+    if K != Kb:
+        raise ValueError(f"gemm inner dims differ: {K} vs {Kb}")
+    if out is None:
+        od = out_dtype or a.dtype
+        out = torch.empty((M, N), dtype=od, device=a.device)
+        if accumulate:
+            out.zero_()
+    if bias is not None and bias.dtype != F32:
+        raise TypeError("bias must be fp32")
+    if residual is not None and residual.dtype != out.dtype:
+        raise TypeError("residual dtype must match the output")
+    _lib.call("irc_gemm", _code(a), _code(out), 1 if trans_a else 0, 0 if b_is_nk else 1,
+              int(epilogue), M, N, K, float(alpha), ptr(a), a.stride(0), 0, ptr(b), b.stride(0),
+              0, ptr(bias), 0, ptr(residual), residual.stride(0) if residual is not None else 0, 0,
+              ptr(out), out.stride(0), 0, 1 if accumulate else 0, 1, stream_ptr(a.device))
+    return out
+
+
+def embed_ln(ids, word, pos, type0, gamma, beta, eps=1e-12):
+    require_hip(ids, word, pos, type0, gamma, beta)
+    B, L = ids.shape
+    H = word.shape[1]
+    y = torch.empty((B * L, H), dtype=word.dtype, device=word.device)
+    _lib.call("irc_embed_ln", _code(word), ptr(ids), ptr(word), ptr(pos), ptr(type0), ptr(gamma),
+              ptr(beta), ptr(y), B * L, L, H, float(eps), stream_ptr(word.device))
+    return y
+
+
+def layernorm(x, gamma, beta, eps=1e-12, out=None):
+    require_hip(x, gamma, beta)
+    out = torch.empty_like(x) if out is None else out
+    H = x.shape[-1]
+    _lib.call("irc_layernorm", _code(x), ptr(x), ptr(out), ptr(gamma), ptr(beta),
+              x.numel() // H, H, float(eps), stream_ptr(x.device))
+    return out
+
+
+def attention(qkv, mask, B, L, H, heads):
+    require_hip(qkv, mask)
+    ctx = torch.empty((B * L, H), dtype=qkv.dtype, device=qkv.device)
+    _lib.call("irc_attention", _code(qkv), ptr(qkv), ptr(mask), ptr(ctx), B, L, H, heads,
+              stream_ptr(qkv.device))
+    return ctx
+
+
+def lstm_fwd(xp, whh, B, L, H, ndir, h_dtype, save=True):
+    """xp [B*L, ndir*4H] fp32 -> hout [B*L, ndir*H] (+ saved state for BPTT)."""
+    require_hip(xp, whh)
+    dev = xp.device
+    hout = torch.empty((B * L, ndir * H), dtype=h_dtype, device=dev)
+    gsave = torch.empty((ndir, B * L, 4 * H), dtype=F32, device=dev) if save else None
+    csave = torch.empty((ndir, B * L, H), dtype=F32, device=dev) if save else None
+    hprev = torch.empty((ndir, B * L, H), dtype=h_dtype, device=dev) if save else None
+    if whh.dtype != h_dtype:
+        raise TypeError("W_hh dtype must match the hidden-state dtype")
+    _lib.call("irc_lstm_fwd", _code(whh), ptr(xp), ptr(whh), ptr(hout), ptr(gsave), ptr(csave),
+              ptr(hprev), B, L, H, ndir, stream_ptr(dev))
+    return hout, gsave, csave, hprev
+
+
+def lstm_bwd(dy, whh, gsave, csave, B, L, H, ndir):
+    require_hip(dy, whh, gsave, csave)
+    dg = torch.empty((ndir, B * L, 4 * H), dtype=F32, device=dy.device)
+    _lib.call("irc_lstm_bwd", _code(whh), ptr(dy), ptr(whh), ptr(gsave), ptr(csave), ptr(dg), B,
+              L, H, ndir, stream_ptr(dy.device))
+    return dg
+
+
+def mean_rows(x, B, L, C, ldx=None):
+    require_hip(x)
+    out = torch.empty((B, C), dtype=F32, device=x.device)
+    _lib.call("irc_mean_rows", _code(x), ptr(x), ptr(out), B, L, C, ldx or C,
+              stream_ptr(x.device))
+    return out
+
+
+def bcast_rows(g, B, L, scale):
+    require_hip(g)
+    C = g.shape[1]
+    y = torch.empty((B * L, C), dtype=F32, device=g.device)
+    _lib.call("irc_bcast_rows", ptr(g), ptr(y), B, L, C, float(scale), stream_ptr(g.device))
+    return y
+
+
+def l2norm_fwd(x, eps=1e-12):
+    require_hip(x)
+    y = torch.empty_like(x)
+    nrm = torch.empty((x.shape[0],), dtype=F32, device=x.device)
+    _lib.call("irc_l2norm_fwd", ptr(x), ptr(y), ptr(nrm), x.shape[0], x.shape[1], float(eps),
+              stream_ptr(x.device))
+    return y, nrm
+
+
+def l2norm_bwd(dy, y, nrm, eps=1e-12):
+    require_hip(dy, y, nrm)
+    dx = torch.empty_like(dy)
+    _lib.call("irc_l2norm_bwd", ptr(dy), ptr(y), ptr(nrm), ptr(dx), dy.shape[0], dy.shape[1],
+              float(eps), stream_ptr(dy.device))
+    return dx
+
+
+def nce_lse(S, LQ, N, K, T):
+    require_hip(S, LQ)
+    lse = torch.empty((2 * N,), dtype=F32, device=S.device)
+    loss_row = torch.empty((2 * N,), dtype=F32, device=S.device)
+    _lib.call("irc_nce_lse", ptr(S), ptr(LQ), N, K, float(T), ptr(lse), ptr(loss_row),
+              stream_ptr(S.device))
+    return lse, loss_row
+
+
+def nce_grads(S, LQ, lse, N, K, T, gscale=None):
+    """Softmax gradients of the InfoNCE rows, times the device scalar gscale."""
+    require_hip(S, LQ, lse, gscale)
+    GS = torch.empty_like(S)
+    GQ = torch.empty((N, K), dtype=F32, device=S.device) if K > 0 else None
+    _lib.call("irc_nce_grads", ptr(S), ptr(LQ), ptr(lse), N, K, float(T), ptr(gscale), ptr(GS),
+              ptr(GQ), stream_ptr(S.device))
+    return GS, GQ
+
+
+def axpby(x, y, a=1.0, b=1.0, out=None):
+    require_hip(x, y, out)
+    out = torch.empty_like(x) if out is None else out
+    _lib.call("irc_axpby", ptr(out), ptr(x), ptr(y), float(a), float(b), x.numel(),
+              stream_ptr(x.device))
+    return out
+
+
+def dsum(x, scale=1.0):
+    """Deterministic fp32 sum (fixed order) -> 0-d tensor."""
+    require_hip(x)
+    partial = torch.empty((1024,), dtype=F32, device=x.device)
+    out = torch.empty((2,), dtype=F32, device=x.device)
+    _lib.call("irc_sum", ptr(x), x.numel(), float(scale), ptr(partial), ptr(out),
+              stream_ptr(x.device))
+    return out[0]
+
+
+def grad_norm_clip(g, max_norm):
+    """[||g||, min(1, max_norm / (||g|| + 1e-6))] as a device tensor (no sync)."""
+    require_hip(g)
+    partial = torch.empty((1024,), dtype=F32, device=g.device)
+    out = torch.empty((2,), dtype=F32, device=g.device)
+    _lib.call("irc_grad_norm_clip", ptr(g), g.numel(), float(max_norm), ptr(partial), ptr(out),
+              stream_ptr(g.device))
+    return out
+
+
+def adam_step(p, g, m, v, coef, b1, b2, step_size, bc2_sqrt, eps):
+    require_hip(p, g, m, v, coef)
+    _lib.call("irc_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(coef), float(b1),
+              float(b2), float(step_size), float(bc2_sqrt), float(eps), stream_ptr(p.device))
+
+
+def momentum_update(pk, pq, mom):
+    require_hip(pk, pq)
+    _lib.call("irc_momentum_update", ptr(pk), ptr(pq), pk.numel(), float(mom),
+              stream_ptr(pk.device))
+
+
+def enqueue(queue, keys, qptr):
+    require_hip(queue, keys, qptr)
+    D, K = queue.shape
+    _lib.call("irc_enqueue", ptr(queue), ptr(keys), ptr(qptr), D, K, keys.shape[0],
+              stream_ptr(queue.device))
+
+
+def cast_bf16(x):
+    require_hip(x)
+    y = torch.empty(x.shape, dtype=BF16, device=x.device)
+    _lib.call("irc_cast_bf16", ptr(x), ptr(y), x.numel(), stream_ptr(x.device))
+    return y
+
+
+def colsum(x, out=None, accumulate=False):
+    require_hip(x)
+    R, C = x.shape
+    if out is None:
+        out = torch.empty((C,), dtype=F32, device=x.device)
+    partial = torch.empty((max(1, (R + 255) // 256) * C,), dtype=F32, device=x.device)
+    _lib.call("irc_colsum", ptr(x), ptr(out), R, C, x.stride(0), 1 if accumulate else 0,
+              ptr(partial), stream_ptr(x.device))
+    return out

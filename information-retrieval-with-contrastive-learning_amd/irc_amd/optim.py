@@ -1,0 +1,99 @@
+"""Fused optimizers over the flat fp32 parameter buffer of the encoder head.
+
+Reference semantics (src/model.py:44-58, src/train.py:150-169): Adam(lr, betas)
+(eps 1e-8, no weight decay) over model.parameters(); parameters without a
+gradient (frozen BERT, the momentum encoder) are skipped, so only encoder_q
+moves.  clip_grad_norm_(max_norm) is fused into the step: the global norm and
+the clip coefficient are computed on the device and applied inside the update
+kernel (no host sync).  The optimizer follows the module across .to(device):
+it reads head.flat / head.flat_grad at step time and keeps its moments on the
+same device.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+
+
+class FusedAdam:
+    def __init__(self, head, lr=2.5e-4, betas=(0.9, 0.999), eps=1e-8):
+        self.head = head
+        self.lr = float(lr)
+        self.b1, self.b2 = (float(b) for b in betas)
+        self.eps = float(eps)
+        self.step_count = 0
+        self.exp_avg = None
+        self.exp_avg_sq = None
+        self.last_norm = None  # device tensor [grad norm, clip coef] of the last step
+
+    def _moments(self):
+        flat = self.head.flat
+        if self.exp_avg is None:
+            self.exp_avg = torch.zeros(flat.shape, dtype=torch.float32, device=flat.device)
+            self.exp_avg_sq = torch.zeros_like(self.exp_avg)
+        elif self.exp_avg.device != flat.device:
+            self.to(flat.device)
+        return self.exp_avg, self.exp_avg_sq
+
+    def to(self, device):
+        if self.exp_avg is not None:
+            self.exp_avg = self.exp_avg.to(device)
+            self.exp_avg_sq = self.exp_avg_sq.to(device)
+        return self
+
+    def clip_and_step(self, max_norm: float | None = None):
+        """clip_grad_norm_(max_norm) (if given) + one Adam step; returns the device
+        tensor [norm, coef]."""
+        g = self.head.flat_grad
+        m, v = self._moments()
+        coef = ops.grad_norm_clip(g, max_norm if max_norm is not None else float("inf"))
+        self.last_norm = coef
+        self.step_count += 1
+        t = self.step_count
+        bc1 = 1 - self.b1 ** t
+        bc2 = 1 - self.b2 ** t
+        ops.adam_step(self.head.flat.detach(), g, m, v, coef if max_norm is not None else None,
+                      self.b1, self.b2, self.lr / bc1, math.sqrt(bc2), self.eps)
+        return coef
+
+    def step(self):
+        return self.clip_and_step(None)
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.head.flat_grad.zero_()
+
+    # torch.optim-style checkpoint dict (flat state under parameter index 0)
+    def state_dict(self):
+        m, v = self._moments()
+        return {"state": {0: {"step": torch.tensor(float(self.step_count)), "exp_avg": m,
+                              "exp_avg_sq": v}},
+                "param_groups": [{"lr": self.lr, "betas": (self.b1, self.b2), "eps": self.eps,
+                                  "weight_decay": 0, "amsgrad": False, "params": [0]}]}
+
+    def load_state_dict(self, sd):
+        """Accepts this class's dict, or a reference torch.optim.Adam dict whose
+        parameter indices 0..n-1 are encoder_q's parameters in nn.LSTM order."""
+        m, v = self._moments()
+        st = sd.get("state", {})
+        specs = self.head.specs
+        if 0 in st and st[0]["exp_avg"].numel() == m.numel():
+            self.step_count = int(float(st[0]["step"]))
+            m.copy_(st[0]["exp_avg"])
+            v.copy_(st[0]["exp_avg_sq"])
+        elif st:
+            for i, (name, shape) in enumerate(specs):
+                if i in st:
+                    self.head.view(name, m).copy_(st[i]["exp_avg"].reshape(shape))
+                    self.head.view(name, v).copy_(st[i]["exp_avg_sq"].reshape(shape))
+                    self.step_count = int(float(st[i]["step"]))
+        pg = sd["param_groups"][0]
+        self.lr = float(pg["lr"])
+        self.b1, self.b2 = (float(b) for b in pg["betas"])
+        self.eps = float(pg.get("eps", self.eps))
+
+    @property
+    def param_groups(self):
+        return [{"lr": self.lr}]

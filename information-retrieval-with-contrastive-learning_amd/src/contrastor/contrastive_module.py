@@ -1,0 +1,113 @@
+"""Drop-in for src/contrastor/contrastive_module.py (RetrievalModelWrapper).
+
+Same constructor, attributes (encoder_q, encoder_k, queue [dim, K] buffer,
+queue_ptr, add_queue_to_loss, use_momentum, use_queue, bert_tokenizer,
+bert_model, criterion, loss_config) and methods (bert_extract,
+_momentum_update_key_encoder, _dequeue_and_enqueue, forward, ctx2vec, seq2vec)
+as the reference (contrastive_module.py:6-112).  Device work runs on the irc
+HIP kernels: BERT on irc_amd.bert, the BiLSTM head + seq2vec on
+irc_amd.lstm_head, the loss on irc_amd.nce, momentum and enqueue as single
+fused launches.  Like the reference, ``use_momentum``/``use_queue`` arguments
+are ignored in favour of loss_config (contrastive_module.py:12-13).
+
+Extension (superset): the BERT source/config/tokenizer come from the optional
+``bert`` section of config.yaml; offline, a preset name builds the architecture
+with seeded random weights instead of fetching 'bert-base-uncased'.
+"""
+import copy
+
+import torch
+import torch.nn as nn
+
+from irc_amd import ops
+from irc_amd.bert import BertModel
+from irc_amd.lstm_head import LSTMHead, seq2vec as head_seq2vec
+from irc_amd.tokenizer import load_tokenizer
+
+
+class RetrievalModelWrapper(nn.Module):
+    def __init__(self, base_encoder, criterion, loss_config, use_momentum=True, use_queue=True,
+                 use_LSTM=True, bert_config=None):
+        super().__init__()
+        self.criterion = criterion
+        self.loss_config = loss_config
+        self.use_momentum = self.loss_config["use_momentum"]
+        self.use_queue = self.loss_config["use_queue"]
+        self.use_LSTM = use_LSTM
+
+        self.encoder_q = copy.deepcopy(base_encoder)
+        if self.use_momentum:
+            self.encoder_k = copy.deepcopy(base_encoder)
+            with torch.no_grad():
+                self.encoder_k.flat.copy_(self.encoder_q.flat)
+            self.encoder_k.flat.requires_grad_(False)
+
+        if self.use_queue:
+            self.register_buffer("queue", torch.randn(self.loss_config["dim"],
+                                                      self.loss_config["queue_size"]))
+            self.queue = nn.functional.normalize(self.queue, dim=0)  # host-side init
+            self.register_buffer("queue_ptr", torch.zeros(1, dtype=torch.long))
+            self.add_queue_to_loss = False
+
+        bc = dict(bert_config or {})
+        name = bc.get("name", "bert-base-uncased")
+        self.bert_model = BertModel.from_pretrained(name, config=bc.get("config"),
+                                                    seed=int(bc.get("seed", 0)))
+        self.bert_tokenizer = load_tokenizer(bc.get("vocab"), self.bert_model.config.vocab_size)
+        self.bert_model.eval()
+
+    @torch.no_grad()
+    def bert_extract(self, d1, d2, device):
+        t = self.bert_tokenizer(list(d1) + list(d2), padding=True, truncation=True,
+                                return_tensors="pt")
+        out = self.bert_model.encode(t["input_ids"].to(device), t["attention_mask"].to(device))
+        return out[:len(d1)], out[len(d1):]
+
+    @torch.no_grad()
+    def bert_extract_ids(self, input_ids, attention_mask, n_anchor):
+        """Same as bert_extract for already-tokenised (device) batches."""
+        out = self.bert_model.encode(input_ids, attention_mask)
+        return out[:n_anchor], out[n_anchor:]
+
+    @torch.no_grad()
+    def _momentum_update_key_encoder(self):
+        """theta_k <- m theta_k + (1 - m) theta_q: one fused launch over the flat buffers."""
+        ops.momentum_update(self.encoder_k.flat.detach(), self.encoder_q.flat.detach(),
+                            float(self.loss_config["momentum"]))
+
+    @torch.no_grad()
+    def _dequeue_and_enqueue(self, keys):
+        batch_size = keys.shape[0]
+        if self.loss_config["queue_size"] % batch_size == 0:  # reference rule (:59)
+            ops.enqueue(self.queue, keys.float().contiguous(), self.queue_ptr)
+
+    def forward(self, anchor_sample, positive_sample, device, cluster_result=None, indexes=None):
+        if indexes is not None:
+            indexes = indexes.view(-1)
+        anchor_sample, positive_sample = self.bert_extract(anchor_sample, positive_sample, device)
+        return self.forward_features(anchor_sample, positive_sample, cluster_result, indexes)
+
+    def forward_features(self, anchor_feat, positive_feat, cluster_result=None, indexes=None):
+        """forward() from BERT features on: heads, loss, enqueue."""
+        emb_q = self.seq2vec(anchor_feat)
+        emb_k = self.seq2vec(positive_feat, query=False) if self.use_momentum else \
+            self.seq2vec(positive_feat)
+        queue = None if not self.use_queue or not self.add_queue_to_loss else self.queue
+        loss = self.criterion(emb_q, emb_k, queue, cluster_result, indexes)
+        if self.use_queue and self.training:
+            self._dequeue_and_enqueue(emb_k.detach())
+        return loss
+
+    def ctx2vec(self, context, device):
+        t = self.bert_tokenizer(list(context), padding=True, truncation=True, return_tensors="pt")
+        out = self.bert_model.encode(t["input_ids"].to(device), t["attention_mask"].to(device))
+        return self.seq2vec(out)
+
+    def seq2vec(self, seq, query=True):
+        assert seq.ndim == 3
+        if query:
+            return head_seq2vec(self.encoder_q, seq, grad=True)
+        return head_seq2vec(self.encoder_k, seq, grad=False)
+
+
+__all__ = ["RetrievalModelWrapper", "LSTMHead"]

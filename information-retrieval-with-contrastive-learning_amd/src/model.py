@@ -1,0 +1,65 @@
+"""Drop-in for src/model.py: LSTM head, build_model, get_optimizer, save/load.
+
+``LSTM`` keeps the reference's config keys, parameter names and initialisation
+(src/model.py:7-41) on the flat-buffer head of irc_amd.lstm_head.
+``get_optimizer`` returns the fused Adam over encoder_q's flat buffer
+(model.py:44-58 semantics); checkpoints keep the reference layout
+{Model, Optimizer, Current_step, Args} and file name (model.py:76-99).
+"""
+import torch
+
+from irc_amd.lstm_head import LSTMHead
+from irc_amd.optim import FusedAdam
+from src.contrastor.contrastive_loss import NCELoss
+from src.contrastor.contrastive_module import RetrievalModelWrapper
+
+
+class LSTM(LSTMHead):
+    """nn.LSTM(input, hidden, layers, batch_first, bidirectional) + Linear + Identity."""
+
+
+def get_optimizer(args, model):
+    if args.opt == "adam":
+        return FusedAdam(model.encoder_q,
+                         lr=float(args.config["optimizer"]["Adam"]["learning_rate"]),
+                         betas=tuple(args.config["optimizer"]["Adam"]["betas"]))
+    raise NotImplementedError("--opt sgd is not built yet (Adam is the reference default)")
+
+
+def build_model(args):
+    print("[Runner] - Building contrastive model")
+    loss_config = args.config["loss"][f"{args.loss}"]
+    loss_config["dim"] = args.config["model"]["LSTM"]["output_size"]
+    if args.loss in ["InfoNCE", "ProtoNCE", "HProtoNCE"]:
+        criterion = NCELoss(loss_config)
+    if args.model != "LSTM":
+        raise ValueError(f"unknown model {args.model!r}")
+    bk_model = LSTM(args.config)
+    return RetrievalModelWrapper(bk_model, criterion, loss_config, use_LSTM=True,
+                                 bert_config=args.config.get("bert"))
+
+
+def save_model(model, optimizer, args, current_step):
+    path = f"{args.ckptdir}/{args.sample}_{args.loss}_{args.model}_{current_step}.pth"
+    all_states = {
+        "Model": model.state_dict(),
+        "Optimizer": optimizer.state_dict(),
+        "Current_step": current_step,
+        "Args": args,
+    }
+    torch.save(all_states, path)
+
+
+def load_model(path):
+    # Our own checkpoints hold an argparse.Namespace ("Args"), as the reference's do.
+    ckpt = torch.load(path, map_location="cpu", weights_only=False)
+    args = ckpt["Args"]
+    model = build_model(args)
+    print("[Runner] - Loading model parameters")
+    res = model.load_state_dict(ckpt["Model"], strict=False)
+    missing = [k for k in res.missing_keys if not k.endswith("position_ids")]
+    if missing:
+        raise RuntimeError(f"checkpoint is missing {missing[:8]}")
+    optimizer = get_optimizer(args, model)
+    optimizer.load_state_dict(ckpt["Optimizer"])
+    return args, model, optimizer, ckpt["Current_step"]

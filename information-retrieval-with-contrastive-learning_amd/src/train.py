@@ -1,0 +1,158 @@
+"""Drop-in for src/train.py: the contrastive training loop.
+
+Same loop semantics as the reference (src/train.py:41-201): micro-batches of
+``train.batch_size`` pairs, loss / acml_batch_size, gradient accumulation up to
+``acml_batch_size`` (or a short last batch), clip_grad_norm_(gradient_clipping)
++ optimizer step + momentum update + zero_grad, queue switched on at
+``queue_start_steps``, scalars + checkpoint every ``log_step``, and the OOM
+catch-and-skip (matching "HIP out of memory" as well as the CUDA text).
+
+Differences on purpose: the clip is fused into the optimizer step (no host
+sync); TensorBoard is used when importable, else the scalars are printed.
+"""
+import math
+import os
+import shutil
+
+import numpy as np
+import torch
+from tqdm import tqdm
+
+from src.dataset import get_dataloader
+from src.model import build_model, get_optimizer, load_model, save_model
+
+OOM_MARKERS = ("CUDA out of memory", "HIP out of memory", "out of memory")
+
+
+class _PrintWriter:
+    def __init__(self, logdir):
+        self.logdir = logdir
+
+    def add_scalar(self, tag, value, step):
+        print(f"[{tag}] step {step}: {value:.6f}")
+
+    def close(self):
+        pass
+
+
+def _writer(logdir):
+    try:
+        from torch.utils.tensorboard import SummaryWriter
+
+        return SummaryWriter(logdir)
+    except Exception:
+        return _PrintWriter(logdir)
+
+
+class TrainState:
+    """One training run's mutable state, stepped one micro-batch at a time.
+
+    Shared by ``train`` (below) and the parity tests / bench, which drive it with
+    pre-tokenised batches."""
+
+    def __init__(self, args, model, optimizer, init_step=0):
+        self.args = args
+        self.model = model
+        self.optimizer = optimizer
+        self.cfg = args.config
+        self.acml = int(self.cfg["train"]["acml_batch_size"])
+        self.bsz = int(self.cfg["train"]["batch_size"])
+        assert self.acml % self.bsz == 0
+        self.max_norm = float(self.cfg["optimizer"].get("gradient_clipping", 1.0))
+        self.step_sum = init_step
+        self.batch_size = 0
+        self.loss_record = []
+        self.loss_sum = 0.0
+        self.grad_norm = None
+
+    def _maybe_enable_queue(self):
+        m = self.model
+        if m.use_queue and self.step_sum >= self.cfg["loss"][self.args.loss]["queue_start_steps"] \
+                and not m.add_queue_to_loss:
+            m.add_queue_to_loss = True
+
+    def micro_batch(self, n_pairs, forward_fn, sync_loss=True):
+        """forward_fn() -> loss tensor of this micro-batch (model(...) call)."""
+        self._maybe_enable_queue()
+        self.batch_size += n_pairs
+        loss = forward_fn() / self.acml
+        loss.backward()
+        if sync_loss:
+            self.loss_sum += loss.item()  # the reference logs every micro-batch (train.py:148)
+        else:
+            self.loss_sum = self.loss_sum + loss.detach()
+        stepped = False
+        if self.batch_size == self.acml or n_pairs != self.bsz:
+            self.grad_norm = self.optimizer.clip_and_step(self.max_norm)
+            if self.model.use_momentum:
+                self.model._momentum_update_key_encoder()
+            self.optimizer.zero_grad()
+            self.loss_record.append(self.loss_sum)
+            self.step_sum += 1
+            self.batch_size = 0
+            self.loss_sum = 0.0
+            stepped = True
+        return loss, stepped
+
+
+def train(args):
+    if args.ckpt is None:
+        model = build_model(args)
+        optimizer = get_optimizer(args, model)
+        init_step = 0
+    else:
+        _, model, optimizer, init_step = load_model(args.ckpt)
+    model = model.to(args.device)
+    optimizer.to(args.device)
+    model.train()
+
+    train_loader = get_dataloader(args, train=True)
+    if args.loss in ["ProtoNCE", "HProtoNCE"]:
+        raise NotImplementedError("ProtoNCE/HProtoNCE: next row (SURVEY.md 8f); use InfoNCE")
+    cluster_result = None
+
+    args.logdir = f"{args.logdir}/{args.loss}_{args.model}"
+    if os.path.isdir(args.logdir):
+        shutil.rmtree(args.logdir)
+    os.makedirs(args.logdir)
+    log = _writer(args.logdir)
+    os.makedirs(args.ckptdir, exist_ok=True)
+
+    st = TrainState(args, model, optimizer, init_step)
+    total_steps = args.config["train"]["total_steps"]
+    log_step = int(args.config["train"]["log_step"])
+    print("[Runner] - Start training")
+    pbar = tqdm(initial=init_step, total=total_steps, dynamic_ncols=True)
+
+    while st.step_sum < total_steps:
+        for batch in train_loader:
+            try:
+                indexes, anchor_sample, positive_sample = batch
+                _, stepped = st.micro_batch(
+                    len(indexes),
+                    lambda: model(anchor_sample, positive_sample, args.device, cluster_result,
+                                  indexes))
+                if stepped:
+                    pbar.update(1)
+                    if st.step_sum % log_step == 0:
+                        loss_avg = float(np.mean(st.loss_record))
+                        st.loss_record = []
+                        grad_norm = float(st.grad_norm[0].item())
+                        if math.isnan(grad_norm) or math.isinf(grad_norm):
+                            print(f"[Runner] - Error : grad norm is nan/inf at step {st.step_sum}")
+                        log.add_scalar("train_loss", loss_avg, st.step_sum)
+                        log.add_scalar("grad_norm", grad_norm, st.step_sum)
+                        pbar.set_description("Train_Loss %.5f" % (loss_avg))
+                        print("Train_Loss %.5f" % (loss_avg))
+                        save_model(model, optimizer, args, st.step_sum)
+            except RuntimeError as e:
+                if not any(m in str(e) for m in OOM_MARKERS):
+                    raise
+                print("[Runner] - HIP out of memory at step: ", st.step_sum)
+                optimizer.zero_grad()
+                torch.cuda.empty_cache()
+            if st.step_sum >= total_steps:
+                break
+
+    pbar.close()
+    log.close()

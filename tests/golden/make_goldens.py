@@ -173,6 +173,23 @@ def gen_seq2vec(out, tmp):
     print("seq2vec:", len(res), "arrays")
 
 
+def gen_lstm_init(out):
+    """Initial parameters of the reference LSTM head for fixed seeds (model.py:8-36):
+    pins the RNG-consumption order of nn.LSTM + Linear + init_weights."""
+    from src.model import LSTM
+
+    res = {}
+    for tag, (inp, hid, layers, outd, seed) in {"s": (24, 16, 2, 8, 1337),
+                                                 "m": (64, 32, 3, 16, 7)}.items():
+        torch.manual_seed(seed)
+        m = LSTM(_lstm_cfg(inp, hid, layers, outd))
+        res[f"{tag}_dims"] = np.array([inp, hid, layers, outd, seed])
+        for name, prm in m.named_parameters():
+            res[f"{tag}_{name}"] = _np(prm)
+    np.savez_compressed(os.path.join(out, "lstm_init.npz"), **res)
+    print("lstm init:", len(res), "arrays")
+
+
 def gen_bert(out, tmp):
     """HF BertModel last_hidden_state with padding (contrastive_module.py:36-41)."""
     from transformers import BertConfig, BertModel
@@ -361,7 +378,13 @@ def gen_train_traj(out, tmp):
 def main():
     _import_ref()
     with tempfile.TemporaryDirectory() as tmp:
+        if len(sys.argv) > 1:  # regenerate selected fixtures only
+            for name in sys.argv[1:]:
+                fn = globals()[f"gen_{name}"]
+                fn(HERE, tmp) if fn.__code__.co_argcount == 2 else fn(HERE)
+            return
         gen_nce(HERE)
+        gen_lstm_init(HERE)
         gen_seq2vec(HERE, tmp)
         gen_bert(HERE, tmp)
         gen_scan(HERE)

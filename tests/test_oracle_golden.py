@@ -133,3 +133,23 @@ def test_enqueue_rule():
     assert ptr == 0 and (q2[:, 8:] == 1).all()
     q3, ptr = O.dequeue_and_enqueue(queue, 0, np.ones((5, 4)))  # 12 % 5 != 0: no update
     assert ptr == 0 and (q3 == 0).all()
+
+
+def test_lstm_head_init_matches_reference_rng_order():
+    """irc_amd.lstm_head.LSTMHead(config) after torch.manual_seed(s) starts from the
+    exact parameters the reference's LSTM(config) gets (host-side init)."""
+    import torch
+
+    from irc_amd.lstm_head import LSTMHead
+
+    g = load_golden("lstm_init.npz")
+    for tag in ("s", "m"):
+        inp, hid, layers, outd, seed = (int(x) for x in g[f"{tag}_dims"])
+        cfg = {"model": {"LSTM": {"num_layers": layers, "bidirectional": True,
+                                  "input_size": inp, "hidden_size": hid, "output_size": outd,
+                                  "activation": "Identity"}}}
+        torch.manual_seed(seed)
+        h = LSTMHead(cfg)
+        sd = h.state_dict()
+        for name, _ in h.specs:
+            np.testing.assert_array_equal(sd[name].numpy(), g[f"{tag}_{name}"], err_msg=name)
