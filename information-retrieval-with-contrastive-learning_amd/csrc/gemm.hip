@@ -62,6 +62,7 @@ struct Args {
   int64_t sA, sB, sC, sR, sBias;  // batch strides (elements)
   float alpha;
   int accumulate;  // C += result (fp32 C only)
+  int vec_a, vec_b;  // operand rows 16-byte aligned: vector staging allowed
 };
 
 // Load one [rows x BK] slab of an operand into registers (as 16-byte vectors).
@@ -75,8 +76,10 @@ struct Slab {
   static constexpr int PER_T = NVEC / NT;
   u16x8 v[PER_T];
 
+  // vec: rows start 16-byte aligned (ld and base), so whole 16-byte vectors may
+  // be loaded; otherwise every element is loaded on its own.
   __device__ __forceinline__ void load(const T* base, int64_t ld, int row0, int nrows, int k0,
-                                       int K) {
+                                       int K, bool vec) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < PER_T; ++i) {
@@ -92,7 +95,7 @@ struct Slab {
       const int gr = row0 + r, gk = k0 + kk;
       u16x8 val = (u16x8)0;
       if (LAYOUT == ROW) {
-        if (gr < nrows && gk + VEC <= K) {
+        if (vec && gr < nrows && gk + VEC <= K) {
           val = *reinterpret_cast<const u16x8*>(base + (int64_t)gr * ld + gk);
         } else if (gr < nrows) {
           T tmp[VEC];
@@ -101,7 +104,7 @@ struct Slab {
           val = *reinterpret_cast<u16x8*>(tmp);
         }
       } else {
-        if (gk < K && gr + VEC <= nrows) {
+        if (vec && gk < K && gr + VEC <= nrows) {
           val = *reinterpret_cast<const u16x8*>(base + (int64_t)gk * ld + gr);
         } else if (gk < K) {
           T tmp[VEC];
@@ -174,8 +177,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
   Slab<TI, LA> sa;
   Slab<TI, LB> sb;
   const int nk = (g.K + BK - 1) / BK;
-  sa.load(A, g.lda, m0, g.M, 0, g.K);
-  sb.load(B, g.ldb, n0, g.N, 0, g.K);
+  sa.load(A, g.lda, m0, g.M, 0, g.K, g.vec_a);
+  sb.load(B, g.ldb, n0, g.N, 0, g.K, g.vec_b);
   sa.store(lds[0][0]);
   sb.store(lds[0][1]);
   __syncthreads();
@@ -183,8 +186,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      sa.load(A, g.lda, m0, g.M, (kt + 1) * BK, g.K);
-      sb.load(B, g.ldb, n0, g.N, (kt + 1) * BK, g.K);
+      sa.load(A, g.lda, m0, g.M, (kt + 1) * BK, g.K, g.vec_a);
+      sb.load(B, g.ldb, n0, g.N, (kt + 1) * BK, g.K, g.vec_b);
     }
     const char* la = lds[cur][0];
     const char* lb = lds[cur][1];
@@ -328,14 +331,14 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
   IRC_REQUIRE(epilogue >= 0 && epilogue <= 4, "gemm: bad epilogue");
   IRC_REQUIRE(!(epilogue >= 1 && epilogue <= 3) || bias, "gemm: epilogue needs bias");
   IRC_REQUIRE(!(epilogue == 3 || epilogue == 4) || R, "gemm: epilogue needs residual");
+  // 16-byte vector staging needs every row start 16-byte aligned; otherwise the
+  // operand is staged element by element (same results, slower).
   const int vec = in_dtype == 0 ? 8 : 4;
-  IRC_REQUIRE((a_layout == 0 ? lda : lda) % vec == 0 && ldb % vec == 0,
-              "gemm: leading dimensions must be multiples of %d elements", vec);
-  IRC_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0,
-              "gemm: A and B must be 16-byte aligned");
+  const int vec_a = lda % vec == 0 && strideA % vec == 0 && ((uintptr_t)A % 16) == 0;
+  const int vec_b = ldb % vec == 0 && strideB % vec == 0 && ((uintptr_t)B % 16) == 0;
   if (M == 0 || N == 0) return IRC_OK;
   gemm::Args g{A, B, C, bias, R, (int)M, (int)N, (int)K, lda, ldb, ldc, ldr,
-               strideA, strideB, strideC, strideR, strideBias, alpha, accumulate};
+               strideA, strideB, strideC, strideR, strideBias, alpha, accumulate, vec_a, vec_b};
   hipStream_t st = as_stream(stream);
   if (in_dtype == 0 && out_dtype == 0)
     return gemm::by_layout<unsigned short, unsigned short>(a_layout, b_layout, epilogue, g,

@@ -32,7 +32,10 @@ class _InfoNCE(torch.autograd.Function):
     def forward(ctx, q, k, queue, T):
         q = q.float().contiguous()
         k = k.float().contiguous()
-        qu = queue.float().contiguous() if queue is not None else None
+        # snapshot, as the reference's queue.clone().detach() (contrastive_loss.py:80):
+        # the enqueue after forward() overwrites the live buffer before backward runs
+        qu = queue.detach().float().clone(memory_format=torch.contiguous_format) \
+            if queue is not None else None
         N = q.shape[0]
         F, S, LQ = _logits(q, k, qu)
         Kq = LQ.shape[1] if LQ is not None else 0

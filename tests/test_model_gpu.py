@@ -138,7 +138,7 @@ def test_optimizer_ops_vs_oracle(gpu):
     pk = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(gpu)
     ref = O.momentum_update(pk.cpu().numpy(), p, 0.9)
     ops.momentum_update(pk, torch.from_numpy(p).to(gpu), 0.9)
-    np.testing.assert_allclose(pk.cpu().numpy(), ref, rtol=1e-6)
+    np.testing.assert_allclose(pk.cpu().numpy(), ref, rtol=1e-6, atol=1e-6)
 
 
 def test_enqueue_device_pointer(gpu):
