@@ -1,16 +1,23 @@
 """Benchmark of the contrastive-training + dense-retrieval hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--part scan|train|all]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--part all|train|scan]
 
-For N>1 the driver launches one process per GPU with torch.distributed.run; each
-rank reads RANK/LOCAL_RANK/WORLD_SIZE from the environment and RCCL (backend
-"nccl") carries the collectives.  Rank 0 prints ONE JSON line.
+For N>1 the driver launches one process per GPU (torch.distributed.run); each
+rank reads RANK/LOCAL_RANK/WORLD_SIZE and RCCL (backend "nccl") carries the
+collectives.  Rank 0 prints ONE JSON line.
 
-Retrieval leg: each rank keeps a 100k-doc shard (D=768 bf16,
-unit-norm Gaussian, seed 2024+rank) resident in HBM; one step = one batch of
-Q=256 query embeddings all-gathered to every rank, scanned against the local
-shard and reduced to the global top-100 (scaling: weak -- the per-GPU shard is
-fixed, the global corpus grows with N).
+Metric (BASELINE.json): "query-doc pairs/sec (train) + queries/sec @ top-k over
+N docs".  `value` = training pairs/s (whole job); `retrieval` = queries/s.
+
+* Training step (config C2): frozen BERT-base encoder (bf16 MFMA)
+  over 2x256 synthetic sequences (L=64, token ids uniform in [5, 30522), seeded)
+  -> 3-layer BiLSTM head 768->256x2->128 q fwd+bwd and momentum-encoder k fwd
+  -> InfoNCE with the 12544-key queue -> clip + Adam + momentum update + enqueue.
+  One step = 256 (anchor, positive) pairs.  N>1: data-parallel, each rank its
+  own 256 pairs, gradients summed over RCCL before the step (scaling: weak).
+* Retrieval (C2): each rank keeps a 100k-doc shard (D=768 bf16 unit-norm,
+  seed 2024+rank) in HBM; one batch = 256 query embeddings all-gathered,
+  scanned against every shard, reduced to the global top-100.
 """
 from __future__ import annotations
 
@@ -35,10 +42,9 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA spec
 
-SCAN_N_PER_GPU = 100_000
-SCAN_Q = 256
-SCAN_D = 768
-SCAN_K = 100
+METRIC = "query-doc pairs/sec (train) + queries/sec @ top-k over N docs, 1/2/4/8 GPU"
+TRAIN_B, TRAIN_L, VOCAB = 256, 64, 30522
+SCAN_N_PER_GPU, SCAN_Q, SCAN_D, SCAN_K = 100_000, 256, 768, 100
 
 
 def _cpu_model():
@@ -61,12 +67,10 @@ def _blas_threads():
         return int(os.environ.get("OMP_NUM_THREADS", "1"))
 
 
-def _pmc_traffic(kernel_tag: str):
+def _pmc_traffic(tag: str):
     """HBM bytes per launch from a committed rocprofv3 --pmc summary, if present
     (profiles/pmc_<tag>.json, written by tools/pmc_summary.py)."""
-    p = os.path.join(ROOT, "profiles", f"pmc_{kernel_tag}.json")
-    if not os.path.exists(p):
-        return None
+    p = os.path.join(ROOT, "profiles", f"pmc_{tag}.json")
     try:
         with open(p) as f:
             return float(json.load(f)["hbm_bytes_per_launch"])
@@ -74,11 +78,128 @@ def _pmc_traffic(kernel_tag: str):
         return None
 
 
-def _prof_query(lib, name):
-    tot = ctypes.c_double(0)
-    cnt = ctypes.c_int64(0)
-    lib.irc_prof_query(name.encode(), ctypes.byref(tot), ctypes.byref(cnt))
-    return tot.value, cnt.value
+def _prof(lib, name):
+    tot, cnt, work = ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_double(0)
+    lib.irc_prof_query(name.encode(), ctypes.byref(tot), ctypes.byref(cnt), ctypes.byref(work))
+    return tot.value / 1e3, cnt.value, work.value  # seconds, launches, work
+
+
+def _max_over_ranks(x, dev, world):
+    if world == 1:
+        return x
+    t = torch.tensor([x], device=dev, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def synthetic_batch(n_seq, L, seed):
+    """[CLS] w... [SEP] [PAD]...; lengths uniform in [10, L], one row full length."""
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(5, VOCAB, (n_seq, L), generator=g)
+    lens = torch.randint(10, L + 1, (n_seq,), generator=g)
+    lens[0] = L
+    pos = torch.arange(L)[None]
+    mask = (pos < lens[:, None]).long()
+    ids[:, 0] = 2
+    ids = torch.where(mask.bool(), ids, torch.zeros_like(ids))
+    ids[torch.arange(n_seq), lens - 1] = 3
+    return ids, mask
+
+
+def c2_config():
+    import yaml
+
+    with open(os.path.join(PKG, "config.yaml")) as f:
+        cfg = yaml.safe_load(f)
+    cfg["train"].update(batch_size=TRAIN_B, acml_batch_size=TRAIN_B)
+    return cfg
+
+
+def run_train(args, rank, world, dev):
+    from irc_amd import _lib
+    from src.model import build_model, get_optimizer
+    from src.train import TrainState
+
+    lib = _lib.load()
+    cfg = c2_config()
+    ns = argparse.Namespace(config=cfg, loss="InfoNCE", model="LSTM", opt="adam",
+                            sample="uniform")
+    torch.manual_seed(1337)
+    model = build_model(ns).to(dev).train()
+    model.add_queue_to_loss = True  # steady state (step >= queue_start_steps)
+    opt = get_optimizer(ns, model)
+    st = TrainState(ns, model, opt)
+    if world > 1:
+        st.process_group = dist.group.WORLD
+    ids, mask = synthetic_batch(2 * TRAIN_B, TRAIN_L, 1337 + rank)
+    ids, mask = ids.to(dev), mask.to(dev)
+
+    def step():
+        st.micro_batch(TRAIN_B, lambda: model.forward_features(
+            *model.bert_extract_ids(ids, mask, TRAIN_B)), sync_loss=False)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    lib.irc_prof_reset()
+    lib.irc_prof_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    lib.irc_prof_enable(0)
+    dt = _max_over_ranks(dt, dev, world)
+    g_s, g_n, g_flops = _prof(lib, "gemm_bf16")
+    flops_pair = 2 * model.bert_model.flops_per_sequence(TRAIN_L) + _lstm_flops_per_pair(cfg)
+    pairs = TRAIN_B * args.steps * world
+    achieved = g_flops / g_s / 1e12 if g_s > 0 else None
+    loss = float(st.loss_record[-1]) if st.loss_record else None
+    return model, {
+        "pairs_per_s": pairs / dt,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "loss_last": loss,
+        "flops_per_pair": flops_pair,
+        "step_tflops": pairs * flops_pair / dt / 1e12,
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS,
+                     "unit": "TFLOP/s", "frac": achieved / BF16_PEAK_TFS if achieved else None,
+                     "traffic": _pmc_traffic("gemm_bf16"),
+                     "kernel": "gemm_kernel<bf16> (all GEMM launches of the timed steps)",
+                     "launches_per_step": g_n / args.steps,
+                     "gemm_ms_per_step": g_s * 1e3 / args.steps,
+                     "alg_flops_per_step": g_flops / args.steps},
+    }
+
+
+def _lstm_flops_per_pair(cfg):
+    c = cfg["model"]["LSTM"]
+    H, In, nl = c["hidden_size"], c["input_size"], c["num_layers"]
+    per_tok = sum(2 * 4 * H * ((In if l == 0 else 2 * H) + H) * 2 for l in range(nl))
+    return 4 * per_tok * TRAIN_L  # q fwd+bwd (3x) + k fwd (1x)
+
+
+def cpu_baseline_train(model, budget_s):
+    from oracle import bench_cpu
+
+    cfgb = model.bert_model.config
+    bert_w = {k: v.detach().float().cpu().numpy() for k, v in model.bert_model.state_dict().items()}
+    hp = {n: model.encoder_q.view(n).cpu().numpy() for n, _ in model.encoder_q.specs}
+    queue = model.queue.detach().cpu().numpy()
+    n_pairs = 4
+    ids, mask = synthetic_batch(2 * n_pairs, TRAIN_L, 99)
+    v, reps = bench_cpu.train_step_baseline(
+        bert_w, cfgb.num_hidden_layers, cfgb.num_attention_heads, hp,
+        model.encoder_q.num_layers, queue, ids.numpy(), mask.numpy(), budget_s=budget_s)
+    return {"value": v, "unit": "pairs/s", "cores": _blas_threads(), "kind": "port",
+            "cpu_model": _cpu_model(),
+            "sample": f"{reps} x one training micro-batch of {n_pairs} pairs at the C2 shapes "
+                      f"(BERT-base L={TRAIN_L}, 3-layer BiLSTM 768->256->128, queue 12544), "
+                      "numpy fp32 oracle"}
 
 
 def run_scan(args, rank, world, dev):
@@ -90,9 +211,7 @@ def run_scan(args, rank, world, dev):
     shard = shard.bfloat16().to(dev)
     gq = torch.Generator().manual_seed(7)
     allq = torch.nn.functional.normalize(torch.randn(SCAN_Q, SCAN_D, generator=gq)).bfloat16()
-    lo = rank * SCAN_Q // world
-    hi = (rank + 1) * SCAN_Q // world
-    myq = allq[lo:hi].to(dev)
+    myq = allq[rank * SCAN_Q // world:(rank + 1) * SCAN_Q // world].to(dev)
     index = retrieval.ShardedDenseIndex(shard, doc_offset=rank * SCAN_N_PER_GPU,
                                         group=dist.group.WORLD if world > 1 else None)
     for _ in range(args.warmup):
@@ -111,51 +230,37 @@ def run_scan(args, rank, world, dev):
         dist.barrier()
     dt = time.perf_counter() - t0
     lib.irc_prof_enable(0)
-    ktot, kcnt = _prof_query(lib, "scan_filter")
-    if world > 1:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    kavg_s = (ktot / 1e3) / max(kcnt, 1)
-    # algorithmic bytes of one filter-scan launch: the shard once + the queries once
-    alg_bytes = SCAN_N_PER_GPU * SCAN_D * 2 + SCAN_Q * SCAN_D * 2
-    achieved = alg_bytes / kavg_s / 1e9 if kcnt else None
-    traffic = _pmc_traffic("scan_filter")
-    res = {
-        "qps": SCAN_Q * args.steps / dt,
-        "ms_per_step": dt * 1e3 / args.steps,
-        "kernel_avg_us": kavg_s * 1e6,
+    dt = _max_over_ranks(dt, dev, world)
+    k_s, k_n, k_bytes = _prof(lib, "scan_filter")
+    kavg = k_s / max(k_n, 1)
+    achieved = (k_bytes / max(k_n, 1)) / kavg / 1e9 if k_n else None
+    return {
+        "value": SCAN_Q * args.steps / dt, "unit": "queries/s",
+        "ms_per_batch": dt * 1e3 / args.steps,
+        "docs_total": SCAN_N_PER_GPU * world, "queries": SCAN_Q, "dim": SCAN_D, "k": SCAN_K,
+        "query_doc_pairs_per_s": SCAN_Q * SCAN_N_PER_GPU * world * args.steps / dt,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                     "traffic": traffic, "kernel": "scan_tile_kernel<768,4,KEYS> (filter pass)",
-                     "alg_bytes_per_launch": alg_bytes,
-                     "mfma_tflops": 2 * SCAN_Q * SCAN_N_PER_GPU * SCAN_D / kavg_s / 1e12
-                     if kcnt else None},
+                     "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                     "traffic": _pmc_traffic("scan_filter"),
+                     "kernel": "scan_tile_kernel<768,4,2,KEYS> (filter pass)",
+                     "kernel_avg_us": kavg * 1e6,
+                     "alg_bytes_per_launch": k_bytes / max(k_n, 1),
+                     "mfma_tflops": 2 * SCAN_Q * SCAN_N_PER_GPU * SCAN_D / kavg / 1e12
+                     if k_n else None},
     }
-    return res
 
 
-def cpu_baseline_scan(budget_s: float = 10.0):
-    """The oracle's fp32 scan (reference CPU arithmetic: q @ d.T + closest_docs
-    selection) on the host cores, full C2 shape, repeated for ~budget_s."""
-    from oracle import irc_oracle as O
+def cpu_baseline_scan(budget_s):
+    from oracle import bench_cpu
 
     g = torch.Generator().manual_seed(2024)
     d = torch.nn.functional.normalize(torch.randn(SCAN_N_PER_GPU, SCAN_D, generator=g))
-    d = d.bfloat16().float().numpy()
     gq = torch.Generator().manual_seed(7)
     q = torch.nn.functional.normalize(torch.randn(SCAN_Q, SCAN_D, generator=gq))
-    q = q.bfloat16().float().numpy()
-    O.scan_topk_fast_f32(q[:8], d[:20000], SCAN_K)  # warm BLAS
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        O.scan_topk_fast_f32(q, d, SCAN_K)
-        reps += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": SCAN_Q * reps / dt, "unit": "queries/s", "cores": _blas_threads(),
-            "kind": "port", "cpu_model": _cpu_model(),
+    v, reps = bench_cpu.scan_baseline(q.bfloat16().float().numpy(), d.bfloat16().float().numpy(),
+                                      SCAN_K, budget_s)
+    return {"value": v, "unit": "queries/s", "cores": _blas_threads(), "kind": "port",
+            "cpu_model": _cpu_model(),
             "sample": f"{reps} x full C2 batch (Q={SCAN_Q}, N={SCAN_N_PER_GPU}, D={SCAN_D}, "
                       f"k={SCAN_K}), numpy fp32 BLAS + exact top-k"}
 
@@ -163,9 +268,9 @@ def cpu_baseline_scan(budget_s: float = 10.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--part", default="scan", choices=["scan"])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--part", default="all", choices=["all", "train", "scan"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
@@ -179,32 +284,48 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
 
-    scan = run_scan(args, rank, world, dev)
-    cpu = None
+    train = scan = None
+    model = None
+    if args.part in ("all", "train"):
+        model, train = run_train(args, rank, world, dev)
+    if args.part in ("all", "scan"):
+        scan = run_scan(args, rank, world, dev)
+    cpu_t = cpu_s = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_scan(args.cpu_budget)
+        if train is not None:
+            cpu_t = cpu_baseline_train(model, args.cpu_budget)
+        if scan is not None:
+            cpu_s = cpu_baseline_scan(args.cpu_budget)
+    if scan is not None:
+        scan["cpu_baseline"] = cpu_s
     if rank == 0:
+        if train is not None:
+            head = {"value": train["pairs_per_s"], "unit": "pairs/s",
+                    "ms_per_step": train["ms_per_step"], "roofline": train["roofline"],
+                    "cpu_baseline": cpu_t}
+        else:
+            head = {"value": scan["value"], "unit": "queries/s",
+                    "ms_per_step": scan["ms_per_batch"], "roofline": scan["roofline"],
+                    "cpu_baseline": cpu_s}
         line = {
-            "metric": "query-doc pairs/sec (train) + queries/sec @ top-k over N docs, 1/2/4/8 GPU",
-            "value": scan["qps"],
-            "unit": "queries/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": scan["ms_per_step"],
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic (unit-norm Gaussian embeddings, seed 2024+rank)",
-            "config": {"workload": "retrieval: corpus scan + top-k (C2: BERT-base d=768, "
-                                   "100k docs per GPU, 256-query batch, k=100)",
-                       "docs_per_gpu": SCAN_N_PER_GPU, "queries": SCAN_Q, "dim": SCAN_D,
-                       "k": SCAN_K, "parallelism": f"corpus-sharded x{world}"},
-            "roofline": scan["roofline"],
-            "cpu_baseline": cpu,
-            "kernel_avg_us": scan["kernel_avg_us"],
+            "metric": METRIC, "value": head["value"], "unit": head["unit"], "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (seeded token ids / unit-norm Gaussian corpus; random-init "
+                    "BERT-base weights, no checkpoint)",
+            "config": {"workload": "C2: BERT-base bi-encoder (frozen, bf16) + 3-layer BiLSTM "
+                                   "head, 256 pairs/step, L=64, in-batch + 12544-key queue "
+                                   "negatives; retrieval 100k docs/GPU, 256 queries, top-100",
+                       "pairs_per_step_per_gpu": TRAIN_B, "seq_len": TRAIN_L,
+                       "global_batch": TRAIN_B * world,
+                       "parallelism": f"dp{world} (train) / corpus-sharded x{world} (scan)"},
+            "roofline": head["roofline"], "cpu_baseline": head["cpu_baseline"],
         }
+        if train is not None:
+            line["train"] = {k: train[k] for k in ("pairs_per_s", "ms_per_step", "step_tflops",
+                                                   "flops_per_pair", "loss_last")}
+        if scan is not None:
+            line["retrieval"] = scan
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -109,6 +109,30 @@ int irc_lstm_bwd(int dtype, const float* dy, const void* whh, const float* gsave
                  const float* csave, float* dgates, int64_t B, int64_t L, int64_t H,
                  int64_t ndir, irc_stream_t stream);
 
+/* MFMA recurrences (bf16 operands, fp32 gates/state) for the production head
+ * width H = 256: per step gates[32 x 4H] = xp_t + h_{t-1} W_hh^T on
+ * v_mfma_f32_32x32x16_bf16 with h in LDS and W_hh streamed from L2.
+ * irc_lstm_pack: W_ih (fp32 [ndir*4H][In]) -> bf16 with the gate columns of each
+ *   unit interleaved (packed column 4u+g <- original g*H+u) plus the matching
+ *   b_ih + b_hh, and W_hh -> bf16 [ndir][4H][H] and its transpose [ndir][H][4H].
+ * irc_lstm_fwd_mfma: xp_packed = x . wih_packed^T + bias_packed (irc_gemm, fp32),
+ *   hout bf16 [B*L][ndir*H]; gsave/csave (sizes from irc_lstm_mfma_save_floats,
+ *   which 0 = gates, 1 = c; a layout private to these two kernels) and hprev bf16
+ *   [ndir][B*L][H] may be NULL for the no-grad key encoder.
+ * irc_lstm_bwd_mfma: dy fp32 [B*L][ndir*H] -> dgates bf16 [ndir][B*L][4H] in the
+ *   ORIGINAL gate order (the weight-gradient GEMM operand). */
+int irc_lstm_mfma_supported(int64_t H);
+int64_t irc_lstm_mfma_save_floats(int64_t B, int64_t L, int64_t H, int64_t ndir, int which);
+int irc_lstm_pack(const float* wih, const float* bih, const float* bhh, const float* whh,
+                  int64_t In, int64_t H, int64_t ndir, void* wih_packed, float* bias_packed,
+                  void* whh_bf16, void* whhT_bf16, irc_stream_t stream);
+int irc_lstm_fwd_mfma(const float* xp_packed, const void* whh_bf16, void* hout, float* gsave,
+                      float* csave, void* hprev, int64_t B, int64_t L, int64_t H, int64_t ndir,
+                      irc_stream_t stream);
+int irc_lstm_bwd_mfma(const float* dy, const void* whhT_bf16, const float* gsave,
+                      const float* csave, void* dgates, int64_t B, int64_t L, int64_t H,
+                      int64_t ndir, irc_stream_t stream);
+
 /* ------------------------------------------------- seq2vec tail + InfoNCE + optimizer
  * seq2vec mean-over-L (PAD included) + F.normalize (contrastive_module.py:102-112);
  * InfoNCE row log-sum-exp / NLL and softmax gradients (contrastive_loss.py:56-93,
@@ -140,14 +164,18 @@ int irc_enqueue(float* queue, const float* keys, int64_t* ptr, int64_t D, int64_
 int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t stream);
 int irc_axpby(float* out, const float* x, const float* y, float a, float b, int64_t n,
               irc_stream_t stream);
-int irc_colsum(const float* x, float* out, int64_t R, int64_t C, int64_t ldx, int accumulate,
-               float* partial, irc_stream_t stream);
+/* column sums of x [R][C] (dtype 0 bf16, 1 fp32) into fp32 out; partial holds
+ * ceil(R/256)*C floats of scratch (deterministic two-pass order). */
+int irc_colsum(int dtype, const void* x, float* out, int64_t R, int64_t C, int64_t ldx,
+               int accumulate, float* partial, irc_stream_t stream);
 
 /* ------------------------------------------------------------------ profiling
  * HIP-event timing of the dominant kernel of each entry point, recorded on the
- * caller's stream (bench.py's roofline "achieved" figure).  Names: "scan_filter". */
+ * caller's stream (bench.py's roofline "achieved" figure), with the launches'
+ * algorithmic work (flops or bytes).  Names: "scan_filter" (bytes), "gemm_bf16",
+ * "gemm_f32" (flops). */
 int irc_prof_enable(int on);
-int irc_prof_query(const char* name, double* total_ms, int64_t* count);
+int irc_prof_query(const char* name, double* total_ms, int64_t* count, double* work);
 int irc_prof_reset(void);
 
 #ifdef __cplusplus

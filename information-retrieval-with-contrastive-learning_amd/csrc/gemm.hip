@@ -286,7 +286,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
 template <typename TI, typename TO, int LA, int LB, int EPI>
 static int launch(const Args& g, int batch, hipStream_t st) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  prof_begin(st);
   hipLaunchKernelGGL((gemm_kernel<TI, TO, LA, LB, EPI>), dim3(tiles, batch), dim3(NT), 0, st, g);
+  prof_end(sizeof(TI) == 2 ? "gemm_bf16" : "gemm_f32", st, 2.0 * g.M * g.N * g.K * batch);
   return check_launch("gemm_kernel");
 }
 

@@ -47,6 +47,7 @@ struct ProfRec {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
   double total_ms = 0;
   int64_t count = 0;
+  double work = 0;  // algorithmic flops or bytes of the recorded launches
 };
 static std::unordered_map<std::string, ProfRec> g_prof_tab;
 static thread_local hipEvent_t g_open_ev = nullptr;
@@ -59,13 +60,15 @@ void prof_begin(hipStream_t st) {
   hipEventRecord(g_open_ev, st);
 }
 
-void prof_end(const char* name, hipStream_t st) {
+void prof_end(const char* name, hipStream_t st, double work) {
   if (!g_prof || !g_open_ev) return;
   hipEvent_t e;
   hipEventCreate(&e);
   hipEventRecord(e, st);
   std::lock_guard<std::mutex> lk(g_prof_mu);
-  g_prof_tab[name].pending.emplace_back(g_open_ev, e);
+  ProfRec& r = g_prof_tab[name];
+  r.pending.emplace_back(g_open_ev, e);
+  r.work += work;
   g_open_ev = nullptr;
 }
 
@@ -77,14 +80,17 @@ extern "C" int irc_prof_enable(int on) {
 }
 
 // Synchronises the recorded events of `name` and returns accumulated time/count.
-extern "C" int irc_prof_query(const char* name, double* total_ms, int64_t* count) {
+extern "C" int irc_prof_query(const char* name, double* total_ms, int64_t* count,
+                              double* work) {
   std::lock_guard<std::mutex> lk(irc::g_prof_mu);
   auto it = irc::g_prof_tab.find(name);
   if (it == irc::g_prof_tab.end()) {
     *total_ms = 0;
     *count = 0;
+    if (work) *work = 0;
     return IRC_OK;
   }
+  if (work) *work = it->second.work;
   for (auto& pr : it->second.pending) {
     hipEventSynchronize(pr.second);
     float ms = 0;

@@ -740,7 +740,7 @@ extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, i
   prof_begin(st);
   rc = dispatch_tile<KEYS>(D, p, p.g_f, qs, ds, (int)Q, N, 1, p.tpw_f, base,
                            p.two_phase ? thr : nullptr, keys, cnt, p.cap_f, nullptr, st);
-  prof_end("scan_filter", st);
+  prof_end("scan_filter", st, (double)N * D * 2 + (double)Q * D * 2);  // algorithmic bytes
   if (rc) return rc;
   RegionSource s2{keys, cnt, p.g_f, p.qpad, p.cap_f, 2 * p.ks};
   hipLaunchKernelGGL((select_kernel<RegionSource>), dim3(Q), dim3(SEL_NT), 0, st, s2, (int)k,

@@ -244,7 +244,8 @@ __global__ void cast_bf16_kernel(const float* __restrict__ x, unsigned short* __
 // Column sums in two deterministic passes: partial[chunk][c] over a fixed row
 // chunk (grid.y), then out[c] (+)= sum over chunks in order.
 constexpr int COLSUM_ROWS = 256;
-__global__ void colsum_partial_kernel(const float* __restrict__ x, float* __restrict__ partial,
+template <typename T>
+__global__ void colsum_partial_kernel(const T* __restrict__ x, float* __restrict__ partial,
                                       int64_t R, int C, int64_t ldx) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -252,7 +253,7 @@ __global__ void colsum_partial_kernel(const float* __restrict__ x, float* __rest
   int64_t r1 = r0 + COLSUM_ROWS;
   if (r1 > R) r1 = R;
   float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) s += x[r * ldx + c];
+  for (int64_t r = r0; r < r1; ++r) s += ldf(x, r * ldx + c);
   partial[(int64_t)blockIdx.y * C + c] = s;
 }
 
@@ -396,14 +397,17 @@ extern "C" int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t st
 }
 
 // partial: workspace of >= ceil(R / 256) * C floats.
-extern "C" int irc_colsum(const float* x, float* out, int64_t R, int64_t C, int64_t ldx,
+extern "C" int irc_colsum(int dtype, const void* x, float* out, int64_t R, int64_t C, int64_t ldx,
                           int accumulate, float* partial, irc_stream_t stream) {
   if (C == 0) return IRC_OK;
   const int64_t nch = (R + COLSUM_ROWS - 1) / COLSUM_ROWS;
   hipStream_t st = as_stream(stream);
-  if (nch > 0)
-    hipLaunchKernelGGL(colsum_partial_kernel, dim3(nblk(C, 64), (unsigned)nch), dim3(64), 0, st, x,
-                       partial, R, (int)C, ldx);
+  if (nch > 0 && dtype == 0)
+    hipLaunchKernelGGL(colsum_partial_kernel<unsigned short>, dim3(nblk(C, 64), (unsigned)nch),
+                       dim3(64), 0, st, (const unsigned short*)x, partial, R, (int)C, ldx);
+  else if (nch > 0)
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3(nblk(C, 64), (unsigned)nch), dim3(64), 0,
+                       st, (const float*)x, partial, R, (int)C, ldx);
   hipLaunchKernelGGL(colsum_final_kernel, dim3(nblk(C)), dim3(256), 0, st, partial, out, (int)nch,
                      (int)C, accumulate);
   return check_launch("colsum");

@@ -35,6 +35,11 @@ SIGNATURES = {
     "irc_attention": (I32, [I32, P, P, P, I64, I64, I64, I64, P]),
     "irc_lstm_fwd": (I32, [I32, P, P, P, P, P, P, I64, I64, I64, I64, P]),
     "irc_lstm_bwd": (I32, [I32, P, P, P, P, P, I64, I64, I64, I64, P]),
+    "irc_lstm_mfma_supported": (I32, [I64]),
+    "irc_lstm_mfma_save_floats": (I64, [I64, I64, I64, I64, I32]),
+    "irc_lstm_pack": (I32, [P, P, P, P, I64, I64, I64, P, P, P, P, P]),
+    "irc_lstm_fwd_mfma": (I32, [P, P, P, P, P, P, I64, I64, I64, I64, P]),
+    "irc_lstm_bwd_mfma": (I32, [P, P, P, P, P, I64, I64, I64, I64, P]),
     "irc_mean_rows": (I32, [I32, P, P, I64, I64, I64, I64, P]),
     "irc_bcast_rows": (I32, [P, P, I64, I64, I64, F32, P]),
     "irc_l2norm_fwd": (I32, [P, P, P, I64, I64, F32, P]),
@@ -48,9 +53,10 @@ SIGNATURES = {
     "irc_momentum_update": (I32, [P, P, I64, F32, P]),
     "irc_enqueue": (I32, [P, P, P, I64, I64, I64, P]),
     "irc_cast_bf16": (I32, [P, P, I64, P]),
-    "irc_colsum": (I32, [P, P, I64, I64, I64, I32, P, P]),
+    "irc_colsum": (I32, [I32, P, P, I64, I64, I64, I32, P, P]),
     "irc_prof_enable": (I32, [I32]),
-    "irc_prof_query": (I32, [_c.c_char_p, _c.POINTER(_c.c_double), _c.POINTER(I64)]),
+    "irc_prof_query": (I32, [_c.c_char_p, _c.POINTER(_c.c_double), _c.POINTER(I64),
+                             _c.POINTER(_c.c_double)]),
     "irc_prof_reset": (I32, []),
 }
 

@@ -13,7 +13,9 @@ Gradients go to a parallel flat buffer (``flat_grad``); each named parameter's
 ``.grad`` is a view of it.
 
 Forward (per layer): xp = x W_ih^T + (b_ih + b_hh) for both directions in one
-GEMM -> recurrence kernel -> next layer.  Head: mean over positions of the top
+GEMM -> recurrence kernel -> next layer.  In bf16 mode at H = 256 the recurrence
+runs on MFMA (csrc/lstm_mfma.hip; W_ih packed so each unit's four gates are
+adjacent), otherwise on the VALU kernels (csrc/lstm.hip).  Head: mean over positions of the top
 layer, then the Linear (mean and Linear commute exactly in real arithmetic),
 then L2 normalisation.  Backward: l2norm bwd -> Linear grads -> broadcast /L ->
 per layer BPTT kernel -> weight-gradient GEMMs over all (b, t).
@@ -166,6 +168,37 @@ class LSTMHead(nn.Module):
             whh = ops.cast_bf16(whh)
         return wih, whh, bias
 
+    def _layer_fp32(self, l):
+        """fp32 views (W_ih [ndir*4H, In], b_ih, b_hh [ndir*4H], W_hh [ndir*4H, H])."""
+        H, nd = self.hidden, self.ndir
+        in_l = self.input_size if l == 0 else H * nd
+        flat = self.flat.detach()
+        o = self.offsets
+        wih = flat[o[f"lstm.weight_ih_l{l}"]:][:nd * 4 * H * in_l].view(nd * 4 * H, in_l)
+        whh = flat[o[f"lstm.weight_hh_l{l}"]:][:nd * 4 * H * H].view(nd * 4 * H, H)
+        bih = flat[o[f"lstm.bias_ih_l{l}"]:][:nd * 4 * H]
+        bhh = flat[o[f"lstm.bias_hh_l{l}"]:][:nd * 4 * H]
+        return wih, bih, bhh, whh
+
+    def _use_mfma(self, dt):
+        return dt == torch.bfloat16 and ops.lstm_mfma_supported(self.hidden)
+
+    def _layer_fwd(self, l, x, B, L, dt, save):
+        """One BiLSTM layer: (hout, saved-for-BPTT or None)."""
+        H, nd = self.hidden, self.ndir
+        if self._use_mfma(dt):
+            # MFMA recurrence: packed W_ih columns so xp is read as per-unit float4s
+            wih, bih, bhh, whh = self._layer_fp32(l)
+            wp, bp, w, wT = ops.lstm_pack(wih, bih, bhh, whh, H, nd)
+            xp = ops.gemm(x, wp, bias=bp, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
+            hout, gsave, csave, hprev = ops.lstm_fwd_mfma(xp, w, B, L, H, nd, save=save)
+            wih_c = ops.cast_bf16(wih) if (save and l > 0) else None  # dx GEMM operand
+            return hout, ((True, x, wih_c, wT, gsave, csave, hprev) if save else None)
+        wih, whh, bias = self._layer_weights(l, dt)
+        xp = ops.gemm(x, wih, bias=bias, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
+        hout, gsave, csave, hprev = ops.lstm_fwd(xp, whh, B, L, H, nd, dt, save=save)
+        return hout, ((False, x, wih, whh, gsave, csave, hprev) if save else None)
+
     def forward_compute(self, features: torch.Tensor, save: bool):
         """features [B, L, In] -> (emb [B, D] fp32 unit-norm, saved state or None)."""
         B, L, In = features.shape
@@ -179,12 +212,8 @@ class LSTMHead(nn.Module):
         x = x.contiguous()
         layers = []
         for l in range(self.num_layers):
-            wih, whh, bias = self._layer_weights(l, dt)
-            xp = ops.gemm(x, wih, bias=bias, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
-            hout, gsave, csave, hprev = ops.lstm_fwd(xp, whh, B, L, H, nd, dt, save=save)
-            if save:
-                layers.append((x, wih, whh, gsave, csave, hprev))
-            x = hout
+            x, st = self._layer_fwd(l, x, B, L, dt, save)
+            layers.append(st)
         mh = ops.mean_rows(x, B, L, nd * H)  # [B, 2H] fp32
         wl = self.view("scaling_layer.0.weight")
         bl = self.view("scaling_layer.0.bias")
@@ -205,9 +234,12 @@ class LSTMHead(nn.Module):
         dmh = ops.gemm(dm, self.view("scaling_layer.0.weight"), b_is_nk=False)  # [B, 2H]
         dy = ops.bcast_rows(dmh, B, L, 1.0 / L)  # [B*L, 2H] fp32
         for l in range(self.num_layers - 1, -1, -1):
-            x, wih, whh, gsave, csave, hprev = layers[l]
-            dg = ops.lstm_bwd(dy, whh, gsave, csave, B, L, H, nd)  # [nd, B*L, 4H] fp32
-            dgc = ops.cast_bf16(dg) if x.dtype == torch.bfloat16 else dg
+            mfma, x, wih, whh, gsave, csave, hprev = layers[l]
+            if mfma:  # dgates come out in bf16, ready for the weight-gradient GEMMs
+                dg = dgc = ops.lstm_bwd_mfma(dy, whh, gsave, csave, B, L, H, nd)
+            else:
+                dg = ops.lstm_bwd(dy, whh, gsave, csave, B, L, H, nd)  # [nd, B*L, 4H] fp32
+                dgc = ops.cast_bf16(dg) if x.dtype == torch.bfloat16 else dg
             in_l = x.shape[1]
             dx = None
             for d in range(nd):
@@ -231,9 +263,7 @@ class LSTMHead(nn.Module):
         dt = compute_dtype()
         x = features.reshape(B * L, In).to(dt).contiguous()
         for l in range(self.num_layers):
-            wih, whh, bias = self._layer_weights(l, dt)
-            xp = ops.gemm(x, wih, bias=bias, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
-            x, _, _, _ = ops.lstm_fwd(xp, whh, B, L, self.hidden, self.ndir, dt, save=False)
+            x, _ = self._layer_fwd(l, x, B, L, dt, save=False)
         wl = self.view("scaling_layer.0.weight")
         bl = self.view("scaling_layer.0.bias")
         xf = x if x.dtype == torch.float32 else x.float()

@@ -107,6 +107,49 @@ def lstm_bwd(dy, whh, gsave, csave, B, L, H, ndir):
     return dg
 
 
+def lstm_mfma_supported(H):
+    return bool(_lib.load().irc_lstm_mfma_supported(H))
+
+
+def lstm_pack(wih, bih, bhh, whh, H, ndir):
+    """fp32 weights of one layer -> (wih_packed bf16, bias_packed fp32, whh bf16, whhT bf16)."""
+    require_hip(wih, bih, bhh, whh)
+    dev = wih.device
+    In = wih.shape[1]
+    wp = torch.empty((ndir * 4 * H, In), dtype=BF16, device=dev)
+    bp = torch.empty((ndir * 4 * H,), dtype=F32, device=dev)
+    w = torch.empty((ndir, 4 * H, H), dtype=BF16, device=dev)
+    wT = torch.empty((ndir, H, 4 * H), dtype=BF16, device=dev)
+    _lib.call("irc_lstm_pack", ptr(wih), ptr(bih), ptr(bhh), ptr(whh), In, H, ndir, ptr(wp),
+              ptr(bp), ptr(w), ptr(wT), stream_ptr(dev))
+    return wp, bp, w, wT
+
+
+def lstm_fwd_mfma(xp_packed, whh_bf16, B, L, H, ndir, save=True):
+    require_hip(xp_packed, whh_bf16)
+    dev = xp_packed.device
+    lib = _lib.load()
+    hout = torch.empty((B * L, ndir * H), dtype=BF16, device=dev)
+    gsave = csave = hprev = None
+    if save:
+        gsave = torch.empty((lib.irc_lstm_mfma_save_floats(B, L, H, ndir, 0),), dtype=F32,
+                            device=dev)
+        csave = torch.empty((lib.irc_lstm_mfma_save_floats(B, L, H, ndir, 1),), dtype=F32,
+                            device=dev)
+        hprev = torch.empty((ndir, B * L, H), dtype=BF16, device=dev)
+    _lib.call("irc_lstm_fwd_mfma", ptr(xp_packed), ptr(whh_bf16), ptr(hout), ptr(gsave),
+              ptr(csave), ptr(hprev), B, L, H, ndir, stream_ptr(dev))
+    return hout, gsave, csave, hprev
+
+
+def lstm_bwd_mfma(dy, whhT_bf16, gsave, csave, B, L, H, ndir):
+    require_hip(dy, whhT_bf16, gsave, csave)
+    dg = torch.empty((ndir, B * L, 4 * H), dtype=BF16, device=dy.device)
+    _lib.call("irc_lstm_bwd_mfma", ptr(dy), ptr(whhT_bf16), ptr(gsave), ptr(csave), ptr(dg), B, L,
+              H, ndir, stream_ptr(dy.device))
+    return dg
+
+
 def mean_rows(x, B, L, C, ldx=None):
     require_hip(x)
     out = torch.empty((B, C), dtype=F32, device=x.device)
@@ -219,6 +262,6 @@ def colsum(x, out=None, accumulate=False):
     if out is None:
         out = torch.empty((C,), dtype=F32, device=x.device)
     partial = torch.empty((max(1, (R + 255) // 256) * C,), dtype=F32, device=x.device)
-    _lib.call("irc_colsum", ptr(x), ptr(out), R, C, x.stride(0), 1 if accumulate else 0,
+    _lib.call("irc_colsum", _code(x), ptr(x), ptr(out), R, C, x.stride(0), 1 if accumulate else 0,
               ptr(partial), stream_ptr(x.device))
     return out

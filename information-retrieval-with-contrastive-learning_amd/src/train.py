@@ -64,6 +64,10 @@ class TrainState:
         self.loss_record = []
         self.loss_sum = 0.0
         self.grad_norm = None
+        # Data parallel (one process per GPU): the flat encoder_q gradient is summed
+        # over the group with one RCCL all-reduce before the fused clip + Adam, so
+        # every rank applies the identical update.
+        self.process_group = None
 
     def _maybe_enable_queue(self):
         m = self.model
@@ -83,6 +87,10 @@ class TrainState:
             self.loss_sum = self.loss_sum + loss.detach()
         stepped = False
         if self.batch_size == self.acml or n_pairs != self.bsz:
+            if self.process_group is not None:
+                import torch.distributed as dist
+
+                dist.all_reduce(self.model.encoder_q.flat_grad, group=self.process_group)
             self.grad_norm = self.optimizer.clip_and_step(self.max_norm)
             if self.model.use_momentum:
                 self.model._momentum_update_key_encoder()

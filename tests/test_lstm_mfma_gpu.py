@@ -1,0 +1,110 @@
+"""MFMA BiLSTM recurrences (csrc/lstm_mfma.hip) at the production head width
+H = 256 vs the numpy oracle (oracle/irc_oracle.py lstm_head_fwd / seq2vec /
+seq2vec_bwd, which restate nn.LSTM, src/model.py:16-41, and seq2vec,
+contrastive_module.py:102-112) and vs the VALU recurrences at the same precision.
+
+bf16 production mode: W_ih, W_hh and h are bf16 operands, gates / c / accumulation
+fp32.  Tolerances (stated per check): embeddings within 2e-2 absolute (unit
+vectors), per-position head outputs within 3e-2 relative to their max, each
+parameter gradient within 4e-2 relative Frobenius error of the fp64 oracle.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import irc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+H = 256
+
+
+def _head(In, layers, out, dev, seed=0):
+    from irc_amd.lstm_head import LSTMHead
+
+    torch.manual_seed(seed)
+    cfg = {"model": {"LSTM": {"num_layers": layers, "bidirectional": True, "input_size": In,
+                              "hidden_size": H, "output_size": out,
+                              "activation": "Identity"}}}
+    h = LSTMHead(cfg).to(dev)
+    p = {n: v.detach().cpu().numpy().astype(np.float64) for n, v in h.named_flat_params()}
+    return h, p
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.fixture
+def bf16_mode():
+    from irc_amd.precision import get_precision, set_precision
+
+    old = get_precision()
+    set_precision("bf16")
+    yield
+    set_precision(old)
+
+
+@pytest.mark.parametrize("B,L,In,layers", [(40, 9, 64, 2), (5, 1, 32, 1), (64, 16, 128, 1)])
+def test_mfma_forward_vs_oracle(gpu, bf16_mode, B, L, In, layers):
+    from irc_amd import ops
+
+    assert ops.lstm_mfma_supported(H)
+    h, p = _head(In, layers, 48, gpu)
+    assert h._use_mfma(torch.bfloat16)
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((B, L, In)).astype(np.float32)
+    xd = torch.from_numpy(x).to(gpu)
+    y = h(xd).cpu().numpy()
+    y_ref, _ = O.lstm_head_fwd(x.astype(np.float64), p, layers)
+    assert np.abs(y - y_ref).max() <= 3e-2 * np.abs(y_ref).max()
+    emb, _ = h.forward_compute(xd, save=False)
+    e_ref, _ = O.seq2vec(x.astype(np.float64), p, layers)
+    np.testing.assert_allclose(emb.cpu().numpy(), e_ref, atol=2e-2)
+
+
+@pytest.mark.parametrize("B,L,In,layers", [(40, 9, 64, 2), (33, 4, 96, 1)])
+def test_mfma_grads_vs_oracle(gpu, bf16_mode, B, L, In, layers):
+    h, p = _head(In, layers, 32, gpu, seed=3)
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal((B, L, In)).astype(np.float32)
+    demb = rng.standard_normal((B, 32)).astype(np.float32)
+    emb, saved = h.forward_compute(torch.from_numpy(x).to(gpu), save=True)
+    h.flat_grad.zero_()
+    h.backward_compute(saved, torch.from_numpy(demb).to(gpu))
+    _, cache = O.seq2vec(x.astype(np.float64), p, layers)
+    ref = O.seq2vec_bwd(demb.astype(np.float64), p, cache, layers)
+    for name, _ in h.specs:
+        got = h.view(name, h.flat_grad).cpu().numpy()
+        assert _rel(got, ref[name]) <= 4e-2, (name, _rel(got, ref[name]))
+
+
+def test_mfma_matches_valu_same_precision(gpu, bf16_mode, monkeypatch):
+    """Both recurrences see bf16 W and h; they differ only in accumulation order
+    (and hence occasional 1-ulp bf16 roundings of h)."""
+    h, _ = _head(64, 2, 32, gpu, seed=5)
+    rng = np.random.default_rng(4)
+    x = torch.from_numpy(rng.standard_normal((48, 12, 64)).astype(np.float32)).to(gpu)
+    demb = torch.from_numpy(rng.standard_normal((48, 32)).astype(np.float32)).to(gpu)
+
+    def run():
+        e, s = h.forward_compute(x, save=True)
+        h.flat_grad.zero_()
+        h.backward_compute(s, demb)
+        return e.cpu().numpy(), h.flat_grad.cpu().numpy().copy()
+
+    e_m, g_m = run()
+    monkeypatch.setattr(type(h), "_use_mfma", lambda self, dt: False)
+    e_v, g_v = run()
+    np.testing.assert_allclose(e_m, e_v, atol=5e-3)
+    assert _rel(g_m, g_v) <= 2e-2
+
+
+def test_mfma_rejects_unsupported_width(gpu):
+    from irc_amd import _lib, ops
+
+    assert not ops.lstm_mfma_supported(128)
+    w = torch.zeros(8 * 128 * 16, device=gpu)
+    with pytest.raises(_lib.IRCError):
+        ops.lstm_pack(w[:8 * 128 * 16].view(8 * 128, 16), w[:1024], w[:1024],
+                      w[:8 * 128 * 128 // 8].view(-1), 128, 2)
