@@ -80,7 +80,14 @@ int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilog
              int64_t N, int64_t K, float alpha, const void* A, int64_t lda, int64_t strideA,
              const void* B, int64_t ldb, int64_t strideB, const float* bias, int64_t strideBias,
              const void* R, int64_t ldr, int64_t strideR, void* C, int64_t ldc, int64_t strideC,
-             int accumulate, int64_t batch, irc_stream_t stream);
+             int accumulate, int64_t batch, void* workspace, int64_t workspace_bytes,
+             irc_stream_t stream);
+/* Bytes of device workspace irc_gemm would use for a deterministic split-K of
+ * this shape (0: no split).  Split-K is taken only for fp32 C without a fused
+ * epilogue when the output tiles cannot fill the chip (e.g. the LSTM weight
+ * gradients, K = B*L); passing a smaller/NULL workspace disables it. */
+int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M, int64_t N,
+                           int64_t K, int64_t batch);
 
 /* ------------------------------------------------------------- BERT encoder
  * Frozen BERT forward pieces (contrastive_module.py:36-41 -> HF BertModel):
@@ -114,13 +121,15 @@ int irc_lstm_bwd(int dtype, const float* dy, const void* whh, const float* gsave
  * v_mfma_f32_32x32x16_bf16 with h in LDS and W_hh streamed from L2.
  * irc_lstm_pack: W_ih (fp32 [ndir*4H][In]) -> bf16 with the gate columns of each
  *   unit interleaved (packed column 4u+g <- original g*H+u) plus the matching
- *   b_ih + b_hh, and W_hh -> bf16 [ndir][4H][H] and its transpose [ndir][H][4H].
+ *   b_ih + b_hh, and W_hh -> bf16 B-operand fragments for the forward and the
+ *   backward recurrence (4H*H elements per direction each; private layout).
  * irc_lstm_fwd_mfma: xp_packed = x . wih_packed^T + bias_packed (irc_gemm, fp32),
  *   hout bf16 [B*L][ndir*H]; gsave/csave (sizes from irc_lstm_mfma_save_floats,
  *   which 0 = gates, 1 = c; a layout private to these two kernels) and hprev bf16
  *   [ndir][B*L][H] may be NULL for the no-grad key encoder.
- * irc_lstm_bwd_mfma: dy fp32 [B*L][ndir*H] -> dgates bf16 [ndir][B*L][4H] in the
- *   ORIGINAL gate order (the weight-gradient GEMM operand). */
+ * irc_lstm_bwd_mfma: dy fp32 [B*L][ndir*H] -> dgates bf16 [B*L][ndir*4H], each
+ *   direction's 4H columns in the ORIGINAL gate order (weight-gradient GEMM
+ *   operand; dx of the layer is one GEMM against [W_ih fwd; W_ih rev]). */
 int irc_lstm_mfma_supported(int64_t H);
 int64_t irc_lstm_mfma_save_floats(int64_t B, int64_t L, int64_t H, int64_t ndir, int which);
 int irc_lstm_pack(const float* wih, const float* bih, const float* bhh, const float* whh,

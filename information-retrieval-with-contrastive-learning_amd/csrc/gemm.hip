@@ -63,6 +63,8 @@ struct Args {
   float alpha;
   int accumulate;  // C += result (fp32 C only)
   int vec_a, vec_b;  // operand rows 16-byte aligned: vector staging allowed
+  int kchunk;        // split-K: K range of one blockIdx.z slice (multiple of BK)
+  float* P;          // split-K partials [batch][split][M][N] (raw sums), or null
 };
 
 // Load one [rows x BK] slab of an operand into registers (as 16-byte vectors).
@@ -158,6 +160,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
   }
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int batch = blockIdx.y;
+  const int kbeg = blockIdx.z * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
   const TI* A = reinterpret_cast<const TI*>(g.A) + batch * g.sA;
   const TI* B = reinterpret_cast<const TI*>(g.B) + batch * g.sB;
   TO* C = reinterpret_cast<TO*>(g.C) + batch * g.sC;
@@ -176,9 +180,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
 
   Slab<TI, LA> sa;
   Slab<TI, LB> sb;
-  const int nk = (g.K + BK - 1) / BK;
-  sa.load(A, g.lda, m0, g.M, 0, g.K, g.vec_a);
-  sb.load(B, g.ldb, n0, g.N, 0, g.K, g.vec_b);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  sa.load(A, g.lda, m0, g.M, kbeg, kend, g.vec_a);
+  sb.load(B, g.ldb, n0, g.N, kbeg, kend, g.vec_b);
   sa.store(lds[0][0]);
   sb.store(lds[0][1]);
   __syncthreads();
@@ -186,8 +190,8 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      sa.load(A, g.lda, m0, g.M, (kt + 1) * BK, g.K, g.vec_a);
-      sb.load(B, g.ldb, n0, g.N, (kt + 1) * BK, g.K, g.vec_b);
+      sa.load(A, g.lda, m0, g.M, kbeg + (kt + 1) * BK, kend, g.vec_a);
+      sb.load(B, g.ldb, n0, g.N, kbeg + (kt + 1) * BK, kend, g.vec_b);
     }
     const char* la = lds[cur][0];
     const char* lb = lds[cur][1];
@@ -247,6 +251,22 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
 
   // Epilogue: acc[i][j] reg e -> row = m0 + wm*64 + i*32 + (e&3) + 8(e>>2) + 4h,
   //                              col = n0 + wn*64 + j*32 + r32.
+  if (g.P) {  // split-K slice: raw partial sums, reduced in a fixed order afterwards
+    float* P = g.P + ((int64_t)batch * gridDim.z + blockIdx.z) * g.M * g.N;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + j * 32 + r32;
+      if (col >= g.N) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (row < g.M) P[(int64_t)row * g.N + col] = acc[i][j][e];
+        }
+    }
+    return;
+  }
   const float* bias = g.bias ? g.bias + batch * g.sBias : nullptr;
   const TO* R = g.R ? reinterpret_cast<const TO*>(g.R) + batch * g.sR : nullptr;
 #pragma unroll
@@ -283,34 +303,78 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
   }
 }
 
+// C[b][m][n] (=|+=) alpha * sum_s P[b][s][m][n]  (s ascending: deterministic)
+__global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restrict__ C, int M,
+                                     int N, int S, int64_t ldc, int64_t sC, int batch,
+                                     float alpha, int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t mn = (int64_t)M * N;
+  if (e >= mn * batch) return;
+  const int b = (int)(e / mn);
+  const int64_t r = e % mn;
+  const float* p = P + (int64_t)b * S * mn + r;
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += p[k * mn];
+  float* dst = C + b * sC + (r / N) * ldc + (r % N);
+  *dst = accumulate ? *dst + alpha * s : alpha * s;
+}
+
+// Split-K count: only when the output tile grid cannot fill the chip and each
+// slice keeps >= 512 of K.  Restricted to fp32 C with no fused epilogue.
+inline int split_count(int TIbytes, int out_f32, int epi, int64_t M, int64_t N, int64_t K,
+                       int64_t batch) {
+  if (!out_f32 || epi != EPI_NONE) return 1;
+  const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch;
+  const int bk = TIbytes == 2 ? TT<unsigned short>::BK : TT<float>::BK;
+  int64_t s = (512 + tiles - 1) / tiles;
+  const int64_t smax = K / 512;
+  if (s > smax) s = smax;
+  if (s > 32) s = 32;
+  if (s < 2) return 1;
+  // equalise slices on BK boundaries; drop empty trailing slices
+  const int64_t chunk = ((K + s - 1) / s + bk - 1) / bk * bk;
+  return (int)((K + chunk - 1) / chunk);
+}
+
 template <typename TI, typename TO, int LA, int LB, int EPI>
-static int launch(const Args& g, int batch, hipStream_t st) {
+static int launch(const Args& g0, int batch, int splits, hipStream_t st) {
+  Args g = g0;
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  constexpr int bk = TT<TI>::BK;
+  g.kchunk = splits > 1 ? ((g.K + splits - 1) / splits + bk - 1) / bk * bk : (g.K > 0 ? g.K : 1);
   prof_begin(st);
-  hipLaunchKernelGGL((gemm_kernel<TI, TO, LA, LB, EPI>), dim3(tiles, batch), dim3(NT), 0, st, g);
+  hipLaunchKernelGGL((gemm_kernel<TI, TO, LA, LB, EPI>), dim3(tiles, batch, splits), dim3(NT), 0,
+                     st, g);
+  if (splits > 1) {
+    const int64_t n = (int64_t)g.M * g.N * batch;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       g.P, reinterpret_cast<float*>(g.C), g.M, g.N, splits, g.ldc, g.sC, batch,
+                       g.alpha, g.accumulate);
+  }
   prof_end(sizeof(TI) == 2 ? "gemm_bf16" : "gemm_f32", st, 2.0 * g.M * g.N * g.K * batch);
   return check_launch("gemm_kernel");
 }
 
 template <typename TI, typename TO, int LA, int LB>
-static int by_epi(int epi, const Args& g, int batch, hipStream_t st) {
+static int by_epi(int epi, const Args& g, int batch, int splits, hipStream_t st) {
   switch (epi) {
-    case EPI_NONE: return launch<TI, TO, LA, LB, EPI_NONE>(g, batch, st);
-    case EPI_BIAS: return launch<TI, TO, LA, LB, EPI_BIAS>(g, batch, st);
-    case EPI_BIAS_GELU: return launch<TI, TO, LA, LB, EPI_BIAS_GELU>(g, batch, st);
-    case EPI_BIAS_RESID: return launch<TI, TO, LA, LB, EPI_BIAS_RESID>(g, batch, st);
-    case EPI_RESID: return launch<TI, TO, LA, LB, EPI_RESID>(g, batch, st);
+    case EPI_NONE: return launch<TI, TO, LA, LB, EPI_NONE>(g, batch, splits, st);
+    case EPI_BIAS: return launch<TI, TO, LA, LB, EPI_BIAS>(g, batch, 1, st);
+    case EPI_BIAS_GELU: return launch<TI, TO, LA, LB, EPI_BIAS_GELU>(g, batch, 1, st);
+    case EPI_BIAS_RESID: return launch<TI, TO, LA, LB, EPI_BIAS_RESID>(g, batch, 1, st);
+    case EPI_RESID: return launch<TI, TO, LA, LB, EPI_RESID>(g, batch, 1, st);
   }
   set_error("gemm: bad epilogue %d", epi);
   return IRC_E_INVALID;
 }
 
 template <typename TI, typename TO>
-static int by_layout(int la, int lb, int epi, const Args& g, int batch, hipStream_t st) {
-  if (la == ROW && lb == ROW) return by_epi<TI, TO, ROW, ROW>(epi, g, batch, st);
-  if (la == ROW && lb == COL) return by_epi<TI, TO, ROW, COL>(epi, g, batch, st);
-  if (la == COL && lb == ROW) return by_epi<TI, TO, COL, ROW>(epi, g, batch, st);
-  return by_epi<TI, TO, COL, COL>(epi, g, batch, st);
+static int by_layout(int la, int lb, int epi, const Args& g, int batch, int splits,
+                     hipStream_t st) {
+  if (la == ROW && lb == ROW) return by_epi<TI, TO, ROW, ROW>(epi, g, batch, splits, st);
+  if (la == ROW && lb == COL) return by_epi<TI, TO, ROW, COL>(epi, g, batch, splits, st);
+  if (la == COL && lb == ROW) return by_epi<TI, TO, COL, ROW>(epi, g, batch, splits, st);
+  return by_epi<TI, TO, COL, COL>(epi, g, batch, splits, st);
 }
 
 }  // namespace gemm
@@ -318,13 +382,20 @@ static int by_layout(int la, int lb, int epi, const Args& g, int batch, hipStrea
 
 using namespace irc;
 
+extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M,
+                                      int64_t N, int64_t K, int64_t batch) {
+  const int s = gemm::split_count(in_dtype == 0 ? 2 : 4, out_dtype == 1, epilogue, M, N, K, batch);
+  return s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
+}
+
 // dtype codes: 0 = bf16, 1 = fp32
 extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue,
                         int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
                         int64_t strideA, const void* B, int64_t ldb, int64_t strideB,
                         const float* bias, int64_t strideBias, const void* R, int64_t ldr,
                         int64_t strideR, void* C, int64_t ldc, int64_t strideC, int accumulate,
-                        int64_t batch, irc_stream_t stream) {
+                        int64_t batch, void* workspace, int64_t workspace_bytes,
+                        irc_stream_t stream) {
   IRC_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: bad sizes");
   IRC_REQUIRE(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31), "gemm: size too large");
   IRC_REQUIRE(in_dtype == 0 || in_dtype == 1, "gemm: in_dtype must be 0 (bf16) or 1 (fp32)");
@@ -339,16 +410,23 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
   const int vec_a = lda % vec == 0 && strideA % vec == 0 && ((uintptr_t)A % 16) == 0;
   const int vec_b = ldb % vec == 0 && strideB % vec == 0 && ((uintptr_t)B % 16) == 0;
   if (M == 0 || N == 0) return IRC_OK;
+  // split-K when the caller provided the workspace irc_gemm_workspace asked for
+  int splits = gemm::split_count(in_dtype == 0 ? 2 : 4, out_dtype == 1, epilogue, M, N, K, batch);
+  if (splits > 1 && (workspace == nullptr ||
+                     workspace_bytes < (int64_t)splits * M * N * batch * (int64_t)sizeof(float)))
+    splits = 1;
   gemm::Args g{A, B, C, bias, R, (int)M, (int)N, (int)K, lda, ldb, ldc, ldr,
-               strideA, strideB, strideC, strideR, strideBias, alpha, accumulate, vec_a, vec_b};
+               strideA, strideB, strideC, strideR, strideBias, alpha, accumulate, vec_a, vec_b,
+               0, splits > 1 ? static_cast<float*>(workspace) : nullptr};
   hipStream_t st = as_stream(stream);
+  const int nb = (int)batch;
   if (in_dtype == 0 && out_dtype == 0)
-    return gemm::by_layout<unsigned short, unsigned short>(a_layout, b_layout, epilogue, g,
-                                                           (int)batch, st);
+    return gemm::by_layout<unsigned short, unsigned short>(a_layout, b_layout, epilogue, g, nb,
+                                                           1, st);
   if (in_dtype == 0 && out_dtype == 1)
-    return gemm::by_layout<unsigned short, float>(a_layout, b_layout, epilogue, g, (int)batch, st);
+    return gemm::by_layout<unsigned short, float>(a_layout, b_layout, epilogue, g, nb, splits, st);
   if (in_dtype == 1 && out_dtype == 1)
-    return gemm::by_layout<float, float>(a_layout, b_layout, epilogue, g, (int)batch, st);
+    return gemm::by_layout<float, float>(a_layout, b_layout, epilogue, g, nb, splits, st);
   set_error("gemm: fp32 inputs with bf16 output is not supported");
   return IRC_E_INVALID;
 }

@@ -5,8 +5,9 @@
 // Forward, per (batch group of 32 sequences, direction) workgroup of 4 waves:
 //   gates[32 x 4H] = xp_t + h_{t-1}[32 x H] . W_hh^T   (v_mfma_f32_32x32x16_bf16)
 // * h_{t-1} lives in LDS (bf16, padded rows) and is the A operand;
-// * W_hh (bf16 [4H][H], 512 KB per direction, shared by every group) streams from
-//   L2 as 16-byte B fragments each step;
+// * W_hh (bf16, 512 KB per direction, shared by every group) streams from L2
+//   each step, pre-packed fragment-native so every wave load is 1 KB contiguous
+//   (no partial-line over-fetch);
 // * wave w (of 8, two per SIMD) owns hidden units [w*H/8, (w+1)*H/8) and ALL FOUR
 //   gates of them (4 accumulator blocks of 32 columns at H = 256), so the cell
 //   update is lane-local and c stays in registers for the whole sequence;
@@ -110,9 +111,9 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_mfma(
         for (int g = 0; g < 4; ++g)
 #pragma unroll
           for (int hf = 0; hf < G::NH; ++hf) {
-            const int col = g * H + w * G::NU + hf * 32 + r32;
-            const bf16x8 bw =
-                *reinterpret_cast<const bf16x8*>(W + (int64_t)col * H + kk * 16 + 8 * h);
+            // fragment-native: one contiguous 1 KB per wave per (block, kk)
+            const bf16x8 bw = *reinterpret_cast<const bf16x8*>(
+                W + ((int64_t)((w * G::NB + g * G::NH + hf) * G::KKF + kk) * 64 + lane) * 8);
             acc[g * G::NH + hf] =
                 __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw, acc[g * G::NH + hf], 0, 0, 0);
           }
@@ -170,7 +171,8 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_mfma(
 }
 
 // Backward.  dy [B*L][ndir*H] fp32 (dL/dh_t from above), whhT [ndir][H][4H] bf16,
-// gsave/csave from lstm_fwd_mfma; dg out [ndir][B*L][4H] bf16 (original gate order).
+// gsave/csave from lstm_fwd_mfma; dg out [B*L][ndir*4H] bf16 (original gate order per
+// direction), so the layer's dx is ONE GEMM with K = ndir*4H.
 template <int H>
 __global__ __launch_bounds__(NTH, 1) void lstm_bwd_mfma(
     const float* __restrict__ dy, const unsigned short* __restrict__ whhT,
@@ -218,9 +220,8 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_mfma(
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + kk * 16 + 8 * h);
 #pragma unroll
         for (int hf = 0; hf < G::NH; ++hf) {
-          const int u = w * G::NU + hf * 32 + r32;
-          const bf16x8 bw =
-              *reinterpret_cast<const bf16x8*>(WT + (int64_t)u * 4 * H + kk * 16 + 8 * h);
+          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(
+              WT + ((int64_t)((w * G::NH + hf) * G::KKB + kk) * 64 + lane) * 8);
           acc[hf] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bw, acc[hf], 0, 0, 0);
         }
       }
@@ -265,11 +266,12 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_mfma(
     }
     __syncthreads();  // dgl complete (next step's A operand)
     constexpr int PIECES = BG * 4 * H / 8;
-    unsigned short* dgd = dg + (int64_t)dir * B * L * 4 * H;
+    const int64_t gld = (int64_t)ndir * 4 * H;
+    unsigned short* dgd = dg + (int64_t)dir * 4 * H;
     for (int p = threadIdx.x; p < PIECES; p += NTH) {
       const int b = p / (4 * H / 8), c8 = (p % (4 * H / 8)) * 8;
       if (b0 + b < B)
-        *reinterpret_cast<u16x8*>(dgd + ((int64_t)(b0 + b) * L + t) * 4 * H + c8) =
+        *reinterpret_cast<u16x8*>(dgd + ((int64_t)(b0 + b) * L + t) * gld + c8) =
             *reinterpret_cast<const u16x8*>(&dgl[b][c8]);
     }
   }
@@ -281,7 +283,6 @@ template <int H>
 __global__ void pack_wih_kernel(const float* __restrict__ wih, const float* __restrict__ bih,
                                 const float* __restrict__ bhh, unsigned short* __restrict__ dst,
                                 float* __restrict__ bias_dst, int In, int ndir) {
-  using G = Geo<H>;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t rows = (int64_t)ndir * 4 * H;
   if (e >= rows * In) return;
@@ -293,18 +294,36 @@ __global__ void pack_wih_kernel(const float* __restrict__ wih, const float* __re
   if (k == 0) bias_dst[r] = bih[orig] + bhh[orig];
 }
 
-// W_hh [ndir][4H][H] fp32 -> bf16 copy and bf16 transpose [ndir][H][4H]
+// W_hh [ndir][4H][H] fp32 -> bf16 B fragments in the order the recurrences read
+// them (each wave's 64 x 16-byte fragment of one (block, kk) is 1 KB contiguous):
+//   w  [dir][wave][block g*NH+hf][kk < H/16][lane][8]:  W[g*H + u][kk*16 + 8h + j]
+//   wT [dir][wave][hf][kk < 4H/16][lane][8]:            W[kk*16 + 8h + j][u]
+// with u = wave*NU + hf*32 + (lane & 31), h = lane >> 5.
+template <int H>
 __global__ void pack_whh_kernel(const float* __restrict__ whh, unsigned short* __restrict__ w,
-                                unsigned short* __restrict__ wT, int H, int ndir) {
+                                unsigned short* __restrict__ wT, int ndir) {
+  using G = Geo<H>;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t per = (int64_t)4 * H * H;
   if (e >= per * ndir) return;
   const int dir = (int)(e / per);
   const int64_t r = e % per;
-  const int g = (int)(r / H), k = (int)(r % H);
-  const unsigned short v = f32_to_bf16(whh[e]);
-  w[e] = v;
-  wT[dir * per + (int64_t)k * 4 * H + g] = v;
+  const int j = (int)(r & 7), lane = (int)((r >> 3) & 63);
+  const int h = lane >> 5, r32 = lane & 31;
+  const float* W = whh + dir * per;
+  {  // forward fragments: r = ((wv*NB + blk)*KKF + kk)*512 + lane*8 + j
+    const int kk = (int)((r >> 9) % G::KKF);
+    const int blk = (int)((r >> 9) / G::KKF % G::NB), wv = (int)((r >> 9) / G::KKF / G::NB);
+    const int g = blk / G::NH, hf = blk % G::NH;
+    const int u = wv * G::NU + hf * 32 + r32;
+    w[e] = f32_to_bf16(W[(int64_t)(g * H + u) * H + kk * 16 + 8 * h + j]);
+  }
+  {  // backward fragments: r = ((wv*NH + hf)*KKB + kk)*512 + lane*8 + j
+    const int kk = (int)((r >> 9) % G::KKB);
+    const int hf = (int)((r >> 9) / G::KKB % G::NH), wv = (int)((r >> 9) / G::KKB / G::NH);
+    const int u = wv * G::NU + hf * 32 + r32;
+    wT[e] = f32_to_bf16(W[(int64_t)(kk * 16 + 8 * h + j) * H + u]);
+  }
 }
 
 // hprev[dir][b*L + t] = h_{t-1} (forward order) of direction dir, 0 at the start.
@@ -352,8 +371,8 @@ extern "C" int irc_lstm_pack(const float* wih, const float* bih, const float* bh
     hipLaunchKernelGGL(lstmm::pack_wih_kernel<256>, dim3(nb256(n1)), dim3(256), 0, st, wih, bih,
                        bhh, (unsigned short*)wih_packed, bias_packed, (int)In, (int)ndir);
   const int64_t n2 = ndir * 4 * H * H;
-  hipLaunchKernelGGL(lstmm::pack_whh_kernel, dim3(nb256(n2)), dim3(256), 0, st, whh,
-                     (unsigned short*)whh_bf16, (unsigned short*)whhT_bf16, (int)H, (int)ndir);
+  hipLaunchKernelGGL(lstmm::pack_whh_kernel<256>, dim3(nb256(n2)), dim3(256), 0, st, whh,
+                     (unsigned short*)whh_bf16, (unsigned short*)whhT_bf16, (int)ndir);
   return check_launch("lstm_pack");
 }
 

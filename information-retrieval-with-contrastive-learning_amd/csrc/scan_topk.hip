@@ -438,7 +438,7 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
       mn = s_mm[0][w] < mn ? s_mm[0][w] : mn;
       mx = s_mm[1][w] > mx ? s_mm[1][w] : mx;
     }
-    const int top = 63 - __builtin_clzll(mn ^ mx | 1ull);  // highest differing bit
+    const int top = 63 - __builtin_clzll((mn ^ mx) | 1ull);  // highest differing bit
     const int first_shift = (top / 8) * 8;
     const int last_shift = (mode == SEL_THRESHOLD) ? 48 : 0;
     uint64_t pmask = first_shift >= 56 ? 0ull : (~0ull << (first_shift + 8));

@@ -29,7 +29,8 @@ SIGNATURES = {
     "irc_topk_merge": (I32, [P, P, I64, I64, I64, I64, P, P, P]),
     "irc_scan_scores": (I32, [P, P, I64, I64, I64, P, P]),
     "irc_gemm": (I32, [I32, I32, I32, I32, I32, I64, I64, I64, F32, P, I64, I64, P, I64, I64,
-                       P, I64, P, I64, I64, P, I64, I64, I32, I64, P]),
+                       P, I64, P, I64, I64, P, I64, I64, I32, I64, P, I64, P]),
+    "irc_gemm_workspace": (I64, [I32, I32, I32, I64, I64, I64, I64]),
     "irc_embed_ln": (I32, [I32, P, P, P, P, P, P, P, I64, I64, I64, F32, P]),
     "irc_layernorm": (I32, [I32, P, P, P, P, I64, I64, F32, P]),
     "irc_attention": (I32, [I32, P, P, P, I64, I64, I64, I64, P]),

@@ -235,11 +235,11 @@ class LSTMHead(nn.Module):
         dy = ops.bcast_rows(dmh, B, L, 1.0 / L)  # [B*L, 2H] fp32
         for l in range(self.num_layers - 1, -1, -1):
             mfma, x, wih, whh, gsave, csave, hprev = layers[l]
-            if mfma:  # dgates come out in bf16, ready for the weight-gradient GEMMs
-                dg = dgc = ops.lstm_bwd_mfma(dy, whh, gsave, csave, B, L, H, nd)
-            else:
-                dg = ops.lstm_bwd(dy, whh, gsave, csave, B, L, H, nd)  # [nd, B*L, 4H] fp32
-                dgc = ops.cast_bf16(dg) if x.dtype == torch.bfloat16 else dg
+            if mfma:
+                dy = self._layer_bwd_mfma(l, dy, x, wih, whh, gsave, csave, hprev, B, L)
+                continue
+            dg = ops.lstm_bwd(dy, whh, gsave, csave, B, L, H, nd)  # [nd, B*L, 4H] fp32
+            dgc = ops.cast_bf16(dg) if x.dtype == torch.bfloat16 else dg
             in_l = x.shape[1]
             dx = None
             for d in range(nd):
@@ -255,6 +255,37 @@ class LSTMHead(nn.Module):
                     dx = ops.gemm(dgc[d], w_d, b_is_nk=False, out=dx, accumulate=dx is not None,
                                   out_dtype=torch.float32)
             dy = dx
+
+    def _layer_bwd_mfma(self, l, dy, x, wih_c, whhT, gsave, csave, hprev, B, L):
+        """BPTT of one layer on the MFMA path; returns dL/dx (None for layer 0).
+
+        dgates [B*L, ndir*4H] bf16 -> both directions' dW_ih / dW_hh as one batched
+        GEMM each (K = B*L, deterministic split-K), the bias grads as one column
+        sum over both directions, and dx as one GEMM with K = ndir*4H."""
+        H, nd = self.hidden, self.ndir
+        g = self.flat_grad
+        o = self.offsets
+        dg = ops.lstm_bwd_mfma(dy, whhT, gsave, csave, B, L, H, nd)
+        In = x.shape[1]
+        BL = B * L
+        ih, hh = o[f"lstm.weight_ih_l{l}"], o[f"lstm.weight_hh_l{l}"]
+        bi, bh = o[f"lstm.bias_ih_l{l}"], o[f"lstm.bias_hh_l{l}"]
+        if nd == 2:  # both directions' slices are adjacent in the flat buffer
+            assert o[f"lstm.weight_ih_l{l}_reverse"] == ih + 4 * H * In
+            assert o[f"lstm.weight_hh_l{l}_reverse"] == hh + 4 * H * H
+            assert o[f"lstm.bias_ih_l{l}_reverse"] == bi + 4 * H
+            assert o[f"lstm.bias_hh_l{l}_reverse"] == bh + 4 * H
+        ops.gemm_strided(dg, x, g[ih:], M=4 * H, N=In, K=BL, batch=nd, lda=nd * 4 * H,
+                         sA=4 * H, ldb=x.stride(0), sB=0, ldc=In, sC=4 * H * In, trans_a=True,
+                         b_is_nk=False, accumulate=True)
+        ops.gemm_strided(dg, hprev, g[hh:], M=4 * H, N=H, K=BL, batch=nd, lda=nd * 4 * H,
+                         sA=4 * H, ldb=H, sB=BL * H, ldc=H, sC=4 * H * H, trans_a=True,
+                         b_is_nk=False, accumulate=True)
+        ops.colsum(dg, out=g[bi:bi + nd * 4 * H], accumulate=True)
+        ops.colsum(dg, out=g[bh:bh + nd * 4 * H], accumulate=True)
+        if l == 0:
+            return None
+        return ops.gemm(dg, wih_c, b_is_nk=False, out_dtype=torch.float32)  # [B*L, In]
 
     def forward(self, features, **kwargs):
         """Per-position head output [B, L, D] (reference LSTM.forward semantics);

@@ -30,7 +30,7 @@ def gemm(a, b, *, trans_a=False, b_is_nk=True, bias=None, epilogue=EPI_NONE, res
 
     a: [M, K] (or [K, M] with trans_a); b: [N, K] when b_is_nk (nn.Linear weight
     layout, i.e. a @ b.T) else [K, N].  Inputs bf16 or fp32 (same dtype);
-    fp32 inputs run the exact fp32 MFMA.  2-D only (see gemm_batched).
+    fp32 inputs run the exact fp32 MFMA.  2-D only (see gemm_strided).
     """
     require_hip(a, b, bias, residual, out)
     if a.dtype != b.dtype:
@@ -50,10 +50,35 @@ def gemm(a, b, *, trans_a=False, b_is_nk=True, bias=None, epilogue=EPI_NONE, res
         raise TypeError("bias must be fp32")
     if residual is not None and residual.dtype != out.dtype:
         raise TypeError("residual dtype must match the output")
+    ws, nws = _splitk_ws(a, out, epilogue, M, N, K, 1)
     _lib.call("irc_gemm", _code(a), _code(out), 1 if trans_a else 0, 0 if b_is_nk else 1,
               int(epilogue), M, N, K, float(alpha), ptr(a), a.stride(0), 0, ptr(b), b.stride(0),
               0, ptr(bias), 0, ptr(residual), residual.stride(0) if residual is not None else 0, 0,
-              ptr(out), out.stride(0), 0, 1 if accumulate else 0, 1, stream_ptr(a.device))
+              ptr(out), out.stride(0), 0, 1 if accumulate else 0, 1, ptr(ws), nws,
+              stream_ptr(a.device))
+    return out
+
+
+def _splitk_ws(a, out, epilogue, M, N, K, batch):
+    """Device workspace for the GEMM's deterministic split-K (None when unused)."""
+    nws = _lib.load().irc_gemm_workspace(_code(a), _code(out), int(epilogue), M, N, K, batch)
+    if nws <= 0:
+        return None, 0
+    return torch.empty((nws,), dtype=torch.uint8, device=a.device), nws
+
+
+def gemm_strided(a, b, out, *, M, N, K, batch, lda, sA, ldb, sB, ldc, sC, trans_a=False,
+                 b_is_nk=True, alpha=1.0, accumulate=False):
+    """Batched C_i (=|+=) alpha * op(A_i) @ op(B_i) over raw strides (elements):
+    A_i = a + i*sA, etc.  Same operand layouts as ``gemm``; no epilogue."""
+    require_hip(a, b, out)
+    if a.dtype != b.dtype:
+        raise TypeError("gemm operands must share a dtype")
+    ws, nws = _splitk_ws(a, out, EPI_NONE, M, N, K, batch)
+    _lib.call("irc_gemm", _code(a), _code(out), 1 if trans_a else 0, 0 if b_is_nk else 1,
+              EPI_NONE, M, N, K, float(alpha), ptr(a), lda, sA, ptr(b), ldb, sB, None, 0, None,
+              0, 0, ptr(out), ldc, sC, 1 if accumulate else 0, batch, ptr(ws), nws,
+              stream_ptr(a.device))
     return out
 
 
@@ -144,7 +169,7 @@ def lstm_fwd_mfma(xp_packed, whh_bf16, B, L, H, ndir, save=True):
 
 def lstm_bwd_mfma(dy, whhT_bf16, gsave, csave, B, L, H, ndir):
     require_hip(dy, whhT_bf16, gsave, csave)
-    dg = torch.empty((ndir, B * L, 4 * H), dtype=BF16, device=dy.device)
+    dg = torch.empty((B * L, ndir * 4 * H), dtype=BF16, device=dy.device)
     _lib.call("irc_lstm_bwd_mfma", ptr(dy), ptr(whhT_bf16), ptr(gsave), ptr(csave), ptr(dg), B, L,
               H, ndir, stream_ptr(dy.device))
     return dg

@@ -77,3 +77,49 @@ def test_fp32_mfma_is_exact_on_integers(gpu):
     b = torch.randint(-50, 50, (33, 64), generator=g).float()
     out = ops.gemm(a.to(gpu), b.to(gpu)).cpu()
     assert torch.equal(out, a @ b.t())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K", [(1024, 256, 16384), (200, 72, 5000), (64, 64, 1030)])
+def test_splitk_batched_accumulate(gpu, dtype, M, N, K):
+    """Weight-gradient shape (K = B*L >> M, N): the deterministic split-K path,
+    batched over two directions with an interleaved A ([K][2M], lda = 2M) and a
+    shared B, accumulating into fp32 C.  Bitwise reproducible run to run."""
+    from irc_amd import _lib, ops
+
+    code = 0 if dtype == torch.bfloat16 else 1
+    assert _lib.load().irc_gemm_workspace(code, 1, 0, M, N, K, 2) > 0 or K < 1024
+    g = torch.Generator().manual_seed(K)
+    a = torch.randn((K, 2 * M), generator=g).to(dtype)
+    b = torch.randn((K, N), generator=g).to(dtype)
+    c0 = torch.randn((2, M, N), generator=g)
+    out = c0.clone().to(gpu)
+    ad, bd = a.to(gpu), b.to(gpu)
+    ops.gemm_strided(ad, bd, out, M=M, N=N, K=K, batch=2, lda=2 * M, sA=M, ldb=N, sB=0, ldc=N,
+                     sC=M * N, trans_a=True, b_is_nk=False, accumulate=True)
+    af, bf = a.float(), b.float()
+    for d in range(2):
+        ref = c0[d] + af[:, d * M:(d + 1) * M].t().double().matmul(bf.double()).float()
+        tol = 1e-5 * K if dtype == torch.float32 else 1e-4 * K
+        assert (out[d].cpu() - ref).abs().max().item() <= tol, d
+    out2 = c0.clone().to(gpu)
+    ops.gemm_strided(ad, bd, out2, M=M, N=N, K=K, batch=2, lda=2 * M, sA=M, ldb=N, sB=0, ldc=N,
+                     sC=M * N, trans_a=True, b_is_nk=False, accumulate=True)
+    assert torch.equal(out, out2)
+
+
+def test_splitk_matches_unsplit(gpu):
+    """Same GEMM with and without the workspace: equal within fp32 reassociation."""
+    from irc_amd import _lib, ops
+    from irc_amd._torch import ptr, stream_ptr
+
+    M, N, K = 256, 128, 8192
+    g = torch.Generator().manual_seed(7)
+    a = torch.randn((K, M), generator=g).to(torch.bfloat16).to(gpu)
+    b = torch.randn((K, N), generator=g).to(torch.bfloat16).to(gpu)
+    split = ops.gemm(a, b, trans_a=True, b_is_nk=False, out_dtype=torch.float32)
+    plain = torch.empty((M, N), device=gpu)
+    _lib.call("irc_gemm", 0, 1, 1, 1, 0, M, N, K, 1.0, ptr(a), M, 0, ptr(b), N, 0, None, 0, None,
+              0, 0, ptr(plain), N, 0, 0, 1, None, 0, stream_ptr(a.device))
+    assert _lib.load().irc_gemm_workspace(0, 1, 0, M, N, K, 1) > 0
+    torch.testing.assert_close(split, plain, rtol=1e-5, atol=1e-3)
