@@ -134,7 +134,12 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
     nvalid = n;
   }
   __syncthreads();
-  const int nv = nvalid;
+  // all keys masked: HF's finfo.min bias swamps every score -> uniform weights
+  const bool uniform = nvalid == 0;
+  if (uniform)
+    for (int j = threadIdx.x; j < L; j += blockDim.x) valid[j] = j;
+  __syncthreads();
+  const int nv = uniform ? L : nvalid;
   for (int i = threadIdx.x; i < L; i += blockDim.x) {
     float qv[DH];
 #pragma unroll
@@ -149,6 +154,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
       float s = 0.f;
 #pragma unroll
       for (int d = 0; d < DH; ++d) s += qv[d] * kr[d];
+      if (uniform) s = 0.f;
       const float mn = fmaxf(m, s);
       const float corr = __expf(m - mn);
       const float p = __expf(s - mn);
@@ -162,6 +168,124 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
 #pragma unroll
     for (int d = 0; d < DH; ++d) st(ctx, (base + i) * H + a * DH + d, o[d] * inv);
   }
+}
+
+// MFMA attention, bf16, head dim 64, L = 32*NJ (NJ <= 4): one wave per
+// (sequence, head, block of 32 queries).
+//  * S^T[j][i] = K[j] . Q[i] on v_mfma_f32_32x32x16_bf16 (A = K rows, B = Q rows,
+//    both read straight from the fused QKV rows as 16-byte fragments), so lane
+//    (i, half) holds query i's scores for the keys j = 32jb + (e&3) + 8(e>>2) + 4*half:
+//    the softmax over keys is lane-local plus one exchange with lane ^ 32;
+//  * key mask as an additive bias (0 / -1e30: masked keys get exactly zero
+//    weight; an all-masked row degrades to a uniform average, as HF's finfo.min
+//    bias does), fp32 softmax, probabilities rounded to bf16 (HF bf16 semantics);
+//  * O = P . V: P goes straight from registers into the A operand; summing over
+//    keys in the lane's permuted key order is matched by reading the V operand
+//    from a per-wave transposed V^T copy in LDS (two ds_read_b64 per fragment).
+template <int NJ>
+__global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned short* __restrict__ qkv,
+                                                            const int64_t* __restrict__ mask,
+                                                            unsigned short* __restrict__ ctx,
+                                                            int B, int H, int heads, float scale) {
+  constexpr int L = 32 * NJ, DH = 64;
+  constexpr int VP = L + 4;  // V^T row pitch (u16): 8-byte aligned, conflict-free b64 reads
+  __shared__ __attribute__((aligned(16))) unsigned short vt[4][DH][VP];
+  __shared__ __attribute__((aligned(16))) float mb[4][L];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int64_t item = (int64_t)blockIdx.x * 4 + wv;  // (b, head, ib)
+  const bool active = item < (int64_t)B * heads * NJ;
+  const int ib = active ? (int)(item % NJ) : 0;
+  const int a = active ? (int)(item / NJ % heads) : 0;
+  const int b = active ? (int)(item / NJ / heads) : 0;
+  const int64_t ld3 = 3LL * H;
+  const unsigned short* base = qkv + (int64_t)b * L * ld3 + a * DH;  // + j*ld3: Q | +H: K | +2H: V
+  if (active) {
+    for (int p = lane; p < (L / 2) * 8; p += 64) {
+      const int dc = p & 7, j = (p >> 3) * 2;  // 8-wide d chunk, key pair (j, j+1)
+      const u16x8 v0 = *reinterpret_cast<const u16x8*>(base + (int64_t)j * ld3 + 2 * H + dc * 8);
+      const u16x8 v1 =
+          *reinterpret_cast<const u16x8*>(base + (int64_t)(j + 1) * ld3 + 2 * H + dc * 8);
+#pragma unroll
+      for (int dd = 0; dd < 8; ++dd)
+        *reinterpret_cast<uint32_t*>(&vt[wv][dc * 8 + dd][j]) =
+            (uint32_t)v0[dd] | ((uint32_t)v1[dd] << 16);
+    }
+    for (int j = lane; j < L; j += 64)
+      mb[wv][j] = (mask == nullptr || mask[(int64_t)b * L + j] != 0) ? 0.f : -1e30f;
+  }
+  __syncthreads();
+  if (!active) return;  // past the only barrier
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+    qf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)(32 * ib + r32) * ld3 + 16 * kk + 8 * h);
+  f32x16 s[NJ];
+#pragma unroll
+  for (int jb = 0; jb < NJ; ++jb) {
+    s[jb] = (f32x16)0.f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(base + (int64_t)(32 * jb + r32) * ld3 + H +
+                                                         16 * kk + 8 * h);
+      s[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], s[jb], 0, 0, 0);
+    }
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int jb = 0; jb < NJ; ++jb)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 bias = *reinterpret_cast<const f32x4*>(&mb[wv][32 * jb + 8 * q + 4 * h]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = s[jb][4 * q + r] * scale + bias[r];
+        s[jb][4 * q + r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int jb = 0; jb < NJ; ++jb)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float p = __expf(s[jb][e] - mx);
+      s[jb][e] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+
+  f32x16 o[2] = {(f32x16)0.f, (f32x16)0.f};
+#pragma unroll
+  for (int jb = 0; jb < NJ; ++jb)
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      bf16x8 pa;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) pa[t] = (__bf16)(s[jb][8 * k2 + t] * inv);
+      const int j0 = 32 * jb + 16 * k2 + 4 * h;  // keys of slots t<4: j0+t; t>=4: j0+8+t-4
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const int d = 32 * db + r32;
+        const u16x4 lo = *reinterpret_cast<const u16x4*>(&vt[wv][d][j0]);
+        const u16x4 hi = *reinterpret_cast<const u16x4*>(&vt[wv][d][j0 + 8]);
+        const u16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(bf16x8, vv), o[db],
+                                                        0, 0, 0);
+      }
+    }
+  // O C layout: col = d (lane), row = query 32ib + (e&3) + 8(e>>2) + 4h
+  unsigned short* out = ctx + ((int64_t)b * L + 32 * ib) * H + a * DH;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int i = (e & 3) + 8 * (e >> 2) + 4 * h;
+      out[(int64_t)i * H + 32 * db + r32] = f32_to_bf16(o[db][e]);
+    }
 }
 
 }  // namespace enc
@@ -226,6 +350,29 @@ extern "C" int irc_attention(int dtype, const void* qkv, const int64_t* mask, vo
               "attention: L=%lld too long for LDS staging", (long long)L);
   if (B == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
+  if (dtype == 0 && dh == 64 && L % 32 == 0 && L <= 128) {  // production shape: MFMA
+    const int64_t waves = B * heads * (L / 32);
+    const dim3 grid((unsigned)((waves + 3) / 4));
+    const float sc = 0.125f;  // 1/sqrt(64)
+    prof_begin(st);
+    switch (L / 32) {
+      case 1: hipLaunchKernelGGL(enc::attention_mfma_kernel<1>, grid, dim3(256), 0, st,
+                                 (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B,
+                                 (int)H, (int)heads, sc); break;
+      case 2: hipLaunchKernelGGL(enc::attention_mfma_kernel<2>, grid, dim3(256), 0, st,
+                                 (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B,
+                                 (int)H, (int)heads, sc); break;
+      case 3: hipLaunchKernelGGL(enc::attention_mfma_kernel<3>, grid, dim3(256), 0, st,
+                                 (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B,
+                                 (int)H, (int)heads, sc); break;
+      default: hipLaunchKernelGGL(enc::attention_mfma_kernel<4>, grid, dim3(256), 0, st,
+                                  (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B,
+                                  (int)H, (int)heads, sc); break;
+    }
+    // algorithmic bytes: QKV read once + ctx written
+    prof_end("attention", st, (double)B * L * (3 * H + H) * 2.0);
+    return check_launch("attention_mfma_kernel");
+  }
 #define IRC_ATT(DH)                                                                  \
   if (dh == DH)                                                                      \
     return dtype == 0 ? attn_launch<unsigned short, DH>(qkv, mask, ctx, B, L, H, heads, st) \

@@ -26,6 +26,19 @@ def stream_ptr(device: torch.device | None = None):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+_side: dict = {}
+
+
+def side_stream(device: torch.device, tag: str = "side") -> torch.cuda.Stream:
+    """A persistent secondary HIP stream per (device, tag) for overlapping
+    independent launches (e.g. the key encoder, weight-gradient GEMMs)."""
+    key = (torch.device(device).index, tag)
+    s = _side.get(key)
+    if s is None:
+        s = _side[key] = torch.cuda.Stream(device=device)
+    return s
+
+
 def contig(t: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
     if t.dtype != dtype:
         t = t.to(dtype)

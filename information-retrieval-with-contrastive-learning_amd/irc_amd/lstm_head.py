@@ -237,6 +237,8 @@ class LSTMHead(nn.Module):
             mfma, x, wih, whh, gsave, csave, hprev = layers[l]
             if mfma:
                 dy = self._layer_bwd_mfma(l, dy, x, wih, whh, gsave, csave, hprev, B, L)
+                if l == 0:
+                    torch.cuda.current_stream(x.device).wait_stream(self._wgrad_pending)
                 continue
             dg = ops.lstm_bwd(dy, whh, gsave, csave, B, L, H, nd)  # [nd, B*L, 4H] fp32
             dgc = ops.cast_bf16(dg) if x.dtype == torch.bfloat16 else dg
@@ -275,17 +277,26 @@ class LSTMHead(nn.Module):
             assert o[f"lstm.weight_hh_l{l}_reverse"] == hh + 4 * H * H
             assert o[f"lstm.bias_ih_l{l}_reverse"] == bi + 4 * H
             assert o[f"lstm.bias_hh_l{l}_reverse"] == bh + 4 * H
-        ops.gemm_strided(dg, x, g[ih:], M=4 * H, N=In, K=BL, batch=nd, lda=nd * 4 * H,
-                         sA=4 * H, ldb=x.stride(0), sB=0, ldc=In, sC=4 * H * In, trans_a=True,
-                         b_is_nk=False, accumulate=True)
-        ops.gemm_strided(dg, hprev, g[hh:], M=4 * H, N=H, K=BL, batch=nd, lda=nd * 4 * H,
-                         sA=4 * H, ldb=H, sB=BL * H, ldc=H, sC=4 * H * H, trans_a=True,
-                         b_is_nk=False, accumulate=True)
-        ops.colsum(dg, out=g[bi:bi + nd * 4 * H], accumulate=True)
-        ops.colsum(dg, out=g[bh:bh + nd * 4 * H], accumulate=True)
-        if l == 0:
-            return None
-        return ops.gemm(dg, wih_c, b_is_nk=False, out_dtype=torch.float32)  # [B*L, In]
+        # dx is the critical path (next layer's recurrence); the weight/bias
+        # gradients go to a side stream and overlap that recurrence, which only
+        # occupies B/32 * ndir CUs.  Joined in backward_compute.
+        dx = ops.gemm(dg, wih_c, b_is_nk=False, out_dtype=torch.float32) if l > 0 else None
+        cur = torch.cuda.current_stream(dg.device)
+        side = side_stream(dg.device, "lstm_wgrad")
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            ops.gemm_strided(dg, x, g[ih:], M=4 * H, N=In, K=BL, batch=nd, lda=nd * 4 * H,
+                             sA=4 * H, ldb=x.stride(0), sB=0, ldc=In, sC=4 * H * In,
+                             trans_a=True, b_is_nk=False, accumulate=True)
+            ops.gemm_strided(dg, hprev, g[hh:], M=4 * H, N=H, K=BL, batch=nd, lda=nd * 4 * H,
+                             sA=4 * H, ldb=H, sB=BL * H, ldc=H, sC=4 * H * H, trans_a=True,
+                             b_is_nk=False, accumulate=True)
+            ops.colsum(dg, out=g[bi:bi + nd * 4 * H], accumulate=True)
+            ops.colsum(dg, out=g[bh:bh + nd * 4 * H], accumulate=True)
+        for t in (dg, x, hprev):  # allocated on cur, read on side
+            t.record_stream(side)
+        self._wgrad_pending = side
+        return dx
 
     def forward(self, features, **kwargs):
         """Per-position head output [B, L, D] (reference LSTM.forward semantics);

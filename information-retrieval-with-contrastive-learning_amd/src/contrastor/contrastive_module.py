@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from irc_amd import ops
+from irc_amd._torch import side_stream
 from irc_amd.bert import BertModel
 from irc_amd.lstm_head import LSTMHead, seq2vec as head_seq2vec
 from irc_amd.tokenizer import load_tokenizer
@@ -89,9 +90,22 @@ class RetrievalModelWrapper(nn.Module):
 
     def forward_features(self, anchor_feat, positive_feat, cluster_result=None, indexes=None):
         """forward() from BERT features on: heads, loss, enqueue."""
-        emb_q = self.seq2vec(anchor_feat)
-        emb_k = self.seq2vec(positive_feat, query=False) if self.use_momentum else \
-            self.seq2vec(positive_feat)
+        if self.use_momentum and positive_feat.is_cuda:
+            # the no-grad key encoder is independent of the query encoder until the
+            # loss: run it on a side stream so the two recurrences share the chip
+            cur = torch.cuda.current_stream(positive_feat.device)
+            side = side_stream(positive_feat.device, "key_encoder")
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                emb_k = self.seq2vec(positive_feat, query=False)
+            positive_feat.record_stream(side)
+            emb_q = self.seq2vec(anchor_feat)
+            cur.wait_stream(side)
+            emb_k.record_stream(cur)
+        else:
+            emb_q = self.seq2vec(anchor_feat)
+            emb_k = self.seq2vec(positive_feat, query=False) if self.use_momentum else \
+                self.seq2vec(positive_feat)
         queue = None if not self.use_queue or not self.add_queue_to_loss else self.queue
         loss = self.criterion(emb_q, emb_k, queue, cluster_result, indexes)
         if self.use_queue and self.training:
