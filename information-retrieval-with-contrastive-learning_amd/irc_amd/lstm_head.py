@@ -28,6 +28,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
+from ._torch import side_stream
 from .precision import compute_dtype
 
 ALIGN = 16  # floats (64 B) per slice start: GEMM operands need 16-byte alignment
