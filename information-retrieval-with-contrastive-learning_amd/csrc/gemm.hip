@@ -336,8 +336,160 @@ inline int split_count(int TIbytes, int out_f32, int epi, int64_t M, int64_t N, 
   return (int)((K + chunk - 1) / chunk);
 }
 
+// ---------------------------------------------------------------------------
+// Large-tile bf16 path for K-contiguous operands (A [M][K], B [N][K]: the BERT
+// and LSTM-projection GEMMs).  256x256x64 block tile, 8 waves as 2(M) x 4(N),
+// 128x64 per wave = 4x2 blocks of v_mfma_f32_32x32x16_bf16.  Both tiles move
+// global -> LDS by global_load_lds_dwordx4 (no VGPR staging), double buffered
+// (128 KB LDS): tile k+1 is in flight while tile k is consumed.  LDS rows are
+// 128 B (64 k); the 16-byte chunk c of row r is stored at chunk c ^ (r & 7) so the
+// row-wise ds_read_b128 fragment reads are conflict free -- applied on the
+// SOURCE address, since the DMA destination is lane-linear.  Rows past M / N
+// load a clamped valid row and are never stored.  Requires K % 64 == 0, lda/ldb
+// % 8 == 0 and 16-byte aligned bases.
+namespace big {
+constexpr int BM = 256, BN = 256, BK = 64, NW = 8, NT = NW * 64;
+constexpr int TILE_BYTES = BM * BK * 2;  // 32 KB per operand per stage
+constexpr int GL_PER_T = TILE_BYTES / (NT * 16);  // glds per thread per operand (4)
+
+__device__ __forceinline__ void stage(const unsigned short* __restrict__ X, int64_t ld, int r0,
+                                      int nrows, int k0, char* lds_tile, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < GL_PER_T; ++i) {
+    const int p = (i * NW + wave) * 64 + lane;  // 16-byte LDS chunk index (lane-linear)
+    const int row = p >> 3;
+    const int c = (p & 7) ^ (row & 7);          // logical k-chunk stored at this slot
+    int gr = r0 + row;
+    gr = gr < nrows ? gr : nrows - 1;
+    glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
+  }
+}
+}  // namespace big
+
+template <typename TO, int EPI>
+__global__ __launch_bounds__(big::NT, 1) void gemm256_kernel(Args g) {
+  using big::BK; using big::NT; using big::NW; using big::TILE_BYTES;
+  constexpr int BM = big::BM, BN = big::BN;
+  __shared__ __attribute__((aligned(1024))) char lds[2][2][big::TILE_BYTES];  // [stage][A/B]
+  const int tiles_m = (g.M + BM - 1) / BM;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int batch = blockIdx.y;
+  const unsigned short* A = reinterpret_cast<const unsigned short*>(g.A) + batch * g.sA;
+  const unsigned short* B = reinterpret_cast<const unsigned short*>(g.B) + batch * g.sB;
+  TO* C = reinterpret_cast<TO*>(g.C) + batch * g.sC;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int h = lane >> 5, r32 = lane & 31;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16)0.0f;
+
+  const int nk = g.K / BK;
+  big::stage(A, g.lda, m0, g.M, 0, lds[0][0], wave, lane);
+  big::stage(B, g.ldb, n0, g.N, 0, lds[0][1], wave, lane);
+  wait_vmcnt<0>();
+  __syncthreads();
+  // fragment byte offsets within a stage: row r, logical chunk c -> r*128 + ((c ^ (r&7)) * 16)
+  const int swz = r32 & 7;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      big::stage(A, g.lda, m0, g.M, (kt + 1) * BK, lds[cur ^ 1][0], wave, lane);
+      big::stage(B, g.ldb, n0, g.N, (kt + 1) * BK, lds[cur ^ 1][1], wave, lane);
+    }
+    const char* la = lds[cur][0];
+    const char* lb = lds[cur][1];
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int coff = (((2 * kk + h) ^ swz) * 16);
+      bf16x8 fa[4], fb[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 32 + r32) * 128 + coff);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(lb + (wn * 64 + j * 32 + r32) * 128 + coff);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+
+  const float* bias = g.bias ? g.bias + batch * g.sBias : nullptr;
+  const TO* R = g.R ? reinterpret_cast<const TO*>(g.R) + batch * g.sR : nullptr;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 64 + j * 32 + r32;
+    if (col >= g.N) continue;
+    const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESID) ? bias[col]
+                                                                                        : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = m0 + wm * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row >= g.M) continue;
+        float v = acc[i][j][e] * g.alpha + bv;
+        if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+        if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
+          if constexpr (sizeof(TO) == 2)
+            v += bf16_to_f32(reinterpret_cast<const unsigned short*>(R)[(int64_t)row * g.ldr + col]);
+          else
+            v += reinterpret_cast<const float*>(R)[(int64_t)row * g.ldr + col];
+        }
+        TO* dst = C + (int64_t)row * g.ldc + col;
+        if constexpr (sizeof(TO) == 2) {
+          *reinterpret_cast<unsigned short*>(dst) = f32_to_bf16(v);
+        } else {
+          if (g.accumulate)
+            *reinterpret_cast<float*>(dst) += v;
+          else
+            *reinterpret_cast<float*>(dst) = v;
+        }
+      }
+    }
+  }
+}
+
+// The large-tile path applies: bf16 in, A [M][K] and B [N][K], aligned, K % 64,
+// and enough 256x256 tiles to occupy the chip.
+inline bool use_big(const Args& g, int batch, int la, int lb) {
+  if (la != ROW || lb != ROW || !g.vec_a || !g.vec_b) return false;
+  if (g.K % big::BK != 0 || g.K == 0) return false;
+  const int64_t tiles = (int64_t)((g.M + 255) / 256) * ((g.N + 255) / 256) * batch;
+  return tiles >= 128;
+}
+
+template <typename TO, int EPI>
+static int launch_big(const Args& g, int batch, hipStream_t st) {
+  const int tiles = ((g.M + big::BM - 1) / big::BM) * ((g.N + big::BN - 1) / big::BN);
+  prof_begin(st);
+  hipLaunchKernelGGL((gemm256_kernel<TO, EPI>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
+  prof_end("gemm_bf16", st, 2.0 * g.M * g.N * g.K * batch);
+  return check_launch("gemm256_kernel");
+}
+
 template <typename TI, typename TO, int LA, int LB, int EPI>
 static int launch(const Args& g0, int batch, int splits, hipStream_t st) {
+  if constexpr (sizeof(TI) == 2) {
+    if (splits == 1 && use_big(g0, batch, LA, LB)) return launch_big<TO, EPI>(g0, batch, st);
+  }
   Args g = g0;
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   constexpr int bk = TT<TI>::BK;

@@ -123,3 +123,39 @@ def test_splitk_matches_unsplit(gpu):
               0, 0, ptr(plain), N, 0, 0, 1, None, 0, stream_ptr(a.device))
     assert _lib.load().irc_gemm_workspace(0, 1, 0, M, N, K, 1) > 0
     torch.testing.assert_close(split, plain, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K", [(4000, 2100, 640), (4096, 2048, 768)])
+def test_big_tile_path(gpu, epi, out_dtype, M, N, K):
+    """256x256 global_load_lds path (bf16, A [M][K], B [N][K], K % 64 == 0, >= 128
+    tiles), ragged M / N, every fused epilogue, vs a torch fp32 reference."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(M + N + K + epi)
+    a = (torch.randn((M, K), generator=g) * 0.5).to(torch.bfloat16)
+    b = (torch.randn((N, K), generator=g) * 0.5).to(torch.bfloat16)
+    bias = torch.randn((N,), generator=g) if epi in (1, 2, 3) else None
+    res = torch.randn((M, N), generator=g).to(out_dtype) if epi in (3, 4) else None
+    out = ops.gemm(a.to(gpu), b.to(gpu), bias=None if bias is None else bias.to(gpu), epilogue=epi,
+                   residual=None if res is None else res.to(gpu), alpha=0.75,
+                   out_dtype=out_dtype)
+    ref = _ref(a, b, False, True, bias, epi, res, 0.75)
+    err = (out.float().cpu() - ref).abs()
+    tol = 2e-3 * K ** 0.5 + (2e-2 * ref.abs() if out_dtype == torch.bfloat16 else 0)
+    assert (err <= tol).all(), err.max().item()
+
+
+def test_big_tile_accumulate_fp32(gpu):
+    from irc_amd import ops
+
+    M, N, K = 2048, 4096, 1024
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn((M, K), generator=g).to(torch.bfloat16)
+    b = torch.randn((N, K), generator=g).to(torch.bfloat16)
+    c0 = torch.randn((M, N), generator=g)
+    out = c0.to(gpu)
+    ops.gemm(a.to(gpu), b.to(gpu), out=out, accumulate=True)
+    ref = c0 + a.float() @ b.float().t()
+    assert (out.cpu() - ref).abs().max().item() <= 2e-3 * K ** 0.5

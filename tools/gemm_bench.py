@@ -1,0 +1,61 @@
+"""GEMM microbenchmark on the training-step shapes (C2: 2x256 sequences x L=64).
+
+    python tools/gemm_bench.py [--iters 20]
+
+Prints one line per shape: M N K epilogue, us per launch (HIP events on the
+launch stream), TFLOP/s and the fraction of the 2.5 PF dense bf16 peak.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "information-retrieval-with-contrastive-learning_amd"))
+
+import torch  # noqa: E402
+
+SHAPES = [  # (name, M, N, K, epilogue)
+    ("qkv", 32768, 2304, 768, 1),
+    ("attn_out+res", 32768, 768, 768, 3),
+    ("ffn1+gelu", 32768, 3072, 768, 2),
+    ("ffn2+res", 32768, 768, 3072, 3),
+    ("lstm_xp_l0", 16384, 2048, 768, 1),
+    ("lstm_xp_l12", 16384, 2048, 512, 1),
+    ("lstm_dx", 16384, 512, 2048, 0),
+    ("square4k", 4096, 4096, 4096, 0),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    from irc_amd import ops
+
+    dev = torch.device("cuda:0")
+    for name, M, N, K, epi in SHAPES:
+        a = torch.randn((M, K), device=dev).to(torch.bfloat16)
+        b = torch.randn((N, K), device=dev).to(torch.bfloat16)
+        bias = torch.randn((N,), device=dev) if epi in (1, 2, 3) else None
+        res = torch.randn((M, N), device=dev).to(torch.bfloat16) if epi in (3, 4) else None
+        od = torch.float32 if name in ("lstm_dx",) or name.startswith("lstm_xp") else torch.bfloat16
+        if res is not None:
+            res = res.to(od)
+        out = torch.empty((M, N), device=dev, dtype=od)
+        for _ in range(3):
+            ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(args.iters):
+            ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
+        e1.record(st)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / args.iters
+        tf = 2.0 * M * N * K / us / 1e6
+        print(f"{name:14s} M={M:6d} N={N:5d} K={K:5d} epi={epi}  {us:9.1f} us  {tf:7.1f} TF/s  "
+              f"{tf / 2500:.1%}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
