@@ -63,6 +63,7 @@ struct Args {
   float alpha;
   int accumulate;  // C += result (fp32 C only)
   int vec_a, vec_b;  // operand rows 16-byte aligned: vector staging allowed
+  int vec_c;         // C (and R) rows 16-byte aligned and N % 8 == 0: vector epilogue
   int kchunk;        // split-K: K range of one blockIdx.z slice (multiple of BK)
   float* P;          // split-K partials [batch][split][M][N] (raw sums), or null
 };
@@ -433,6 +434,81 @@ __global__ __launch_bounds__(big::NT, 1) void gemm256_kernel(Args g) {
 
   const float* bias = g.bias ? g.bias + batch * g.sBias : nullptr;
   const TO* R = g.R ? reinterpret_cast<const TO*>(g.R) + batch * g.sR : nullptr;
+  if (g.vec_c) {
+    // Staged epilogue: the wave's 128x64 fp32 tile goes through LDS in two
+    // 64-row passes (16 KB per wave per pass; the k-loop's last barrier has
+    // retired every LDS read) and leaves as coalesced 16-byte row pieces, with
+    // bias / GELU before and residual / accumulate after, all in fp32 (one
+    // rounding, as the direct path).  Column bit 5 is XORed with row bit 2 so
+    // the two half-waves' ds_write_b32 (rows r and r+4) hit disjoint banks.
+    float* st = reinterpret_cast<float*>(&lds[0][0][0]) + wave * (64 * 64);
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cl = j * 32 + r32;
+        const int col = n0 + wn * 64 + cl;
+        const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESID) &&
+                                 col < g.N ? bias[col] : 0.f;
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int rl = i2 * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;  // row within the pass
+            float v = acc[pass * 2 + i2][j][e] * g.alpha + bv;
+            if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+            st[rl * 64 + (cl ^ (((rl >> 2) & 1) << 5))] = v;
+          }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int rbase = m0 + wm * 128 + pass * 64;
+      const int cbase = n0 + wn * 64;
+      if constexpr (sizeof(TO) == 2) {
+        // 8 lanes per 64-column row (8 bf16 = 16 B each), 8 rows per step
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int rl = it * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+          const int row = rbase + rl, col = cbase + c8;
+          if (row >= g.M || col >= g.N) continue;
+          const int sw = ((rl >> 2) & 1) << 5;
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(&st[rl * 64 + (c8 ^ sw)]);
+          const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * 64 + ((c8 + 4) ^ sw)]);
+          float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
+            const u16x8 rr = *reinterpret_cast<const u16x8*>(
+                reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[t] += bf16_to_f32(rr[t]);
+          }
+          u16x8 o;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) o[t] = f32_to_bf16(v[t]);
+          *reinterpret_cast<u16x8*>(reinterpret_cast<unsigned short*>(C) + (int64_t)row * g.ldc +
+                                    col) = o;
+        }
+      } else {
+        // 16 lanes per 64-column row (4 fp32 = 16 B each), 4 rows per step
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+          const int rl = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+          const int row = rbase + rl, col = cbase + c4;
+          if (row >= g.M || col >= g.N) continue;
+          const int sw = ((rl >> 2) & 1) << 5;
+          f32x4 v = *reinterpret_cast<const f32x4*>(&st[rl * 64 + (c4 ^ sw)]);
+          if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID)
+            v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(R) +
+                                                (int64_t)row * g.ldr + col);
+          float* dst = reinterpret_cast<float*>(C) + (int64_t)row * g.ldc + col;
+          if (g.accumulate) v += *reinterpret_cast<const f32x4*>(dst);
+          *reinterpret_cast<f32x4*>(dst) = v;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int col = n0 + wn * 64 + j * 32 + r32;
@@ -567,9 +643,14 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
   if (splits > 1 && (workspace == nullptr ||
                      workspace_bytes < (int64_t)splits * M * N * batch * (int64_t)sizeof(float)))
     splits = 1;
+  const int cvec = out_dtype == 0 ? 8 : 4;
+  const int vec_c = N % 8 == 0 && ldc % cvec == 0 && strideC % cvec == 0 &&
+                    ((uintptr_t)C % 16) == 0 &&
+                    (R == nullptr || (ldr % cvec == 0 && strideR % cvec == 0 &&
+                                      ((uintptr_t)R % 16) == 0));
   gemm::Args g{A, B, C, bias, R, (int)M, (int)N, (int)K, lda, ldb, ldc, ldr,
                strideA, strideB, strideC, strideR, strideBias, alpha, accumulate, vec_a, vec_b,
-               0, splits > 1 ? static_cast<float*>(workspace) : nullptr};
+               vec_c, 0, splits > 1 ? static_cast<float*>(workspace) : nullptr};
   hipStream_t st = as_stream(stream);
   const int nb = (int)batch;
   if (in_dtype == 0 && out_dtype == 0)
