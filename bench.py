@@ -14,7 +14,9 @@ N docs".  `value` = training pairs/s (whole job); `retrieval` = queries/s.
   -> 3-layer BiLSTM head 768->256x2->128 q fwd+bwd and momentum-encoder k fwd
   -> InfoNCE with the 12544-key queue -> clip + Adam + momentum update + enqueue.
   One step = 256 (anchor, positive) pairs.  N>1: data-parallel, each rank its
-  own 256 pairs, gradients summed over RCCL before the step (scaling: weak).
+  own 256 pairs; q/k embeddings all-gathered over RCCL so the InfoNCE negatives
+  span the global batch (256*N pairs), head gradients all-reduced before the
+  step (scaling: weak).
 * Retrieval (C2): each rank keeps a 100k-doc shard (D=768 bf16 unit-norm,
   seed 2024+rank) in HBM; one batch = 256 query embeddings all-gathered,
   scanned against every shard, reduced to the global top-100.
@@ -130,7 +132,7 @@ def run_train(args, rank, world, dev):
     opt = get_optimizer(ns, model)
     st = TrainState(ns, model, opt)
     if world > 1:
-        st.process_group = dist.group.WORLD
+        st.set_process_group(dist.group.WORLD)
     ids, mask = synthetic_batch(2 * TRAIN_B, TRAIN_L, 1337 + rank)
     ids, mask = ids.to(dev), mask.to(dev)
 
@@ -232,6 +234,7 @@ def run_scan(args, rank, world, dev):
     lib.irc_prof_enable(0)
     dt = _max_over_ranks(dt, dev, world)
     k_s, k_n, k_bytes = _prof(lib, "scan_filter")
+    sweep = scan_q_sweep(shard, dev) if rank == 0 else None
     kavg = k_s / max(k_n, 1)
     achieved = (k_bytes / max(k_n, 1)) / kavg / 1e9 if k_n else None
     return {
@@ -247,7 +250,39 @@ def run_scan(args, rank, world, dev):
                      "alg_bytes_per_launch": k_bytes / max(k_n, 1),
                      "mfma_tflops": 2 * SCAN_Q * SCAN_N_PER_GPU * SCAN_D / kavg / 1e12
                      if k_n else None},
+        "q_sweep_local": sweep,
     }
+
+
+def scan_q_sweep(shard, dev, qs=(1, 16, 64, 256), reps=20):
+    """Local scan filter at several query-batch sizes (SURVEY.md 8d grades the HBM
+    fraction at Q in {1, 16, 64, 256}): kernel HIP-event time and algorithmic bytes
+    (N*D*2 + Q*D*2) -> GB/s, plus the whole call's queries/s."""
+    from irc_amd import _lib, retrieval
+
+    lib = _lib.load()
+    out = []
+    for q in qs:
+        g = torch.Generator().manual_seed(11 + q)
+        qq = torch.nn.functional.normalize(torch.randn(q, SCAN_D, generator=g)).bfloat16().to(dev)
+        for _ in range(3):
+            retrieval.scan_topk(qq, shard, SCAN_K)
+        torch.cuda.synchronize()
+        lib.irc_prof_reset()
+        lib.irc_prof_enable(1)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            retrieval.scan_topk(qq, shard, SCAN_K)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        lib.irc_prof_enable(0)
+        k_s, k_n, k_bytes = _prof(lib, "scan_filter")
+        kavg = k_s / max(k_n, 1)
+        gbs = (k_bytes / max(k_n, 1)) / kavg / 1e9 if k_n else None
+        out.append({"Q": q, "filter_us": kavg * 1e6, "filter_GB_s": gbs,
+                    "hbm_frac": gbs / HBM_PEAK_GBS if gbs else None,
+                    "call_us": dt / reps * 1e6, "queries_per_s": q * reps / dt})
+    return out
 
 
 def cpu_baseline_scan(budget_s):

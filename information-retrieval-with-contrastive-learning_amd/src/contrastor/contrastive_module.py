@@ -21,6 +21,7 @@ import torch.nn as nn
 
 from irc_amd import ops
 from irc_amd._torch import side_stream
+from irc_amd.dist import gather_rows
 from irc_amd.bert import BertModel
 from irc_amd.lstm_head import LSTMHead, seq2vec as head_seq2vec
 from irc_amd.tokenizer import load_tokenizer
@@ -56,6 +57,8 @@ class RetrievalModelWrapper(nn.Module):
                                                     seed=int(bc.get("seed", 0)))
         self.bert_tokenizer = load_tokenizer(bc.get("vocab"), self.bert_model.config.vocab_size)
         self.bert_model.eval()
+        # data-parallel group for global in-batch negatives (None: single process)
+        self.dist_group = None
 
     @torch.no_grad()
     def bert_extract(self, d1, d2, device):
@@ -106,6 +109,10 @@ class RetrievalModelWrapper(nn.Module):
             emb_q = self.seq2vec(anchor_feat)
             emb_k = self.seq2vec(positive_feat, query=False) if self.use_momentum else \
                 self.seq2vec(positive_feat)
+        group = getattr(self, "dist_group", None)
+        if group is not None:  # global in-batch negatives (irc_amd.dist)
+            emb_q = gather_rows(emb_q, group)
+            emb_k = gather_rows(emb_k.detach(), group)
         queue = None if not self.use_queue or not self.add_queue_to_loss else self.queue
         loss = self.criterion(emb_q, emb_k, queue, cluster_result, indexes)
         if self.use_queue and self.training:

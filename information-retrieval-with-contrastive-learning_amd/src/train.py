@@ -69,6 +69,12 @@ class TrainState:
         # every rank applies the identical update.
         self.process_group = None
 
+    def set_process_group(self, group):
+        """Data-parallel training over ``group``: embeddings all-gathered for global
+        in-batch negatives (model.dist_group) + head gradients all-reduced."""
+        self.process_group = group
+        self.model.dist_group = group
+
     def _maybe_enable_queue(self):
         m = self.model
         if m.use_queue and self.step_sum >= self.cfg["loss"][self.args.loss]["queue_start_steps"] \
@@ -88,9 +94,9 @@ class TrainState:
         stepped = False
         if self.batch_size == self.acml or n_pairs != self.bsz:
             if self.process_group is not None:
-                import torch.distributed as dist
+                from irc_amd.dist import all_reduce_sum_
 
-                dist.all_reduce(self.model.encoder_q.flat_grad, group=self.process_group)
+                all_reduce_sum_(self.model.encoder_q.flat_grad, self.process_group)
             self.grad_norm = self.optimizer.clip_and_step(self.max_norm)
             if self.model.use_momentum:
                 self.model._momentum_update_key_encoder()
