@@ -339,24 +339,28 @@ inline int split_count(int TIbytes, int out_f32, int epi, int64_t M, int64_t N, 
 
 // ---------------------------------------------------------------------------
 // Large-tile bf16 path for K-contiguous operands (A [M][K], B [N][K]: the BERT
-// and LSTM-projection GEMMs).  256x256x64 block tile, 8 waves as 2(M) x 4(N),
-// 128x64 per wave = 4x2 blocks of v_mfma_f32_32x32x16_bf16.  Both tiles move
-// global -> LDS by global_load_lds_dwordx4 (no VGPR staging), double buffered
-// (128 KB LDS): tile k+1 is in flight while tile k is consumed.  LDS rows are
-// 128 B (64 k); the 16-byte chunk c of row r is stored at chunk c ^ (r & 7) so the
-// row-wise ds_read_b128 fragment reads are conflict free -- applied on the
-// SOURCE address, since the DMA destination is lane-linear.  Rows past M / N
-// load a clamped valid row and are never stored.  Requires K % 64 == 0, lda/ldb
-// % 8 == 0 and 16-byte aligned bases.
+// and LSTM-projection GEMMs).  256 x (128*WNB) x 64 block tile, 8 waves as
+// 2(M) x 4(N), 128 x 32*WNB per wave = 4 x WNB blocks of v_mfma_f32_32x32x16_bf16.
+// WNB = 3 (256x384) when N % 384 == 0 -- every BERT-base N (768, 2304, 3072), so
+// M = 32768 gives whole waves of tiles over 256 CUs -- else WNB = 2 (256x256).
+// Both tiles move global -> LDS by global_load_lds_dwordx4 (no VGPR staging),
+// double buffered (2 x 80 KB at WNB=3): tile k+1 is in flight while tile k is
+// consumed.  LDS rows are 128 B (64 k); the 16-byte chunk c of row r is stored at
+// chunk c ^ (r & 7) so the row-wise ds_read_b128 fragment reads are conflict
+// free -- applied on the SOURCE address, since the DMA destination is
+// lane-linear.  Rows past M / N load a clamped valid row and are never stored.
+// Requires K % 64 == 0, lda/ldb % 8 == 0 and 16-byte aligned bases.
 namespace big {
-constexpr int BM = 256, BN = 256, BK = 64, NW = 8, NT = NW * 64;
-constexpr int TILE_BYTES = BM * BK * 2;  // 32 KB per operand per stage
-constexpr int GL_PER_T = TILE_BYTES / (NT * 16);  // glds per thread per operand (4)
+constexpr int BM = 256, BK = 64, NW = 8, NT = NW * 64;
+constexpr int ROW_BYTES = BK * 2;  // 128
 
+// rows [0, nrows_tile) of one operand tile: nrows_tile*8 16-byte chunks, NT per pass
+template <int ROWS>
 __device__ __forceinline__ void stage(const unsigned short* __restrict__ X, int64_t ld, int r0,
                                       int nrows, int k0, char* lds_tile, int wave, int lane) {
+  constexpr int PASSES = ROWS * 8 / NT;
 #pragma unroll
-  for (int i = 0; i < GL_PER_T; ++i) {
+  for (int i = 0; i < PASSES; ++i) {
     const int p = (i * NW + wave) * 64 + lane;  // 16-byte LDS chunk index (lane-linear)
     const int row = p >> 3;
     const int c = (p & 7) ^ (row & 7);          // logical k-chunk stored at this slot
@@ -367,16 +371,20 @@ __device__ __forceinline__ void stage(const unsigned short* __restrict__ X, int6
 }
 }  // namespace big
 
-template <typename TO, int EPI>
-__global__ __launch_bounds__(big::NT, 1) void gemm256_kernel(Args g) {
-  using big::BK; using big::NT; using big::NW; using big::TILE_BYTES;
-  constexpr int BM = big::BM, BN = big::BN;
-  __shared__ __attribute__((aligned(1024))) char lds[2][2][big::TILE_BYTES];  // [stage][A/B]
+template <typename TO, int EPI, int WNB>
+__global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
+  using big::BK;
+  using big::NT;
+  using big::NW;
+  constexpr int BM = big::BM, BN = 128 * WNB;
+  constexpr int A_BYTES = BM * big::ROW_BYTES, B_BYTES = BN * big::ROW_BYTES;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];  // [stage][A | B]
   const int tiles_m = (g.M + BM - 1) / BM;
   const int tiles_n = (g.N + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
   int bid = blockIdx.x;
-  {
+  {  // XCD-aware bijective remap: blocks sharing an XCD walk consecutive tiles
     const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
@@ -391,41 +399,41 @@ __global__ __launch_bounds__(big::NT, 1) void gemm256_kernel(Args g) {
   const int wm = wave >> 2, wn = wave & 3;
   const int h = lane >> 5, r32 = lane & 31;
 
-  f32x16 acc[4][2];
+  f32x16 acc[4][WNB];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16)0.0f;
+    for (int j = 0; j < WNB; ++j) acc[i][j] = (f32x16)0.0f;
 
   const int nk = g.K / BK;
-  big::stage(A, g.lda, m0, g.M, 0, lds[0][0], wave, lane);
-  big::stage(B, g.ldb, n0, g.N, 0, lds[0][1], wave, lane);
+  big::stage<BM>(A, g.lda, m0, g.M, 0, lds, wave, lane);
+  big::stage<BN>(B, g.ldb, n0, g.N, 0, lds + A_BYTES, wave, lane);
   wait_vmcnt<0>();
   __syncthreads();
-  // fragment byte offsets within a stage: row r, logical chunk c -> r*128 + ((c ^ (r&7)) * 16)
   const int swz = r32 & 7;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      big::stage(A, g.lda, m0, g.M, (kt + 1) * BK, lds[cur ^ 1][0], wave, lane);
-      big::stage(B, g.ldb, n0, g.N, (kt + 1) * BK, lds[cur ^ 1][1], wave, lane);
+      char* nxt = lds + (cur ^ 1) * STAGE;
+      big::stage<BM>(A, g.lda, m0, g.M, (kt + 1) * BK, nxt, wave, lane);
+      big::stage<BN>(B, g.ldb, n0, g.N, (kt + 1) * BK, nxt + A_BYTES, wave, lane);
     }
-    const char* la = lds[cur][0];
-    const char* lb = lds[cur][1];
+    const char* la = lds + cur * STAGE;
+    const char* lb = la + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
       const int coff = (((2 * kk + h) ^ swz) * 16);
-      bf16x8 fa[4], fb[2];
+      bf16x8 fa[4], fb[WNB];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 32 + r32) * 128 + coff);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(lb + (wn * 64 + j * 32 + r32) * 128 + coff);
+      for (int j = 0; j < WNB; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(lb + (wn * 32 * WNB + j * 32 + r32) * 128 + coff);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < WNB; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
     wait_vmcnt<0>();
@@ -434,46 +442,48 @@ __global__ __launch_bounds__(big::NT, 1) void gemm256_kernel(Args g) {
 
   const float* bias = g.bias ? g.bias + batch * g.sBias : nullptr;
   const TO* R = g.R ? reinterpret_cast<const TO*>(g.R) + batch * g.sR : nullptr;
+  constexpr int WCOLS = 32 * WNB;  // columns per wave
   if (g.vec_c) {
-    // Staged epilogue: the wave's 128x64 fp32 tile goes through LDS in two
-    // 64-row passes (16 KB per wave per pass; the k-loop's last barrier has
-    // retired every LDS read) and leaves as coalesced 16-byte row pieces, with
-    // bias / GELU before and residual / accumulate after, all in fp32 (one
-    // rounding, as the direct path).  Column bit 5 is XORed with row bit 2 so
-    // the two half-waves' ds_write_b32 (rows r and r+4) hit disjoint banks.
-    float* st = reinterpret_cast<float*>(&lds[0][0][0]) + wave * (64 * 64);
+    // Staged epilogue: the wave's 128 x WCOLS fp32 tile goes through LDS in four
+    // 32-row passes (row pitch WCOLS+8 floats: rows r and r+4 of the two
+    // half-waves land 128 B apart in bank space, so the ds_write_b32 are
+    // conflict free) and leaves as coalesced 16-byte row pieces; bias / GELU
+    // before, residual / accumulate after, all fp32 (one rounding).
+    constexpr int PITCH = WCOLS + 8;
+    float* st = reinterpret_cast<float*>(lds) + wave * (32 * PITCH);
+    const int rbase0 = m0 + wm * 128;
+    const int cbase = n0 + wn * WCOLS;
+    float bv[WNB];
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int j = 0; j < WNB; ++j) {
+      const int col = cbase + j * 32 + r32;
+      bv[j] = (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESID) && col < g.N
+                  ? bias[col] : 0.f;
+    }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int cl = j * 32 + r32;
-        const int col = n0 + wn * 64 + cl;
-        const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESID) &&
-                                 col < g.N ? bias[col] : 0.f;
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int i2 = 0; i2 < 2; ++i2)
+      for (int j = 0; j < WNB; ++j)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int rl = i2 * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;  // row within the pass
-            float v = acc[pass * 2 + i2][j][e] * g.alpha + bv;
-            if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
-            st[rl * 64 + (cl ^ (((rl >> 2) & 1) << 5))] = v;
-          }
-      }
+        for (int e = 0; e < 16; ++e) {
+          const int rl = (e & 3) + 8 * (e >> 2) + 4 * h;
+          float v = acc[i][j][e] * g.alpha + bv[j];
+          if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+          st[rl * PITCH + j * 32 + r32] = v;
+        }
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const int rbase = m0 + wm * 128 + pass * 64;
-      const int cbase = n0 + wn * 64;
+      const int rbase = rbase0 + i * 32;
       if constexpr (sizeof(TO) == 2) {
-        // 8 lanes per 64-column row (8 bf16 = 16 B each), 8 rows per step
+        constexpr int CPR = WCOLS / 8;  // 16-byte bf16 chunks per row
 #pragma unroll
-        for (int it = 0; it < 8; ++it) {
-          const int rl = it * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+        for (int it = 0; it < 32 * CPR / 64; ++it) {
+          const int c = it * 64 + lane;
+          const int rl = c / CPR, c8 = (c % CPR) * 8;
           const int row = rbase + rl, col = cbase + c8;
           if (row >= g.M || col >= g.N) continue;
-          const int sw = ((rl >> 2) & 1) << 5;
-          const f32x4 v0 = *reinterpret_cast<const f32x4*>(&st[rl * 64 + (c8 ^ sw)]);
-          const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * 64 + ((c8 + 4) ^ sw)]);
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c8]);
+          const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c8 + 4]);
           float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
           if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
             const u16x8 rr = *reinterpret_cast<const u16x8*>(
@@ -488,14 +498,14 @@ __global__ __launch_bounds__(big::NT, 1) void gemm256_kernel(Args g) {
                                     col) = o;
         }
       } else {
-        // 16 lanes per 64-column row (4 fp32 = 16 B each), 4 rows per step
+        constexpr int CPR = WCOLS / 4;  // 16-byte fp32 chunks per row
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
-          const int rl = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+        for (int it = 0; it < 32 * CPR / 64; ++it) {
+          const int c = it * 64 + lane;
+          const int rl = c / CPR, c4 = (c % CPR) * 4;
           const int row = rbase + rl, col = cbase + c4;
           if (row >= g.M || col >= g.N) continue;
-          const int sw = ((rl >> 2) & 1) << 5;
-          f32x4 v = *reinterpret_cast<const f32x4*>(&st[rl * 64 + (c4 ^ sw)]);
+          f32x4 v = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c4]);
           if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID)
             v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(R) +
                                                 (int64_t)row * g.ldr + col);
@@ -510,8 +520,8 @@ __global__ __launch_bounds__(big::NT, 1) void gemm256_kernel(Args g) {
     return;
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn * 64 + j * 32 + r32;
+  for (int j = 0; j < WNB; ++j) {
+    const int col = n0 + wn * WCOLS + j * 32 + r32;
     if (col >= g.N) continue;
     const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESID) ? bias[col]
                                                                                         : 0.f;
@@ -544,27 +554,35 @@ __global__ __launch_bounds__(big::NT, 1) void gemm256_kernel(Args g) {
 }
 
 // The large-tile path applies: bf16 in, A [M][K] and B [N][K], aligned, K % 64,
-// and enough 256x256 tiles to occupy the chip.
-inline bool use_big(const Args& g, int batch, int la, int lb) {
-  if (la != ROW || lb != ROW || !g.vec_a || !g.vec_b) return false;
-  if (g.K % big::BK != 0 || g.K == 0) return false;
-  const int64_t tiles = (int64_t)((g.M + 255) / 256) * ((g.N + 255) / 256) * batch;
-  return tiles >= 128;
+// and enough tiles to occupy the chip.  Returns the per-wave N blocks (0: no).
+inline int big_wnb(const Args& g, int batch, int la, int lb) {
+  if (la != ROW || lb != ROW || !g.vec_a || !g.vec_b) return 0;
+  if (g.K % big::BK != 0 || g.K == 0) return 0;
+  const int wnb = g.N % 384 == 0 ? 3 : 2;
+  const int64_t tiles = (int64_t)((g.M + 255) / 256) * ((g.N + 128 * wnb - 1) / (128 * wnb)) * batch;
+  return tiles >= 128 ? wnb : 0;
 }
 
 template <typename TO, int EPI>
-static int launch_big(const Args& g, int batch, hipStream_t st) {
-  const int tiles = ((g.M + big::BM - 1) / big::BM) * ((g.N + big::BN - 1) / big::BN);
+static int launch_big(const Args& g, int batch, int wnb, hipStream_t st) {
+  const int bn = 128 * wnb;
+  const int tiles = ((g.M + big::BM - 1) / big::BM) * ((g.N + bn - 1) / bn);
   prof_begin(st);
-  hipLaunchKernelGGL((gemm256_kernel<TO, EPI>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
+  if (wnb == 3)
+    hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 3>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
+  else
+    hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 2>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
   prof_end("gemm_bf16", st, 2.0 * g.M * g.N * g.K * batch);
-  return check_launch("gemm256_kernel");
+  return check_launch("gemm_big_kernel");
 }
 
 template <typename TI, typename TO, int LA, int LB, int EPI>
 static int launch(const Args& g0, int batch, int splits, hipStream_t st) {
   if constexpr (sizeof(TI) == 2) {
-    if (splits == 1 && use_big(g0, batch, LA, LB)) return launch_big<TO, EPI>(g0, batch, st);
+    if (splits == 1) {
+      const int wnb = big_wnb(g0, batch, LA, LB);
+      if (wnb) return launch_big<TO, EPI>(g0, batch, wnb, st);
+    }
   }
   Args g = g0;
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);

@@ -127,10 +127,11 @@ def test_splitk_matches_unsplit(gpu):
 
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("M,N,K", [(4000, 2100, 640), (4096, 2048, 768)])
+@pytest.mark.parametrize("M,N,K", [(4000, 2100, 640), (4096, 2048, 768), (8000, 1536, 384)])
 def test_big_tile_path(gpu, epi, out_dtype, M, N, K):
-    """256x256 global_load_lds path (bf16, A [M][K], B [N][K], K % 64 == 0, >= 128
-    tiles), ragged M / N, every fused epilogue, vs a torch fp32 reference."""
+    """Large-tile global_load_lds path (bf16, A [M][K], B [N][K], K % 64 == 0, >= 128
+    tiles; 256x384 when N % 384 == 0 else 256x256), ragged M / N, every fused
+    epilogue, vs a torch fp32 reference."""
     from irc_amd import ops
 
     g = torch.Generator().manual_seed(M + N + K + epi)
