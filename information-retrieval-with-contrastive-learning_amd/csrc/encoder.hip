@@ -104,6 +104,63 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
   }
 }
 
+// bf16 LayerNorm for H % 256 == 0 (BERT-base 768, -large 1024): one half-wave
+// (32 lanes) per row, 16-byte loads/stores (H/256 chunks of 8 per lane), the
+// two half-waves of a wave on consecutive rows; statistics fp32 in the same
+// order-independent two-pass form as layernorm_kernel.
+template <int CPL>
+__global__ __launch_bounds__(256) void layernorm_vec_kernel(const unsigned short* __restrict__ x,
+                                                           unsigned short* __restrict__ y,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           int64_t rows, float eps) {
+  constexpr int H = CPL * 256;
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool ok = row < rows;
+  const unsigned short* xr = x + (ok ? row : 0) * H;
+  float v[CPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const u16x8 u = *reinterpret_cast<const u16x8*>(xr + (i * 32 + hl) * 8);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      v[i][t] = bf16_to_f32(u[t]);
+      s += v[i][t];
+    }
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / H;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float d = v[i][t] - mean;
+      s2 += d * d;
+    }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+  const float rstd = rsqrtf(s2 / H + eps);
+  if (!ok) return;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c0 = (i * 32 + hl) * 8;
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c0);
+    const f32x4 g1 = *reinterpret_cast<const f32x4*>(gamma + c0 + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + c0);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(beta + c0 + 4);
+    const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+    const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+    u16x8 o;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) o[t] = f32_to_bf16((v[i][t] - mean) * rstd * gg[t] + bb[t]);
+    *reinterpret_cast<u16x8*>(y + row * H + c0) = o;
+  }
+}
+
 // Attention: one workgroup per (sequence b, head a).  qkv is the fused
 // projection output [B*L, 3H] (cols [0,H)=Q, [H,2H)=K, [2H,3H)=V, head a at
 // a*dh); ctx [B*L, H].  K and V of the (b, a) pair are staged in LDS as fp32;
@@ -299,6 +356,24 @@ extern "C" int irc_layernorm(int dtype, const void* x, void* y, const float* gam
   IRC_REQUIRE(H >= 1 && H <= 64 * enc::MAXH_PER_LANE, "layernorm: H=%lld unsupported",
               (long long)H);
   if (rows == 0) return IRC_OK;
+  const bool al = ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 &&
+                  ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0;
+  if (dtype == 0 && al && (H == 768 || H == 1024 || H == 512)) {
+    const dim3 g8((unsigned)((rows + 7) / 8));
+    hipStream_t st = as_stream(stream);
+    prof_begin(st);
+    if (H == 768)
+      hipLaunchKernelGGL((enc::layernorm_vec_kernel<3>), g8, dim3(256), 0, st,
+                         (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
+    else if (H == 1024)
+      hipLaunchKernelGGL((enc::layernorm_vec_kernel<4>), g8, dim3(256), 0, st,
+                         (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
+    else
+      hipLaunchKernelGGL((enc::layernorm_vec_kernel<2>), g8, dim3(256), 0, st,
+                         (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
+    prof_end("layernorm", st, (double)rows * H * 4.0);
+    return check_launch("layernorm_vec_kernel");
+  }
   dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == 0)
     hipLaunchKernelGGL((enc::layernorm_kernel<unsigned short>), grid, dim3(256), 0,

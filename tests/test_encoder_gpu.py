@@ -1,0 +1,26 @@
+"""irc_layernorm vs a plain PyTorch fp32 reference of the same op (HF BertSelfOutput /
+BertOutput LayerNorm, eps 1e-12, reached from contrastive_module.py:39).
+
+bf16 rows with H in {512, 768, 1024} take the vectorised half-wave kernel, other
+shapes the one-wave-per-row kernel.  Tolerance: bf16 output rounding, 2e-2
+absolute on O(1) outputs; fp32 1e-5."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype,rows,H", [(torch.bfloat16, 1000, 768), (torch.bfloat16, 7, 1024),
+                                          (torch.bfloat16, 33, 512), (torch.bfloat16, 9, 300),
+                                          (torch.float32, 65, 768)])
+def test_layernorm(gpu, dtype, rows, H):
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(rows + H)
+    x = (torch.randn((rows, H), generator=g) * 3 + 1).to(dtype)
+    gamma = torch.rand((H,), generator=g) + 0.5
+    beta = torch.randn((H,), generator=g)
+    y = ops.layernorm(x.to(gpu), gamma.to(gpu), beta.to(gpu), eps=1e-12)
+    ref = torch.nn.functional.layer_norm(x.float(), (H,), gamma, beta, eps=1e-12)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert (y.float().cpu() - ref).abs().max().item() <= tol
