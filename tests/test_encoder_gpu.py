@@ -2,8 +2,8 @@
 BertOutput LayerNorm, eps 1e-12, reached from contrastive_module.py:39).
 
 bf16 rows with H in {512, 768, 1024} take the vectorised half-wave kernel, other
-shapes the one-wave-per-row kernel.  Tolerance: bf16 output rounding, 2e-2
-absolute on O(1) outputs; fp32 1e-5."""
+shapes the one-wave-per-row kernel.  Tolerance: bf16 output rounding
+(1e-3 + 4e-3 |y|); fp32 1e-5."""
 import pytest
 import torch
 
@@ -22,5 +22,6 @@ def test_layernorm(gpu, dtype, rows, H):
     beta = torch.randn((H,), generator=g)
     y = ops.layernorm(x.to(gpu), gamma.to(gpu), beta.to(gpu), eps=1e-12)
     ref = torch.nn.functional.layer_norm(x.float(), (H,), gamma, beta, eps=1e-12)
-    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
-    assert (y.float().cpu() - ref).abs().max().item() <= tol
+    # bf16: one output rounding (half-ulp = 2^-9 |y|) plus fp32 statistics
+    tol = (1e-3 + 4e-3 * ref.abs()) if dtype == torch.bfloat16 else 1e-5
+    assert ((y.float().cpu() - ref).abs() <= tol).all()
