@@ -141,6 +141,31 @@ int irc_lstm_fwd_mfma(const float* xp_packed, const void* whh_bf16, void* hout, 
 int irc_lstm_bwd_mfma(const float* dy, const void* whhT_bf16, const float* gsave,
                       const float* csave, void* dgates, int64_t B, int64_t L, int64_t H,
                       int64_t ndir, irc_stream_t stream);
+/* hprev bf16 [ndir][B*L][H] = h_{t-1} of each direction (0 at its first step). */
+int irc_lstm_hprev(const void* hout, void* hprev, int64_t B, int64_t L, int64_t H, int64_t ndir,
+                   irc_stream_t stream);
+
+/* Multi-CU recurrences (csrc/lstm_coop.hip), H = 256: each (32-sequence group,
+ * direction) is a cluster of 4 workgroups on 4 CUs, each holding a quarter of
+ * W_hh resident in LDS; the hidden state (forward) / partial dh (backward) is
+ * exchanged through L2 every step (write-through stores + flags, bounded spins).
+ * irc_lstm_coop_sizes(which): 0 gates floats, 1 c floats, 2 forward exchange
+ *   bytes, 3 backward exchange bytes, 4 sync bytes (flags + timeout word).
+ * irc_lstm_coop_pack: W_hh fp32 [ndir][4H][H] -> wf, wb bf16 (4H*H per dir each).
+ * irc_lstm_fwd_coop: xp_packed as irc_lstm_fwd_mfma; gsave/csave (NULL for the
+ *   no-grad encoder) in a layout private to the coop pair.  sync is zeroed by the
+ *   call; its last word is nonzero after a cluster timed out (never expected).
+ * irc_lstm_bwd_coop: dy fp32 [B*L][ndir*H] -> dgates bf16 [B*L][ndir*4H]. */
+int irc_lstm_coop_supported(int64_t H);
+int64_t irc_lstm_coop_sizes(int64_t B, int64_t L, int64_t H, int64_t ndir, int which);
+int irc_lstm_coop_pack(const float* whh, int64_t H, int64_t ndir, void* wf, void* wb,
+                       irc_stream_t stream);
+int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* hout, float* gsave,
+                      float* csave, void* xch, void* sync, int64_t B, int64_t L, int64_t H,
+                      int64_t ndir, irc_stream_t stream);
+int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* gsave, const float* csave,
+                      void* dgates, void* xch, void* sync, int64_t B, int64_t L, int64_t H,
+                      int64_t ndir, irc_stream_t stream);
 
 /* ------------------------------------------------- seq2vec tail + InfoNCE + optimizer
  * seq2vec mean-over-L (PAD included) + F.normalize (contrastive_module.py:102-112);

@@ -1,0 +1,488 @@
+// Multi-CU MFMA BiLSTM recurrences for the production head width H = 256
+// (reference: nn.LSTM in src/model.py:16-22, 39 -- gate order i, f, g, o, zero
+// initial state, the padded sequence processed as is).
+//
+// Why: a single-CU recurrence must stream all of W_hh (512 KB bf16 per
+// direction) through one CU every step; the per-CU L2 path bounds that at
+// ~3.4 us/step.  Here each (group of 32 sequences, direction) is a CLUSTER of
+// P = 4 workgroups, one per CU, each holding a quarter of W_hh resident in LDS
+// (128 KB) for the whole sequence, so the per-step traffic is only the hidden
+// state exchange.
+//
+// Forward: member m owns hidden units [64m, 64m+64) and all four gates of them;
+//   per step gates[32 x 256] = xp_t + h_{t-1}[32 x 256] . W_slice with
+//   v_mfma_f32_16x16x32_bf16 (wave w: 16 units x 4 gates, 2 row blocks); the
+//   cell update is lane-local (c in registers); the member's 4 KB slice of h_t
+//   is published and the other three slices gathered into LDS.
+// Backward (K-split): member m holds dgates of its own units (32 x 256: the A
+//   operand, local) and W_hh rows of those gate columns; it computes a PARTIAL
+//   dh over all 256 units, publishes it (fp32), and sums the four partials of
+//   its own units in member order 0..3 (deterministic).
+//
+// Inter-workgroup hand-off (cdna_hip_programming.md Guideline 16, form R1 with
+// sc1 loads): payload stored write-through (relaxed agent-scope 8-byte atomic
+// stores = global_store sc1); every storing wave drains (s_waitcnt vmcnt(0));
+// workgroup barrier; ONE lane stores the member's flag (relaxed agent atomic);
+// ONE wave polls the flags relaxed (>= epoch) with bounded spins; barrier; every
+// load of the payload is a relaxed agent-scope atomic load (global_load sc1).
+// Exchange buffers are double-buffered by step parity (a member can be at most
+// one step ahead of any other).  Flags are zeroed by hipMemsetAsync every call.
+// Co-residency: <= 16 groups per launch (<= 128 workgroups per direction pair,
+// one per CU by LDS), so two concurrent launches (query and key encoders) fit
+// the 256 CUs; spins are bounded and set a timeout word instead of hanging.
+#include "irc_common.h"
+
+namespace irc {
+namespace lstmc {
+
+constexpr int H = 256;
+constexpr int P = 4;            // workgroups per cluster
+constexpr int BG = 32;          // sequences per group
+constexpr int NW = 4;           // waves per workgroup
+constexpr int NTH = NW * 64;
+constexpr int UPW = H / P;      // 64 units per member
+constexpr int UPV = UPW / NW;   // 16 units per wave (forward)
+constexpr int KKF = H / 32;     // forward k-steps (K = 256)
+constexpr int HP = H + 8;       // LDS row pitch (bf16) of h / dgates
+constexpr int WSLICE = 4 * UPW * H;          // bf16 elements of one member's W slice (64K)
+constexpr int GSTEP = BG * 4 * H;            // floats of gates per (dir, group, t)
+constexpr int CSTEP = BG * H;                // floats of c per (dir, group, t)
+constexpr int MAX_GROUPS = 16;               // per launch (co-residency bound)
+constexpr unsigned SPIN_MAX = 1u << 24;
+
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_f(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
+
+__device__ __forceinline__ void st_sc1(void* p, unsigned long long v) {
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_sc1(const void* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Publish: every storing wave drains, barrier, one lane raises the member's flag.
+__device__ __forceinline__ void publish(unsigned* flag, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0 polls the P member flags until all >= epoch; returns false (all threads)
+// on timeout.  Ends with a barrier: the payload loads follow it.
+__device__ __forceinline__ bool wait_members(unsigned* flags, unsigned epoch, unsigned* tmo,
+                                             int* abort_lds) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned spins = 0;
+    for (;;) {
+      const unsigned v = lane < P ? __hip_atomic_load((gu32*)(flags + lane), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : 0xffffffffu;
+      if (__all(v >= epoch)) break;
+      if (++spins > SPIN_MAX) {
+        if (lane == 0) {
+          __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *abort_lds = 1;
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  return *abort_lds == 0;
+}
+
+// Cluster decode: blocks b, b+8, b+16, b+24 of each 32-block chunk are the 4
+// members of group (chunk*8 + b%8) -- same XCD (speed only, never correctness).
+struct Member {
+  int m, grp, dir;
+};
+__device__ __forceinline__ Member decode() {
+  const int bx = blockIdx.x;
+  const int rest = bx >> 3;
+  return Member{rest & 3, (rest >> 2) * 8 + (bx & 7), (int)blockIdx.y};
+}
+
+// ---------------------------------------------------------------- forward
+// xp [B*L][ndir*4H] fp32 with per-unit interleaved gates (column 4u+g, plus
+// b_ih + b_hh), wpk [ndir][P][NW][4][KKF][64][8] bf16 (forward fragments),
+// hout [B*L][ndir*H] bf16; gsave/csave (may be null) in the member-fragment
+// order read back by lstm_bwd_coop; xch [ndir][ngrp][2][BG][H] bf16, flags
+// [ndir][ngrp][P] (zeroed), tmo [1].
+__global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
+    const float* __restrict__ xp, const unsigned short* __restrict__ wpk,
+    unsigned short* __restrict__ hout, float* __restrict__ gsave, float* __restrict__ csave,
+    unsigned short* xch, unsigned* flags, unsigned* tmo, int B, int L, int ndir, int grp0,
+    int ngrp_launch, int ngrp_total) {
+  __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
+  __shared__ __attribute__((aligned(16))) unsigned short hb[BG][HP];
+  __shared__ int abort_lds;
+  const Member mb = decode();
+  if (mb.grp >= ngrp_launch) return;  // the whole cluster is absent
+  const int m = mb.m, dir = mb.dir, grp = grp0 + mb.grp;
+  if (grp >= ngrp_total) return;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int b0 = grp * BG;
+  const int64_t xld = (int64_t)ndir * 4 * H, hld = (int64_t)ndir * H;
+
+  {  // resident W slice + zero h_{-1}
+    const u16x8* src = reinterpret_cast<const u16x8*>(wpk + (int64_t)(dir * P + m) * WSLICE);
+    u16x8* dst = reinterpret_cast<u16x8*>(wl);
+    for (int i = threadIdx.x; i < WSLICE / 8; i += NTH) dst[i] = src[i];
+    for (int i = threadIdx.x; i < BG * HP; i += NTH) (&hb[0][0])[i] = 0;
+    if (threadIdx.x == 0) abort_lds = 0;
+  }
+  const int u = m * UPW + w * UPV + r16;  // this lane's hidden unit
+  float c[2][4];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[rb][i] = 0.f;
+  auto load_xp = [&](int t, f32x4 (&dst)[2][4]) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int b = b0 + rb * 16 + 4 * q4 + i;
+        b = b < B ? b : B - 1;
+        dst[rb][i] = *reinterpret_cast<const f32x4*>(xp + ((int64_t)b * L + t) * xld +
+                                                     (int64_t)dir * 4 * H + 4 * u);
+      }
+  };
+  f32x4 xr[2][4];
+  load_xp(dir == 0 ? 0 : L - 1, xr);
+  unsigned short* X = xch + (int64_t)(dir * ngrp_total + grp) * 2 * BG * H;
+  unsigned* fl = flags + (dir * ngrp_total + grp) * P;
+  __syncthreads();
+
+  for (int s = 0; s < L; ++s) {
+    const int t = dir == 0 ? s : L - 1 - s;
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[rb][g][i] = xr[rb][i][g];
+    if (s + 1 < L) load_xp(dir == 0 ? t + 1 : t - 1, xr);
+    if (s > 0) {
+#pragma unroll 2
+      for (int kk = 0; kk < KKF; ++kk) {
+        bf16x8 a[2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+          a[rb] = *reinterpret_cast<const bf16x8*>(&hb[rb * 16 + r16][kk * 32 + 8 * q4]);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(
+              &wl[(((w * 4 + g) * KKF + kk) * 64 + lane) * 8]);
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+            acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw, acc[rb][g], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // every read of h_{t-1} done
+    float* gs = gsave ? gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP : nullptr;
+    float* cs = csave ? csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP : nullptr;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      f32x4 cv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float ig = sigm(acc[rb][0][i]);
+        const float fg = sigm(acc[rb][1][i]);
+        const float g2 = tanh_f(acc[rb][2][i]);
+        const float og = sigm(acc[rb][3][i]);
+        const float cn = fg * c[rb][i] + ig * g2;
+        c[rb][i] = cn;
+        hb[rb * 16 + 4 * q4 + i][u] = f32_to_bf16(og * tanh_f(cn));
+        if (gs) {
+          const f32x4 gv = {ig, fg, g2, og};
+          *reinterpret_cast<f32x4*>(gs + ((((m * NW + w) * 2 + rb) * 4 + i) * 64 + lane) * 4) = gv;
+        }
+        cv[i] = cn;
+      }
+      if (cs) *reinterpret_cast<f32x4*>(cs + (((m * NW + w) * 2 + rb) * 64 + lane) * 4) = cv;
+    }
+    __syncthreads();  // own slice of h_t complete in LDS
+    if (s + 1 < L) {  // publish the own slice (write-through) for the other members
+      unsigned short* Xp = X + (s & 1) * BG * H;
+      for (int p = threadIdx.x; p < BG * UPW / 4; p += NTH) {
+        const int row = p / (UPW / 4), col = m * UPW + (p % (UPW / 4)) * 4;
+        st_sc1(Xp + row * H + col, *reinterpret_cast<const unsigned long long*>(&hb[row][col]));
+      }
+    }
+    for (int p = threadIdx.x; p < BG * UPW / 8; p += NTH) {  // h_t -> hout (own slice)
+      const int row = p / (UPW / 8), col = m * UPW + (p % (UPW / 8)) * 8;
+      if (b0 + row < B)
+        *reinterpret_cast<u16x8*>(hout + ((int64_t)(b0 + row) * L + t) * hld + dir * H + col) =
+            *reinterpret_cast<const u16x8*>(&hb[row][col]);
+    }
+    if (s + 1 < L) {
+      publish(fl + m, (unsigned)(s + 1));
+      if (!wait_members(fl, (unsigned)(s + 1), tmo, &abort_lds)) return;
+      const unsigned short* Xp = X + (s & 1) * BG * H;
+      for (int p = threadIdx.x; p < BG * H / 4; p += NTH) {
+        const int row = p / (H / 4), col = (p % (H / 4)) * 4;
+        if (col / UPW == m) continue;
+        *reinterpret_cast<unsigned long long*>(&hb[row][col]) = ld_sc1(Xp + row * H + col);
+      }
+      __syncthreads();  // h_t complete for the next step
+    }
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// dy [B*L][ndir*H] fp32; wtpk [ndir][P][NW][4 cb][KKB][64][8] bf16: member m's
+// rows of W_hh (its 256 gate columns, k order g*64 + local unit) as B fragments
+// for all 256 output units (wave w: units 64w + 16cb + lane&15); gsave/csave from
+// lstm_fwd_coop; dg out [B*L][ndir*4H] bf16 (original gate order); xch fp32
+// [ndir][ngrp][2][P][64 units/wave-block ... fragment order] partials, flags, tmo.
+constexpr int KKB = 4 * UPW / 32;  // 8 k-steps over the member's 256 gate columns
+constexpr int PART = BG * H;       // floats of one member's partial dh
+
+__global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
+    const float* __restrict__ dy, const unsigned short* __restrict__ wtpk,
+    const float* __restrict__ gsave, const float* __restrict__ csave,
+    unsigned short* __restrict__ dg, float* xch, unsigned* flags, unsigned* tmo, int B, int L,
+    int ndir, int grp0, int ngrp_launch, int ngrp_total) {
+  __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
+  __shared__ __attribute__((aligned(16))) unsigned short dgl[BG][HP];  // own dgates, k = g*64+lu
+  __shared__ int abort_lds;
+  const Member mb = decode();
+  if (mb.grp >= ngrp_launch) return;
+  const int m = mb.m, dir = mb.dir, grp = grp0 + mb.grp;
+  if (grp >= ngrp_total) return;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r16 = lane & 15, q4 = lane >> 4;
+  const int b0 = grp * BG;
+  const int64_t hld = (int64_t)ndir * H, gld = (int64_t)ndir * 4 * H;
+  {
+    const u16x8* src = reinterpret_cast<const u16x8*>(wtpk + (int64_t)(dir * P + m) * WSLICE);
+    u16x8* dst = reinterpret_cast<u16x8*>(wl);
+    for (int i = threadIdx.x; i < WSLICE / 8; i += NTH) dst[i] = src[i];
+    if (threadIdx.x == 0) abort_lds = 0;
+  }
+  // cell ownership as in the forward: lane -> unit u (own), rows rb*16 + 4*q4 + i
+  const int lu = w * UPV + r16;  // local unit 0..63
+  const int u = m * UPW + lu;
+  float dc[2][4];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dc[rb][i] = 0.f;
+  float* X = xch + (int64_t)(dir * ngrp_total + grp) * 2 * P * PART;
+  unsigned* fl = flags + (dir * ngrp_total + grp) * P;
+  __syncthreads();
+
+  for (int s = 0; s < L; ++s) {
+    const int t = dir == 0 ? L - 1 - s : s;   // reverse of the forward order
+    const int tp = dir == 0 ? t - 1 : t + 1;  // previous forward step
+    const bool has_prev = tp >= 0 && tp < L;
+    // dh from dgates of the step after (K-split partial over own gate columns)
+    f32x4 dh[2];  // own cells' summed recurrent gradient
+    dh[0] = dh[1] = (f32x4)0.f;
+    if (s > 0) {
+      f32x4 acc[2][4];  // partial for units 64w + 16cb + r16
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = (f32x4)0.f;
+#pragma unroll 2
+      for (int kk = 0; kk < KKB; ++kk) {
+        bf16x8 a[2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+          a[rb] = *reinterpret_cast<const bf16x8*>(&dgl[rb * 16 + r16][kk * 32 + 8 * q4]);
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(
+              &wl[(((w * 4 + cb) * KKB + kk) * 64 + lane) * 8]);
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw, acc[rb][cb], 0, 0, 0);
+        }
+      }
+      // publish the partial: block (wave w = unit block 64w, cb, rb) in the lane order
+      // the consumer member (w) reads it back
+      float* Xp = X + (int64_t)((s & 1) * P + m) * PART;
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          float* dst = Xp + (((w * 4 + cb) * 2 + rb) * 64 + lane) * 4;
+          const f32x4 v = acc[rb][cb];
+          st_sc1(dst, __builtin_bit_cast(unsigned long long, (float __attribute__((ext_vector_type(2)))){v[0], v[1]}));
+          st_sc1(dst + 2, __builtin_bit_cast(unsigned long long, (float __attribute__((ext_vector_type(2)))){v[2], v[3]}));
+        }
+      publish(fl + m, (unsigned)s);
+      if (!wait_members(fl, (unsigned)s, tmo, &abort_lds)) return;
+      // own units live in every member's block m, cb = w: sum in member order
+#pragma unroll
+      for (int mm = 0; mm < P; ++mm) {
+        const float* src = X + (int64_t)((s & 1) * P + mm) * PART;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          const float* p = src + (((m * 4 + w) * 2 + rb) * 64 + lane) * 4;
+          const unsigned long long lo = ld_sc1(p), hi = ld_sc1(p + 2);
+          const auto a2 = __builtin_bit_cast(float __attribute__((ext_vector_type(2))), lo);
+          const auto b2 = __builtin_bit_cast(float __attribute__((ext_vector_type(2))), hi);
+          dh[rb][0] += a2[0];
+          dh[rb][1] += a2[1];
+          dh[rb][2] += b2[0];
+          dh[rb][3] += b2[1];
+        }
+      }
+    }
+    __syncthreads();  // all reads of dgl (MFMA) done before it is overwritten
+    const float* gs = gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP;
+    const float* cs = csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP;
+    const float* csp =
+        has_prev ? csave + ((int64_t)(dir * ngrp_total + grp) * L + tp) * CSTEP : nullptr;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int64_t co = (((m * NW + w) * 2 + rb) * 64 + lane) * 4;
+      const f32x4 cv = *reinterpret_cast<const f32x4*>(cs + co);
+      const f32x4 cp = csp ? *reinterpret_cast<const f32x4*>(csp + co) : (f32x4)0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = rb * 16 + 4 * q4 + i;
+        const f32x4 gv =
+            *reinterpret_cast<const f32x4*>(gs + ((((m * NW + w) * 2 + rb) * 4 + i) * 64 + lane) * 4);
+        const float ig = gv[0], fg = gv[1], gg = gv[2], og = gv[3];
+        int b = b0 + row;
+        const float dyv = b < B ? dy[((int64_t)b * L + t) * hld + dir * H + u] : 0.f;
+        const float dht = dyv + dh[rb][i];
+        const float tc = tanh_f(cv[i]);
+        const float dct = dht * og * (1.f - tc * tc) + dc[rb][i];
+        dc[rb][i] = dct * fg;
+        dgl[row][0 * UPW + lu] = f32_to_bf16(dct * gg * ig * (1.f - ig));
+        dgl[row][1 * UPW + lu] = f32_to_bf16(dct * cp[i] * fg * (1.f - fg));
+        dgl[row][2 * UPW + lu] = f32_to_bf16(dct * ig * (1.f - gg * gg));
+        dgl[row][3 * UPW + lu] = f32_to_bf16(dht * tc * og * (1.f - og));
+      }
+    }
+    __syncthreads();  // own dgates complete: next step's A operand, and the dg rows
+    for (int p = threadIdx.x; p < BG * 4 * UPW / 8; p += NTH) {
+      const int row = p / (4 * UPW / 8), r = p % (4 * UPW / 8);
+      const int g = r / (UPW / 8), c8 = (r % (UPW / 8)) * 8;
+      if (b0 + row < B)
+        *reinterpret_cast<u16x8*>(dg + ((int64_t)(b0 + row) * L + t) * gld + dir * 4 * H + g * H +
+                                  m * UPW + c8) =
+            *reinterpret_cast<const u16x8*>(&dgl[row][g * UPW + c8]);
+    }
+  }
+}
+
+// W_hh [ndir][4H][H] fp32 -> the resident slices of both recurrences (bf16).
+//  fwd: [dir][m][w][g][kk][lane][8] = W[g*H + 64m + 16w + (lane&15)][kk*32 + 8(lane>>4) + j]
+//  bwd: [dir][m][w][cb][kk][lane][8] = W[g*H + 64m + lu][64w + 16cb + (lane&15)] with
+//       k = kk*32 + 8(lane>>4) + j = g*64 + lu  (the member's gate columns)
+__global__ void pack_coop_kernel(const float* __restrict__ whh, unsigned short* __restrict__ wf,
+                                 unsigned short* __restrict__ wb, int ndir) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)P * WSLICE;  // = 4H*H
+  if (e >= per * ndir) return;
+  const int dir = (int)(e / per);
+  int64_t r = e % per;
+  const int j = (int)(r & 7), lane = (int)((r >> 3) & 63);
+  const int kk = (int)((r >> 9) % KKF);
+  const int x = (int)((r >> 9) / KKF);  // ((m*NW + w)*4 + g|cb)
+  const int gc = x & 3, w = (x >> 2) % NW, m = (x >> 2) / NW;
+  const float* W = whh + dir * per;
+  {
+    const int u = m * UPW + w * UPV + (lane & 15);
+    const int k = kk * 32 + 8 * (lane >> 4) + j;
+    wf[e] = f32_to_bf16(W[(int64_t)(gc * H + u) * H + k]);
+  }
+  {
+    const int n = w * 64 + gc * 16 + (lane & 15);       // output unit
+    const int k = kk * 32 + 8 * (lane >> 4) + j;        // member-local gate column
+    const int g = k / UPW, lu = k % UPW;
+    wb[e] = f32_to_bf16(W[(int64_t)(g * H + m * UPW + lu) * H + n]);
+  }
+}
+
+}  // namespace lstmc
+}  // namespace irc
+
+using namespace irc;
+
+extern "C" int irc_lstm_coop_supported(int64_t H) { return H == lstmc::H; }
+
+extern "C" int64_t irc_lstm_coop_sizes(int64_t B, int64_t L, int64_t H, int64_t ndir, int which) {
+  // 0: gates floats, 1: c floats, 2: fwd exchange bytes, 3: bwd exchange bytes, 4: flag bytes
+  const int64_t ngrp = (B + lstmc::BG - 1) / lstmc::BG;
+  switch (which) {
+    case 0: return ndir * ngrp * L * lstmc::GSTEP;
+    case 1: return ndir * ngrp * L * lstmc::CSTEP;
+    case 2: return ndir * ngrp * 2 * lstmc::BG * H * 2;
+    case 3: return ndir * ngrp * 2 * lstmc::P * lstmc::PART * 4;
+    case 4: return ((ndir * ngrp * lstmc::P + 1) * 4 + 15) / 16 * 16;
+  }
+  return -1;
+}
+
+extern "C" int irc_lstm_coop_pack(const float* whh, int64_t H, int64_t ndir, void* wf, void* wb,
+                                  irc_stream_t stream) {
+  IRC_REQUIRE(H == lstmc::H, "lstm_coop_pack: H=%lld", (long long)H);
+  const int64_t n = ndir * 4 * H * H;
+  hipLaunchKernelGGL(lstmc::pack_coop_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     as_stream(stream), whh, (unsigned short*)wf, (unsigned short*)wb, (int)ndir);
+  return check_launch("lstm_coop_pack");
+}
+
+// sync: flags (ndir*ngrp*P words) followed by the timeout word; zeroed here.
+extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* hout, float* gsave,
+                                 float* csave, void* xch, void* sync, int64_t B, int64_t L,
+                                 int64_t H, int64_t ndir, irc_stream_t stream) {
+  IRC_REQUIRE(H == lstmc::H, "lstm_fwd_coop: H=%lld", (long long)H);
+  IRC_REQUIRE((gsave == nullptr) == (csave == nullptr), "lstm_fwd_coop: gsave/csave together");
+  if (B == 0 || L == 0) return IRC_OK;
+  hipStream_t st = as_stream(stream);
+  const int ngrp = (int)((B + lstmc::BG - 1) / lstmc::BG);
+  unsigned* flags = static_cast<unsigned*>(sync);
+  unsigned* tmo = flags + ndir * ngrp * lstmc::P;
+  hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
+  prof_begin(st);
+  for (int g0 = 0; g0 < ngrp; g0 += lstmc::MAX_GROUPS) {
+    const int n = ngrp - g0 < lstmc::MAX_GROUPS ? ngrp - g0 : lstmc::MAX_GROUPS;
+    const dim3 grid((unsigned)((n + 7) / 8 * 32), (unsigned)ndir);
+    hipLaunchKernelGGL(lstmc::lstm_fwd_coop, grid, dim3(lstmc::NTH), 0, st, xp_packed,
+                       (const unsigned short*)wf, (unsigned short*)hout, gsave, csave,
+                       (unsigned short*)xch, flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp);
+  }
+  prof_end("lstm_fwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
+  return check_launch("lstm_fwd_coop");
+}
+
+extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* gsave,
+                                 const float* csave, void* dg, void* xch, void* sync, int64_t B,
+                                 int64_t L, int64_t H, int64_t ndir, irc_stream_t stream) {
+  IRC_REQUIRE(H == lstmc::H, "lstm_bwd_coop: H=%lld", (long long)H);
+  if (B == 0 || L == 0) return IRC_OK;
+  hipStream_t st = as_stream(stream);
+  const int ngrp = (int)((B + lstmc::BG - 1) / lstmc::BG);
+  unsigned* flags = static_cast<unsigned*>(sync);
+  unsigned* tmo = flags + ndir * ngrp * lstmc::P;
+  hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
+  prof_begin(st);
+  for (int g0 = 0; g0 < ngrp; g0 += lstmc::MAX_GROUPS) {
+    const int n = ngrp - g0 < lstmc::MAX_GROUPS ? ngrp - g0 : lstmc::MAX_GROUPS;
+    const dim3 grid((unsigned)((n + 7) / 8 * 32), (unsigned)ndir);
+    hipLaunchKernelGGL(lstmc::lstm_bwd_coop, grid, dim3(lstmc::NTH), 0, st, dy,
+                       (const unsigned short*)wb, gsave, csave, (unsigned short*)dg, (float*)xch,
+                       flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp);
+  }
+  prof_end("lstm_bwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
+  return check_launch("lstm_bwd_coop");
+}

@@ -397,6 +397,15 @@ extern "C" int irc_lstm_fwd_mfma(const float* xp_packed, const void* whh_bf16, v
   return check_launch("hprev_kernel");
 }
 
+extern "C" int irc_lstm_hprev(const void* hout, void* hprev, int64_t B, int64_t L, int64_t H,
+                              int64_t ndir, irc_stream_t stream) {
+  if (B == 0 || L == 0) return IRC_OK;
+  hipLaunchKernelGGL(lstmm::hprev_kernel, dim3(nb256(ndir * B * L * H)), dim3(256), 0,
+                     as_stream(stream), (const unsigned short*)hout, (unsigned short*)hprev, (int)B,
+                     (int)L, (int)H, (int)ndir);
+  return check_launch("hprev_kernel");
+}
+
 extern "C" int irc_lstm_bwd_mfma(const float* dy, const void* whhT_bf16, const float* gsave,
                                  const float* csave, void* dg, int64_t B, int64_t L, int64_t H,
                                  int64_t ndir, irc_stream_t stream) {

@@ -23,6 +23,7 @@ per layer BPTT kernel -> weight-gradient GEMMs over all (b, t).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -181,24 +182,42 @@ class LSTMHead(nn.Module):
         bhh = flat[o[f"lstm.bias_hh_l{l}"]:][:nd * 4 * H]
         return wih, bih, bhh, whh
 
+    def _recurrence(self, dt):
+        """'coop' (multi-CU MFMA, bf16 at H=256), 'mfma' (single-CU MFMA) or 'valu'
+        (any width, and the fp32 parity mode).  IRC_LSTM_RECURRENCE overrides."""
+        if dt != torch.bfloat16:
+            return "valu"
+        want = os.environ.get("IRC_LSTM_RECURRENCE", "coop")
+        if want == "coop" and ops.lstm_coop_supported(self.hidden):
+            return "coop"
+        if want in ("coop", "mfma") and ops.lstm_mfma_supported(self.hidden):
+            return "mfma"
+        return "valu"
+
     def _use_mfma(self, dt):
-        return dt == torch.bfloat16 and ops.lstm_mfma_supported(self.hidden)
+        return self._recurrence(dt) != "valu"
 
     def _layer_fwd(self, l, x, B, L, dt, save):
         """One BiLSTM layer: (hout, saved-for-BPTT or None)."""
         H, nd = self.hidden, self.ndir
-        if self._use_mfma(dt):
+        kind = self._recurrence(dt)
+        if kind in ("coop", "mfma"):
             # MFMA recurrence: packed W_ih columns so xp is read as per-unit float4s
             wih, bih, bhh, whh = self._layer_fp32(l)
             wp, bp, w, wT = ops.lstm_pack(wih, bih, bhh, whh, H, nd)
             xp = ops.gemm(x, wp, bias=bp, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
-            hout, gsave, csave, hprev = ops.lstm_fwd_mfma(xp, w, B, L, H, nd, save=save)
+            if kind == "coop":
+                wf, wb = ops.lstm_coop_pack(whh, H, nd)
+                hout, gsave, csave, hprev, _ = ops.lstm_fwd_coop(xp, wf, B, L, H, nd, save=save)
+                wT = wb
+            else:
+                hout, gsave, csave, hprev = ops.lstm_fwd_mfma(xp, w, B, L, H, nd, save=save)
             wih_c = ops.cast_bf16(wih) if (save and l > 0) else None  # dx GEMM operand
-            return hout, ((True, x, wih_c, wT, gsave, csave, hprev) if save else None)
+            return hout, ((kind, x, wih_c, wT, gsave, csave, hprev) if save else None)
         wih, whh, bias = self._layer_weights(l, dt)
         xp = ops.gemm(x, wih, bias=bias, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
         hout, gsave, csave, hprev = ops.lstm_fwd(xp, whh, B, L, H, nd, dt, save=save)
-        return hout, ((False, x, wih, whh, gsave, csave, hprev) if save else None)
+        return hout, (("valu", x, wih, whh, gsave, csave, hprev) if save else None)
 
     def forward_compute(self, features: torch.Tensor, save: bool):
         """features [B, L, In] -> (emb [B, D] fp32 unit-norm, saved state or None)."""
@@ -235,9 +254,9 @@ class LSTMHead(nn.Module):
         dmh = ops.gemm(dm, self.view("scaling_layer.0.weight"), b_is_nk=False)  # [B, 2H]
         dy = ops.bcast_rows(dmh, B, L, 1.0 / L)  # [B*L, 2H] fp32
         for l in range(self.num_layers - 1, -1, -1):
-            mfma, x, wih, whh, gsave, csave, hprev = layers[l]
-            if mfma:
-                dy = self._layer_bwd_mfma(l, dy, x, wih, whh, gsave, csave, hprev, B, L)
+            kind, x, wih, whh, gsave, csave, hprev = layers[l]
+            if kind in ("coop", "mfma"):
+                dy = self._layer_bwd_mfma(l, dy, x, wih, whh, gsave, csave, hprev, B, L, kind)
                 if l == 0:
                     torch.cuda.current_stream(x.device).wait_stream(self._wgrad_pending)
                 continue
@@ -259,7 +278,7 @@ class LSTMHead(nn.Module):
                                   out_dtype=torch.float32)
             dy = dx
 
-    def _layer_bwd_mfma(self, l, dy, x, wih_c, whhT, gsave, csave, hprev, B, L):
+    def _layer_bwd_mfma(self, l, dy, x, wih_c, whhT, gsave, csave, hprev, B, L, kind="mfma"):
         """BPTT of one layer on the MFMA path; returns dL/dx (None for layer 0).
 
         dgates [B*L, ndir*4H] bf16 -> both directions' dW_ih / dW_hh as one batched
@@ -268,7 +287,10 @@ class LSTMHead(nn.Module):
         H, nd = self.hidden, self.ndir
         g = self.flat_grad
         o = self.offsets
-        dg = ops.lstm_bwd_mfma(dy, whhT, gsave, csave, B, L, H, nd)
+        if kind == "coop":
+            dg, _ = ops.lstm_bwd_coop(dy, whhT, gsave, csave, B, L, H, nd)
+        else:
+            dg = ops.lstm_bwd_mfma(dy, whhT, gsave, csave, B, L, H, nd)
         In = x.shape[1]
         BL = B * L
         ih, hh = o[f"lstm.weight_ih_l{l}"], o[f"lstm.weight_hh_l{l}"]

@@ -175,6 +175,60 @@ def lstm_bwd_mfma(dy, whhT_bf16, gsave, csave, B, L, H, ndir):
     return dg
 
 
+def lstm_coop_supported(H):
+    return bool(_lib.load().irc_lstm_coop_supported(H))
+
+
+def lstm_coop_pack(whh, H, ndir):
+    """W_hh fp32 [ndir*4H, H] -> (wf, wb) resident-slice layouts (bf16)."""
+    require_hip(whh)
+    wf = torch.empty((ndir * 4 * H * H,), dtype=BF16, device=whh.device)
+    wb = torch.empty_like(wf)
+    _lib.call("irc_lstm_coop_pack", ptr(whh), H, ndir, ptr(wf), ptr(wb), stream_ptr(whh.device))
+    return wf, wb
+
+
+def _coop_bytes(B, L, H, ndir, which):
+    return int(_lib.load().irc_lstm_coop_sizes(B, L, H, ndir, which))
+
+
+def lstm_fwd_coop(xp_packed, wf, B, L, H, ndir, save=True):
+    """Multi-CU forward recurrence -> (hout, gsave, csave, hprev, sync)."""
+    require_hip(xp_packed, wf)
+    dev = xp_packed.device
+    hout = torch.empty((B * L, ndir * H), dtype=BF16, device=dev)
+    gsave = csave = hprev = None
+    if save:
+        gsave = torch.empty((_coop_bytes(B, L, H, ndir, 0),), dtype=F32, device=dev)
+        csave = torch.empty((_coop_bytes(B, L, H, ndir, 1),), dtype=F32, device=dev)
+    xch = torch.empty((_coop_bytes(B, L, H, ndir, 2),), dtype=torch.uint8, device=dev)
+    sync = torch.empty((_coop_bytes(B, L, H, ndir, 4) // 4,), dtype=torch.int32, device=dev)
+    _lib.call("irc_lstm_fwd_coop", ptr(xp_packed), ptr(wf), ptr(hout), ptr(gsave), ptr(csave),
+              ptr(xch), ptr(sync), B, L, H, ndir, stream_ptr(dev))
+    if save:
+        hprev = torch.empty((ndir, B * L, H), dtype=BF16, device=dev)
+        _lib.call("irc_lstm_hprev", ptr(hout), ptr(hprev), B, L, H, ndir, stream_ptr(dev))
+    return hout, gsave, csave, hprev, sync
+
+
+def lstm_bwd_coop(dy, wb, gsave, csave, B, L, H, ndir):
+    """Multi-CU BPTT -> (dgates bf16 [B*L, ndir*4H], sync)."""
+    require_hip(dy, wb, gsave, csave)
+    dev = dy.device
+    dg = torch.empty((B * L, ndir * 4 * H), dtype=BF16, device=dev)
+    xch = torch.empty((_coop_bytes(B, L, H, ndir, 3),), dtype=torch.uint8, device=dev)
+    sync = torch.empty((_coop_bytes(B, L, H, ndir, 4) // 4,), dtype=torch.int32, device=dev)
+    _lib.call("irc_lstm_bwd_coop", ptr(dy), ptr(wb), ptr(gsave), ptr(csave), ptr(dg), ptr(xch),
+              ptr(sync), B, L, H, ndir, stream_ptr(dev))
+    return dg, sync
+
+
+def lstm_coop_timed_out(sync, B, ndir):
+    """Host check (synchronising) of a coop call's timeout word."""
+    n = ndir * ((B + 31) // 32) * 4
+    return int(sync[n].item()) != 0
+
+
 def mean_rows(x, B, L, C, ldx=None):
     require_hip(x)
     out = torch.empty((B, C), dtype=F32, device=x.device)

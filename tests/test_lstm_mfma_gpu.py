@@ -1,5 +1,6 @@
-"""MFMA BiLSTM recurrences (csrc/lstm_mfma.hip) at the production head width
-H = 256 vs the numpy oracle (oracle/irc_oracle.py lstm_head_fwd / seq2vec /
+"""MFMA BiLSTM recurrences at the production head width H = 256 -- the multi-CU
+cluster kernels (csrc/lstm_coop.hip, the default) and the single-CU kernels
+(csrc/lstm_mfma.hip) -- vs the numpy oracle (oracle/irc_oracle.py lstm_head_fwd / seq2vec /
 seq2vec_bwd, which restate nn.LSTM, src/model.py:16-41, and seq2vec,
 contrastive_module.py:102-112) and vs the VALU recurrences at the same precision.
 
@@ -35,6 +36,12 @@ def _rel(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
+@pytest.fixture(params=["coop", "mfma"])
+def rec(request, monkeypatch):
+    monkeypatch.setenv("IRC_LSTM_RECURRENCE", request.param)
+    return request.param
+
+
 @pytest.fixture
 def bf16_mode():
     from irc_amd.precision import get_precision, set_precision
@@ -45,13 +52,14 @@ def bf16_mode():
     set_precision(old)
 
 
-@pytest.mark.parametrize("B,L,In,layers", [(40, 9, 64, 2), (5, 1, 32, 1), (64, 16, 128, 1)])
-def test_mfma_forward_vs_oracle(gpu, bf16_mode, B, L, In, layers):
+@pytest.mark.parametrize("B,L,In,layers", [(40, 9, 64, 2), (5, 1, 32, 1), (64, 16, 128, 1),
+                                           (600, 3, 32, 1)])
+def test_mfma_forward_vs_oracle(gpu, bf16_mode, rec, B, L, In, layers):
     from irc_amd import ops
 
     assert ops.lstm_mfma_supported(H)
     h, p = _head(In, layers, 48, gpu)
-    assert h._use_mfma(torch.bfloat16)
+    assert h._recurrence(torch.bfloat16) == rec
     rng = np.random.default_rng(1)
     x = rng.standard_normal((B, L, In)).astype(np.float32)
     xd = torch.from_numpy(x).to(gpu)
@@ -63,8 +71,8 @@ def test_mfma_forward_vs_oracle(gpu, bf16_mode, B, L, In, layers):
     np.testing.assert_allclose(emb.cpu().numpy(), e_ref, atol=2e-2)
 
 
-@pytest.mark.parametrize("B,L,In,layers", [(40, 9, 64, 2), (33, 4, 96, 1)])
-def test_mfma_grads_vs_oracle(gpu, bf16_mode, B, L, In, layers):
+@pytest.mark.parametrize("B,L,In,layers", [(40, 9, 64, 2), (33, 4, 96, 1), (530, 2, 32, 1)])
+def test_mfma_grads_vs_oracle(gpu, bf16_mode, rec, B, L, In, layers):
     h, p = _head(In, layers, 32, gpu, seed=3)
     rng = np.random.default_rng(2)
     x = rng.standard_normal((B, L, In)).astype(np.float32)
@@ -79,7 +87,7 @@ def test_mfma_grads_vs_oracle(gpu, bf16_mode, B, L, In, layers):
         assert _rel(got, ref[name]) <= 4e-2, (name, _rel(got, ref[name]))
 
 
-def test_mfma_matches_valu_same_precision(gpu, bf16_mode, monkeypatch):
+def test_mfma_matches_valu_same_precision(gpu, bf16_mode, rec, monkeypatch):
     """Both recurrences see bf16 W and h; they differ only in accumulation order
     (and hence occasional 1-ulp bf16 roundings of h)."""
     h, _ = _head(64, 2, 32, gpu, seed=5)
@@ -94,7 +102,7 @@ def test_mfma_matches_valu_same_precision(gpu, bf16_mode, monkeypatch):
         return e.cpu().numpy(), h.flat_grad.cpu().numpy().copy()
 
     e_m, g_m = run()
-    monkeypatch.setattr(type(h), "_use_mfma", lambda self, dt: False)
+    monkeypatch.setenv("IRC_LSTM_RECURRENCE", "valu")
     e_v, g_v = run()
     np.testing.assert_allclose(e_m, e_v, atol=5e-3)
     assert _rel(g_m, g_v) <= 2e-2
@@ -108,3 +116,35 @@ def test_mfma_rejects_unsupported_width(gpu):
     with pytest.raises(_lib.IRCError):
         ops.lstm_pack(w[:8 * 128 * 16].view(8 * 128, 16), w[:1024], w[:1024],
                       w[:8 * 128 * 128 // 8].view(-1), 128, 2)
+
+
+@pytest.mark.parametrize("B,L", [(40, 7), (520, 5)])
+def test_coop_matches_single_cu_and_no_timeout(gpu, B, L):
+    """The cluster recurrence against the single-CU one on identical packed inputs
+    (bf16 h on both sides; they differ only in MFMA shape / summation order), and
+    the cluster timeout word stays clear (every member saw every hand-off)."""
+    from irc_amd import ops
+
+    torch.manual_seed(9)
+    nd = 2
+    whh = (torch.randn(nd * 4 * H, H) * 0.06).to(gpu)
+    wih = (torch.randn(nd * 4 * H, 64) * 0.1).to(gpu)
+    bih = torch.zeros(nd * 4 * H, device=gpu)
+    x = torch.randn(B * L, 64, device=gpu).to(torch.bfloat16)
+    wp, bp, w, wT = ops.lstm_pack(wih, bih, bih, whh, H, nd)
+    xp = ops.gemm(x, wp, bias=bp, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
+    wf, wb = ops.lstm_coop_pack(whh, H, nd)
+    h_c, g_c, c_c, hp_c, sync = ops.lstm_fwd_coop(xp, wf, B, L, H, nd, save=True)
+    h_m, g_m, c_m, hp_m = ops.lstm_fwd_mfma(xp, w, B, L, H, nd, save=True)
+    assert not ops.lstm_coop_timed_out(sync, B, nd)
+    assert (h_c.float() - h_m.float()).abs().max().item() <= 2e-2
+    assert (hp_c.float() - hp_m.float()).abs().max().item() <= 2e-2
+    dy = torch.randn(B * L, nd * H, device=gpu) * 0.1
+    dg_c, sync_b = ops.lstm_bwd_coop(dy, wb, g_c, c_c, B, L, H, nd)
+    dg_m = ops.lstm_bwd_mfma(dy, wT, g_m, c_m, B, L, H, nd)
+    assert not ops.lstm_coop_timed_out(sync_b, B, nd)
+    err = (dg_c.float() - dg_m.float()).norm() / dg_m.float().norm()
+    assert err.item() <= 2e-2
+    # bitwise reproducible (fixed member summation order)
+    dg_c2, _ = ops.lstm_bwd_coop(dy, wb, g_c, c_c, B, L, H, nd)
+    assert torch.equal(dg_c, dg_c2)
