@@ -19,14 +19,14 @@
 //   dh over all 256 units, publishes it (fp32), and sums the four partials of
 //   its own units in member order 0..3 (deterministic).
 //
-// Inter-workgroup hand-off (cdna_hip_programming.md Guideline 16, form R1 with
-// sc1 loads): payload stored write-through (relaxed agent-scope 8-byte atomic
-// stores = global_store sc1); every storing wave drains (s_waitcnt vmcnt(0));
-// workgroup barrier; ONE lane stores the member's flag (relaxed agent atomic);
-// ONE wave polls the flags relaxed (>= epoch) with bounded spins; barrier; every
-// load of the payload is a relaxed agent-scope atomic load (global_load sc1).
-// Exchange buffers are double-buffered by step parity (a member can be at most
-// one step ahead of any other).  Flags are zeroed by hipMemsetAsync every call.
+// Inter-workgroup hand-off (cdna_hip_programming.md Guideline 16, form R2: the
+// data IS the flag): every 32-bit payload word travels in an 8-byte granule
+// {tag = epoch, value} stored write-through (relaxed agent-scope atomic store =
+// global_store_dwordx2 sc1) and read with relaxed agent-scope atomic loads
+// (global_load_dwordx2 sc1); a consumer wave re-reads its granules until every
+// tag equals the step's epoch (bounded spins).  No flag, drain or fence.  Buffers
+// are double-buffered by step parity (a member can be at most one step ahead of
+// any other) and zeroed by hipMemsetAsync every call (tag 0 is never an epoch).
 // Co-residency: <= 16 groups per launch (<= 128 workgroups per direction pair,
 // one per CU by LDS), so two concurrent launches (query and key encoders) fit
 // the 256 CUs; spins are bounded and set a timeout word instead of hanging.
@@ -63,38 +63,33 @@ __device__ __forceinline__ unsigned long long ld_sc1(const void* p) {
   return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Publish: every storing wave drains, barrier, one lane raises the member's flag.
-__device__ __forceinline__ void publish(unsigned* flag, unsigned epoch) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ unsigned long long granule(unsigned epoch, unsigned v) {
+  return ((unsigned long long)epoch << 32) | v;
 }
 
-// Wave 0 polls the P member flags until all >= epoch; returns false (all threads)
-// on timeout.  Ends with a barrier: the payload loads follow it.
-__device__ __forceinline__ bool wait_members(unsigned* flags, unsigned epoch, unsigned* tmo,
-                                             int* abort_lds) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    unsigned spins = 0;
-    for (;;) {
-      const unsigned v = lane < P ? __hip_atomic_load((gu32*)(flags + lane), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                  : 0xffffffffu;
-      if (__all(v >= epoch)) break;
-      if (++spins > SPIN_MAX) {
-        if (lane == 0) {
-          __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          *abort_lds = 1;
-        }
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+// One wave sweeps its N granules (addresses from addr(k)) until every tag ==
+// epoch; values out.  Wave-uniform loop; on timeout sets tmo + the LDS abort word.
+template <int N, typename F>
+__device__ __forceinline__ void sweep(F addr, unsigned epoch, unsigned (&v)[N], unsigned* tmo,
+                                      int* abort_lds) {
+  for (unsigned spins = 0;;) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const unsigned long long x = ld_sc1(addr(k));
+      v[k] = (unsigned)x;
+      ok &= (unsigned)(x >> 32) == epoch;
     }
+    if (__all(ok)) return;
+    if (++spins > SPIN_MAX) {
+      if ((threadIdx.x & 63) == 0) {
+        __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *abort_lds = 1;
+      }
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
-  __syncthreads();
-  return *abort_lds == 0;
 }
 
 // Cluster decode: blocks b, b+8, b+16, b+24 of each 32-block chunk are the 4
@@ -158,8 +153,10 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
   };
   f32x4 xr[2][4];
   load_xp(dir == 0 ? 0 : L - 1, xr);
-  unsigned short* X = xch + (int64_t)(dir * ngrp_total + grp) * 2 * BG * H;
-  unsigned* fl = flags + (dir * ngrp_total + grp) * P;
+  // granules [2 parity][BG][H/2]: {epoch, two bf16 of units 2c, 2c+1}
+  unsigned long long* X =
+      reinterpret_cast<unsigned long long*>(xch) + (int64_t)(dir * ngrp_total + grp) * 2 * BG * (H / 2);
+  (void)flags;
   __syncthreads();
 
   for (int s = 0; s < L; ++s) {
@@ -190,11 +187,9 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
       }
     }
     __syncthreads();  // every read of h_{t-1} done
-    float* gs = gsave ? gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP : nullptr;
-    float* cs = csave ? csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP : nullptr;
+    f32x4 gv[2][4], cv[2];
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb) {
-      f32x4 cv;
+    for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float ig = sigm(acc[rb][0][i]);
@@ -204,20 +199,49 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         const float cn = fg * c[rb][i] + ig * g2;
         c[rb][i] = cn;
         hb[rb * 16 + 4 * q4 + i][u] = f32_to_bf16(og * tanh_f(cn));
-        if (gs) {
-          const f32x4 gv = {ig, fg, g2, og};
-          *reinterpret_cast<f32x4*>(gs + ((((m * NW + w) * 2 + rb) * 4 + i) * 64 + lane) * 4) = gv;
-        }
-        cv[i] = cn;
+        gv[rb][i] = f32x4{ig, fg, g2, og};
+        cv[rb][i] = cn;
       }
-      if (cs) *reinterpret_cast<f32x4*>(cs + (((m * NW + w) * 2 + rb) * 64 + lane) * 4) = cv;
-    }
     __syncthreads();  // own slice of h_t complete in LDS
-    if (s + 1 < L) {  // publish the own slice (write-through) for the other members
-      unsigned short* Xp = X + (s & 1) * BG * H;
-      for (int p = threadIdx.x; p < BG * UPW / 4; p += NTH) {
-        const int row = p / (UPW / 4), col = m * UPW + (p % (UPW / 4)) * 4;
-        st_sc1(Xp + row * H + col, *reinterpret_cast<const unsigned long long*>(&hb[row][col]));
+    if (s + 1 < L) {
+      // publish the own 32 x 64 slice as 1024 granules (4 per thread) ...
+      const unsigned ep = (unsigned)(s + 1);
+      unsigned long long* Xp = X + (s & 1) * BG * (H / 2);
+#pragma unroll
+      for (int k = 0; k < BG * UPW / 2 / NTH; ++k) {
+        const int p = k * NTH + threadIdx.x;
+        const int row = p / (UPW / 2), c2 = m * (UPW / 2) + p % (UPW / 2);
+        st_sc1(Xp + row * (H / 2) + c2,
+               granule(ep, *reinterpret_cast<const unsigned*>(&hb[row][2 * c2])));
+      }
+      // ... and gather the other three (12 granules per thread)
+      constexpr int NG = 3 * BG * UPW / 2 / NTH;
+      unsigned v[NG];
+      auto addr = [&](int k) {
+        const int idx = k * NTH + threadIdx.x;
+        const int mm = (m + 1 + idx / (BG * UPW / 2)) & 3, loc = idx % (BG * UPW / 2);
+        return Xp + (loc / (UPW / 2)) * (H / 2) + mm * (UPW / 2) + loc % (UPW / 2);
+      };
+      sweep<NG>(addr, ep, v, tmo, &abort_lds);
+#pragma unroll
+      for (int k = 0; k < NG; ++k) {
+        const int idx = k * NTH + threadIdx.x;
+        const int mm = (m + 1 + idx / (BG * UPW / 2)) & 3, loc = idx % (BG * UPW / 2);
+        *reinterpret_cast<unsigned*>(&hb[loc / (UPW / 2)][2 * (mm * (UPW / 2) + loc % (UPW / 2))]) =
+            v[k];
+      }
+    }
+    // saves + h_t rows (own slice) after the hand-off: they drain under the next MFMAs
+    if (gsave) {
+      float* gs = gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP;
+      float* cs = csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP;
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<f32x4*>(gs + ((((m * NW + w) * 2 + rb) * 4 + i) * 64 + lane) * 4) =
+              gv[rb][i];
+        *reinterpret_cast<f32x4*>(cs + (((m * NW + w) * 2 + rb) * 64 + lane) * 4) = cv[rb];
       }
     }
     for (int p = threadIdx.x; p < BG * UPW / 8; p += NTH) {  // h_t -> hout (own slice)
@@ -226,17 +250,8 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         *reinterpret_cast<u16x8*>(hout + ((int64_t)(b0 + row) * L + t) * hld + dir * H + col) =
             *reinterpret_cast<const u16x8*>(&hb[row][col]);
     }
-    if (s + 1 < L) {
-      publish(fl + m, (unsigned)(s + 1));
-      if (!wait_members(fl, (unsigned)(s + 1), tmo, &abort_lds)) return;
-      const unsigned short* Xp = X + (s & 1) * BG * H;
-      for (int p = threadIdx.x; p < BG * H / 4; p += NTH) {
-        const int row = p / (H / 4), col = (p % (H / 4)) * 4;
-        if (col / UPW == m) continue;
-        *reinterpret_cast<unsigned long long*>(&hb[row][col]) = ld_sc1(Xp + row * H + col);
-      }
-      __syncthreads();  // h_t complete for the next step
-    }
+    __syncthreads();  // h_t complete for the next step (and the abort word)
+    if (abort_lds) return;
   }
 }
 
@@ -280,8 +295,10 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) dc[rb][i] = 0.f;
-  float* X = xch + (int64_t)(dir * ngrp_total + grp) * 2 * P * PART;
-  unsigned* fl = flags + (dir * ngrp_total + grp) * P;
+  // granules [2 parity][P member][PART]: {epoch, fp32 partial}
+  unsigned long long* X = reinterpret_cast<unsigned long long*>(xch) +
+                          (int64_t)(dir * ngrp_total + grp) * 2 * P * PART;
+  (void)flags;
   __syncthreads();
 
   for (int s = 0; s < L; ++s) {
@@ -312,38 +329,35 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
             acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw, acc[rb][cb], 0, 0, 0);
         }
       }
-      // publish the partial: block (wave w = unit block 64w, cb, rb) in the lane order
-      // the consumer member (w) reads it back
-      float* Xp = X + (int64_t)((s & 1) * P + m) * PART;
+      // publish the partial as granules: block (wave w = unit block 64w, cb, rb) in
+      // the lane order the consumer member (w) reads back
+      const unsigned ep = (unsigned)s;
+      unsigned long long* Xs = X + (int64_t)(s & 1) * P * PART;
+      unsigned long long* Xp = Xs + (int64_t)m * PART;
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          float* dst = Xp + (((w * 4 + cb) * 2 + rb) * 64 + lane) * 4;
-          const f32x4 v = acc[rb][cb];
-          st_sc1(dst, __builtin_bit_cast(unsigned long long, (float __attribute__((ext_vector_type(2)))){v[0], v[1]}));
-          st_sc1(dst + 2, __builtin_bit_cast(unsigned long long, (float __attribute__((ext_vector_type(2)))){v[2], v[3]}));
-        }
-      publish(fl + m, (unsigned)s);
-      if (!wait_members(fl, (unsigned)s, tmo, &abort_lds)) return;
-      // own units live in every member's block m, cb = w: sum in member order
+        for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-      for (int mm = 0; mm < P; ++mm) {
-        const float* src = X + (int64_t)((s & 1) * P + mm) * PART;
+          for (int i = 0; i < 4; ++i)
+            st_sc1(Xp + ((((w * 4 + cb) * 2 + rb) * 4 + i) * 64 + lane),
+                   granule(ep, __float_as_uint(acc[rb][cb][i])));
+      // own units live in every member's block m, cb = w: gather, sum in member order
+      unsigned v[P * 8];
+      auto addr = [&](int k) {
+        const int mm = k >> 3, rb = (k >> 2) & 1, i = k & 3;
+        return Xs + (int64_t)mm * PART + ((((m * 4 + w) * 2 + rb) * 4 + i) * 64 + lane);
+      };
+      sweep<P * 8>(addr, ep, v, tmo, &abort_lds);
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          const float* p = src + (((m * 4 + w) * 2 + rb) * 64 + lane) * 4;
-          const unsigned long long lo = ld_sc1(p), hi = ld_sc1(p + 2);
-          const auto a2 = __builtin_bit_cast(float __attribute__((ext_vector_type(2))), lo);
-          const auto b2 = __builtin_bit_cast(float __attribute__((ext_vector_type(2))), hi);
-          dh[rb][0] += a2[0];
-          dh[rb][1] += a2[1];
-          dh[rb][2] += b2[0];
-          dh[rb][3] += b2[1];
-        }
-      }
+      for (int mm = 0; mm < P; ++mm)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dh[rb][i] += __uint_as_float(v[mm * 8 + rb * 4 + i]);
     }
     __syncthreads();  // all reads of dgl (MFMA) done before it is overwritten
+    if (abort_lds) return;
     const float* gs = gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP;
     const float* cs = csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP;
     const float* csp =
@@ -425,8 +439,8 @@ extern "C" int64_t irc_lstm_coop_sizes(int64_t B, int64_t L, int64_t H, int64_t 
   switch (which) {
     case 0: return ndir * ngrp * L * lstmc::GSTEP;
     case 1: return ndir * ngrp * L * lstmc::CSTEP;
-    case 2: return ndir * ngrp * 2 * lstmc::BG * H * 2;
-    case 3: return ndir * ngrp * 2 * lstmc::P * lstmc::PART * 4;
+    case 2: return ndir * ngrp * 2 * lstmc::BG * (H / 2) * 8;   // granules
+    case 3: return ndir * ngrp * 2 * lstmc::P * lstmc::PART * 8;  // granules
     case 4: return ((ndir * ngrp * lstmc::P + 1) * 4 + 15) / 16 * 16;
   }
   return -1;
@@ -453,6 +467,7 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::P;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
+  hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 2), st);
   prof_begin(st);
   for (int g0 = 0; g0 < ngrp; g0 += lstmc::MAX_GROUPS) {
     const int n = ngrp - g0 < lstmc::MAX_GROUPS ? ngrp - g0 : lstmc::MAX_GROUPS;
@@ -475,6 +490,7 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::P;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
+  hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 3), st);
   prof_begin(st);
   for (int g0 = 0; g0 < ngrp; g0 += lstmc::MAX_GROUPS) {
     const int n = ngrp - g0 < lstmc::MAX_GROUPS ? ngrp - g0 : lstmc::MAX_GROUPS;
