@@ -196,6 +196,8 @@ int irc_momentum_update(float* pk, const float* pq, int64_t n, float mom, irc_st
 int irc_enqueue(float* queue, const float* keys, int64_t* ptr, int64_t D, int64_t K, int64_t B,
                 irc_stream_t stream);
 int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t stream);
+/* y bf16 [C][R] = transpose of x fp32 [R][C] (weights as the NK GEMM operand). */
+int irc_cast_bf16_t(const float* x, void* y, int64_t R, int64_t C, irc_stream_t stream);
 int irc_axpby(float* out, const float* x, const float* y, float a, float b, int64_t n,
               irc_stream_t stream);
 /* column sums of x [R][C] (dtype 0 bf16, 1 fp32) into fp32 out; partial holds

@@ -257,6 +257,45 @@ __global__ void colsum_partial_kernel(const T* __restrict__ x, float* __restrict
   partial[(int64_t)blockIdx.y * C + c] = s;
 }
 
+// bf16 rows, C % 8 == 0: each thread sums 8 adjacent columns over the chunk with
+// 16-byte loads (a wave covers 512 contiguous columns = 1 KB per row).
+__global__ void colsum_partial_vec_kernel(const unsigned short* __restrict__ x,
+                                          float* __restrict__ partial, int64_t R, int C,
+                                          int64_t ldx) {
+  const int c8 = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (c8 >= C) return;
+  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS;
+  int64_t r1 = r0 + COLSUM_ROWS;
+  if (r1 > R) r1 = R;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t r = r0; r < r1; ++r) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(x + r * ldx + c8);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) s[t] += bf16_to_f32(v[t]);
+  }
+  float* p = partial + (int64_t)blockIdx.y * C + c8;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) p[t] = s[t];
+}
+
+// W [R][C] fp32 -> W^T [C][R] bf16 through 32x33 LDS tiles (the nn.Linear-layout
+// operand of GEMMs that consume W as [K][N]).
+__global__ void cast_bf16_t_kernel(const float* __restrict__ x, unsigned short* __restrict__ y,
+                                   int R, int C) {
+  __shared__ float tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? x[(int64_t)r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) y[(int64_t)c * R + r] = f32_to_bf16(tile[tx][i]);
+  }
+}
+
 __global__ void colsum_final_kernel(const float* __restrict__ partial, float* __restrict__ out,
                                     int nchunks, int C, int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -389,6 +428,14 @@ extern "C" int irc_enqueue(float* queue, const float* keys, int64_t* ptr, int64_
   return check_launch("enqueue");
 }
 
+extern "C" int irc_cast_bf16_t(const float* x, void* y, int64_t R, int64_t C,
+                               irc_stream_t stream) {
+  if (R == 0 || C == 0) return IRC_OK;
+  hipLaunchKernelGGL(cast_bf16_t_kernel, dim3((unsigned)((C + 31) / 32), (unsigned)((R + 31) / 32)),
+                     dim3(256), 0, as_stream(stream), x, (unsigned short*)y, (int)R, (int)C);
+  return check_launch("cast_bf16_t");
+}
+
 extern "C" int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t stream) {
   if (n == 0) return IRC_OK;
   hipLaunchKernelGGL(cast_bf16_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), x,
@@ -402,7 +449,10 @@ extern "C" int irc_colsum(int dtype, const void* x, float* out, int64_t R, int64
   if (C == 0) return IRC_OK;
   const int64_t nch = (R + COLSUM_ROWS - 1) / COLSUM_ROWS;
   hipStream_t st = as_stream(stream);
-  if (nch > 0 && dtype == 0)
+  if (nch > 0 && dtype == 0 && C % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0)
+    hipLaunchKernelGGL(colsum_partial_vec_kernel, dim3(nblk(C / 8, 64), (unsigned)nch), dim3(64),
+                       0, st, (const unsigned short*)x, partial, R, (int)C, ldx);
+  else if (nch > 0 && dtype == 0)
     hipLaunchKernelGGL(colsum_partial_kernel<unsigned short>, dim3(nblk(C, 64), (unsigned)nch),
                        dim3(64), 0, st, (const unsigned short*)x, partial, R, (int)C, ldx);
   else if (nch > 0)

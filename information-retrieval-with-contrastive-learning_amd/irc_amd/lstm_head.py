@@ -212,7 +212,9 @@ class LSTMHead(nn.Module):
                 wT = wb
             else:
                 hout, gsave, csave, hprev = ops.lstm_fwd_mfma(xp, w, B, L, H, nd, save=save)
-            wih_c = ops.cast_bf16(wih) if (save and l > 0) else None  # dx GEMM operand
+            # dx GEMM operand, transposed to [In, ndir*4H] so dx = dg . W_ih is an
+            # A[M][K] . B[N][K] GEMM (the big-tile path)
+            wih_c = ops.cast_bf16_t(wih) if (save and l > 0) else None
             return hout, ((kind, x, wih_c, wT, gsave, csave, hprev) if save else None)
         wih, whh, bias = self._layer_weights(l, dt)
         xp = ops.gemm(x, wih, bias=bias, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
@@ -303,7 +305,7 @@ class LSTMHead(nn.Module):
         # dx is the critical path (next layer's recurrence); the weight/bias
         # gradients go to a side stream and overlap that recurrence, which only
         # occupies B/32 * ndir CUs.  Joined in backward_compute.
-        dx = ops.gemm(dg, wih_c, b_is_nk=False, out_dtype=torch.float32) if l > 0 else None
+        dx = ops.gemm(dg, wih_c, out_dtype=torch.float32) if l > 0 else None
         cur = torch.cuda.current_stream(dg.device)
         side = side_stream(dg.device, "lstm_wgrad")
         side.wait_stream(cur)
@@ -314,8 +316,9 @@ class LSTMHead(nn.Module):
             ops.gemm_strided(dg, hprev, g[hh:], M=4 * H, N=H, K=BL, batch=nd, lda=nd * 4 * H,
                              sA=4 * H, ldb=H, sB=BL * H, ldc=H, sC=4 * H * H, trans_a=True,
                              b_is_nk=False, accumulate=True)
-            ops.colsum(dg, out=g[bi:bi + nd * 4 * H], accumulate=True)
-            ops.colsum(dg, out=g[bh:bh + nd * 4 * H], accumulate=True)
+            db = ops.colsum(dg)  # d(b_ih) = d(b_hh): one column sum, added to both
+            ops.axpby(g[bi:bi + nd * 4 * H], db, out=g[bi:bi + nd * 4 * H])
+            ops.axpby(g[bh:bh + nd * 4 * H], db, out=g[bh:bh + nd * 4 * H])
         for t in (dg, x, hprev):  # allocated on cur, read on side
             t.record_stream(side)
         self._wgrad_pending = side

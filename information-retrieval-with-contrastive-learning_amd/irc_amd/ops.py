@@ -335,6 +335,15 @@ def cast_bf16(x):
     return y
 
 
+def cast_bf16_t(x):
+    """x fp32 [R, C] -> bf16 [C, R] (transposed copy)."""
+    require_hip(x)
+    R, C = x.shape
+    y = torch.empty((C, R), dtype=BF16, device=x.device)
+    _lib.call("irc_cast_bf16_t", ptr(x), ptr(y), R, C, stream_ptr(x.device))
+    return y
+
+
 def colsum(x, out=None, accumulate=False):
     require_hip(x)
     R, C = x.shape
