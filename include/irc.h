@@ -201,7 +201,7 @@ int irc_cast_bf16_t(const float* x, void* y, int64_t R, int64_t C, irc_stream_t 
 int irc_axpby(float* out, const float* x, const float* y, float a, float b, int64_t n,
               irc_stream_t stream);
 /* column sums of x [R][C] (dtype 0 bf16, 1 fp32) into fp32 out; partial holds
- * ceil(R/256)*C floats of scratch (deterministic two-pass order). */
+ * ceil(R/64)*C floats of scratch (deterministic two-pass order). */
 int irc_colsum(int dtype, const void* x, float* out, int64_t R, int64_t C, int64_t ldx,
                int accumulate, float* partial, irc_stream_t stream);
 

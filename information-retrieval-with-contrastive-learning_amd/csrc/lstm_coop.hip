@@ -103,6 +103,30 @@ __device__ __forceinline__ void sweep(F addr, unsigned epoch, unsigned (&v)[N], 
   }
 }
 
+// Wave 0 polls one sentinel granule per producer (lanes 0..P-1; cheap, while the
+// producers may still be computing) until every tag == epoch, then a barrier; the
+// full sweep that follows then normally needs a single pass.
+__device__ __forceinline__ void poll_sentinels(const unsigned long long* const* sent,
+                                               unsigned epoch, unsigned* tmo, int* abort_lds) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    for (unsigned spins = 0;;) {
+      bool ok = true;
+      if (lane < P) ok = (unsigned)(ld_sc1(sent[lane]) >> 32) == epoch;
+      if (__all(ok)) break;
+      if (++spins > SPIN_MAX) {
+        if (lane == 0) {
+          __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *abort_lds = 1;
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
 // Cluster decode: blocks b, b+8, b+16, b+24 of each 32-block chunk are the 4
 // members of group (chunk*8 + b%8) -- same XCD (speed only, never correctness).
 struct Member {
@@ -226,6 +250,12 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         st_sc1_pair(Xp + row * (H / 2) + c2, granule(ep, hv.x), granule(ep, hv.y));
       }
       // ... and gather the other three (12 granules per thread)
+      {  // sentinel: each producer's first granule (own slot: already ours)
+        const unsigned long long* sent[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) sent[q] = Xp + q * (UPW / 2);
+        poll_sentinels(sent, ep, tmo, &abort_lds);
+      }
       constexpr int NG = 3 * BG * UPW / 2 / NTH;
       unsigned v[NG];
       auto addr = [&](int k) {
@@ -348,18 +378,22 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          unsigned long long* d = Xp + ((((w * 4 + cb) * 2 + rb) * 64 + lane) * 4);
-          st_sc1_pair(d, granule(ep, __float_as_uint(acc[rb][cb][0])),
-                      granule(ep, __float_as_uint(acc[rb][cb][1])));
-          st_sc1_pair(d + 2, granule(ep, __float_as_uint(acc[rb][cb][2])),
-                      granule(ep, __float_as_uint(acc[rb][cb][3])));
-        }
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            st_sc1(Xp + ((((w * 4 + cb) * 2 + rb) * 4 + i) * 64 + lane),
+                   granule(ep, __float_as_uint(acc[rb][cb][i])));
+      {  // sentinel: the first granule of this member's block in every producer
+        const unsigned long long* sent[P];
+#pragma unroll
+        for (int q = 0; q < P; ++q) sent[q] = Xs + (int64_t)q * PART + (m * 4) * 2 * 4 * 64;
+        poll_sentinels(sent, ep, tmo, &abort_lds);
+      }
       // own units live in every member's block m, cb = w: gather, sum in member order
       unsigned v[P * 8];
       auto addr = [&](int k) {
         const int mm = k >> 3, rb = (k >> 2) & 1, i = k & 3;
-        return Xs + (int64_t)mm * PART + ((((m * 4 + w) * 2 + rb) * 64 + lane) * 4 + i);
+        return Xs + (int64_t)mm * PART + ((((m * 4 + w) * 2 + rb) * 4 + i) * 64 + lane);
       };
       sweep<P * 8>(addr, ep, v, tmo, &abort_lds);
 #pragma unroll

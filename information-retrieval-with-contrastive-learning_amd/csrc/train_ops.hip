@@ -243,7 +243,7 @@ __global__ void cast_bf16_kernel(const float* __restrict__ x, unsigned short* __
 
 // Column sums in two deterministic passes: partial[chunk][c] over a fixed row
 // chunk (grid.y), then out[c] (+)= sum over chunks in order.
-constexpr int COLSUM_ROWS = 256;
+constexpr int COLSUM_ROWS = 64;
 template <typename T>
 __global__ void colsum_partial_kernel(const T* __restrict__ x, float* __restrict__ partial,
                                       int64_t R, int C, int64_t ldx) {
@@ -268,7 +268,17 @@ __global__ void colsum_partial_vec_kernel(const unsigned short* __restrict__ x,
   int64_t r1 = r0 + COLSUM_ROWS;
   if (r1 > R) r1 = R;
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int64_t r = r0; r < r1; ++r) {
+  int64_t r = r0;
+  for (; r + 8 <= r1; r += 8) {  // 8 independent 16-byte loads in flight
+    u16x8 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const u16x8*>(x + (r + q) * ldx + c8);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) s[t] += bf16_to_f32(v[q][t]);
+  }
+  for (; r < r1; ++r) {
     const u16x8 v = *reinterpret_cast<const u16x8*>(x + r * ldx + c8);
 #pragma unroll
     for (int t = 0; t < 8; ++t) s[t] += bf16_to_f32(v[t]);

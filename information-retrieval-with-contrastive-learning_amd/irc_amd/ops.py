@@ -349,7 +349,7 @@ def colsum(x, out=None, accumulate=False):
     R, C = x.shape
     if out is None:
         out = torch.empty((C,), dtype=F32, device=x.device)
-    partial = torch.empty((max(1, (R + 255) // 256) * C,), dtype=F32, device=x.device)
+    partial = torch.empty((max(1, (R + 63) // 64) * C,), dtype=F32, device=x.device)
     _lib.call("irc_colsum", _code(x), ptr(x), ptr(out), R, C, x.stride(0), 1 if accumulate else 0,
               ptr(partial), stream_ptr(x.device))
     return out
