@@ -103,6 +103,53 @@ __device__ __forceinline__ void sweep(F addr, unsigned epoch, unsigned (&v)[N], 
   }
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte write-through store / load (global_*_dwordx4 sc1) for the flag-based
+// hand-off (form R1).  The asm store is drained by the explicit vmcnt(0) before
+// the flag; the asm loads are completed by wait_loaded(), which takes the
+// loaded registers as in/out operands so no use can be scheduled before it.
+__device__ __forceinline__ void st_sc1_x4(void* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ u32x4 ld_sc1_x4(const void* p) {
+  u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// R1 publish: every storing wave drains its stores, barrier, one lane sets the flag.
+__device__ __forceinline__ void publish_flag(unsigned* flag, unsigned epoch) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// R1 consume: wave 0 polls the P flags (relaxed, >= epoch), then a barrier.
+__device__ __forceinline__ void poll_flags(unsigned* flags, unsigned epoch, unsigned* tmo,
+                                           int* abort_lds) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    for (unsigned spins = 0;;) {
+      bool ok = true;
+      if (lane < P)
+        ok = __hip_atomic_load((gu32*)(flags + lane), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+      if (__all(ok)) break;
+      if (++spins > SPIN_MAX) {
+        if (lane == 0) {
+          __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *abort_lds = 1;
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
 // Wave 0 polls one sentinel granule per producer (lanes 0..P-1; cheap, while the
 // producers may still be computing) until every tag == epoch, then a barrier; the
 // full sweep that follows then normally needs a single pass.
@@ -336,10 +383,9 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) dc[rb][i] = 0.f;
-  // granules [2 parity][P member][PART]: {epoch, fp32 partial}
-  unsigned long long* X = reinterpret_cast<unsigned long long*>(xch) +
-                          (int64_t)(dir * ngrp_total + grp) * 2 * P * PART;
-  (void)flags;
+  // partials [2 parity][P member][block = (w*4 + cb)*2 + rb][64 lanes][4] fp32
+  float* X = reinterpret_cast<float*>(xch) + (int64_t)(dir * ngrp_total + grp) * 2 * P * PART;
+  unsigned* fl = flags + (dir * ngrp_total + grp) * P;
   __syncthreads();
 
   for (int s = 0; s < L; ++s) {
@@ -370,38 +416,38 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
             acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw, acc[rb][cb], 0, 0, 0);
         }
       }
-      // publish the partial as granules: block (wave w = unit block 64w, cb, rb) in
-      // the lane order the consumer member (w) reads back
+      // publish the partial (R1): block (wave w = unit block 64w, cb, rb), each
+      // lane's 4 rows as one 16-byte write-through store
       const unsigned ep = (unsigned)s;
-      unsigned long long* Xs = X + (int64_t)(s & 1) * P * PART;
-      unsigned long long* Xp = Xs + (int64_t)m * PART;
+      float* Xs = X + (int64_t)(s & 1) * P * PART;
+      float* Xp = Xs + (int64_t)m * PART;
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
+          st_sc1_x4(Xp + ((((w * 4 + cb) * 2 + rb) * 64 + lane) * 4),
+                    __builtin_bit_cast(u32x4, acc[rb][cb]));
+      publish_flag(fl + m, ep);
+      poll_flags(fl, ep, tmo, &abort_lds);
+      if (abort_lds) return;
+      // own units live in every member's block m, cb = w: sum in member order
+      u32x4 v[P][2];
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            st_sc1(Xp + ((((w * 4 + cb) * 2 + rb) * 4 + i) * 64 + lane),
-                   granule(ep, __float_as_uint(acc[rb][cb][i])));
-      {  // sentinel: the first granule of this member's block in every producer
-        const unsigned long long* sent[P];
+      for (int mm = 0; mm < P; ++mm)
 #pragma unroll
-        for (int q = 0; q < P; ++q) sent[q] = Xs + (int64_t)q * PART + (m * 4) * 2 * 4 * 64;
-        poll_sentinels(sent, ep, tmo, &abort_lds);
-      }
-      // own units live in every member's block m, cb = w: gather, sum in member order
-      unsigned v[P * 8];
-      auto addr = [&](int k) {
-        const int mm = k >> 3, rb = (k >> 2) & 1, i = k & 3;
-        return Xs + (int64_t)mm * PART + ((((m * 4 + w) * 2 + rb) * 4 + i) * 64 + lane);
-      };
-      sweep<P * 8>(addr, ep, v, tmo, &abort_lds);
+        for (int rb = 0; rb < 2; ++rb)
+          v[mm][rb] = ld_sc1_x4(Xs + (int64_t)mm * PART + ((((m * 4 + w) * 2 + rb) * 64 + lane) * 4));
+      asm volatile("s_waitcnt vmcnt(0)"
+                   : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[1][0]), "+v"(v[1][1]), "+v"(v[2][0]),
+                     "+v"(v[2][1]), "+v"(v[3][0]), "+v"(v[3][1])
+                   :
+                   : "memory");
 #pragma unroll
       for (int mm = 0; mm < P; ++mm)
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) dh[rb][i] += __uint_as_float(v[mm * 8 + rb * 4 + i]);
+          for (int i = 0; i < 4; ++i) dh[rb][i] += __uint_as_float(v[mm][rb][i]);
     }
     __syncthreads();  // all reads of dgl (MFMA) done before it is overwritten
     if (abort_lds) return;
@@ -487,7 +533,7 @@ extern "C" int64_t irc_lstm_coop_sizes(int64_t B, int64_t L, int64_t H, int64_t 
     case 0: return ndir * ngrp * L * lstmc::GSTEP;
     case 1: return ndir * ngrp * L * lstmc::CSTEP;
     case 2: return ndir * ngrp * 2 * lstmc::BG * (H / 2) * 8;   // granules
-    case 3: return ndir * ngrp * 2 * lstmc::P * lstmc::PART * 8;  // granules
+    case 3: return ndir * ngrp * 2 * lstmc::P * lstmc::PART * 4;  // fp32 partials
     case 4: return ((ndir * ngrp * lstmc::P + 1) * 4 + 15) / 16 * 16;
   }
   return -1;
@@ -537,7 +583,6 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::P;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
-  hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 3), st);
   prof_begin(st);
   for (int g0 = 0; g0 < ngrp; g0 += lstmc::MAX_GROUPS) {
     const int n = ngrp - g0 < lstmc::MAX_GROUPS ? ngrp - g0 : lstmc::MAX_GROUPS;

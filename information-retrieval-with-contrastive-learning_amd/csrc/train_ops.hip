@@ -306,13 +306,34 @@ __global__ void cast_bf16_t_kernel(const float* __restrict__ x, unsigned short* 
   }
 }
 
+// 64 columns x 4 chunk segments per block: each thread sums its segment in chunk
+// order (8 loads in flight), then the 4 segment sums are added in segment order
+// -- a fixed order, so the result is bitwise reproducible.
 __global__ void colsum_final_kernel(const float* __restrict__ partial, float* __restrict__ out,
                                     int nchunks, int C, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float seg[4][64];
+  const int cl = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int per = (nchunks + 3) / 4;
+  const int k0 = sg * per, k1 = min(nchunks, k0 + per);
   float s = 0.f;
-  for (int k = 0; k < nchunks; ++k) s += partial[(int64_t)k * C + c];
-  out[c] = accumulate ? out[c] + s : s;
+  if (c < C) {
+    int k = k0;
+    for (; k + 8 <= k1; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = partial[(int64_t)(k + q) * C + c];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += v[q];
+    }
+    for (; k < k1; ++k) s += partial[(int64_t)k * C + c];
+  }
+  seg[sg][cl] = s;
+  __syncthreads();
+  if (sg == 0 && c < C) {
+    const float t = ((seg[0][cl] + seg[1][cl]) + seg[2][cl]) + seg[3][cl];
+    out[c] = accumulate ? out[c] + t : t;
+  }
 }
 
 }  // namespace tops
@@ -468,8 +489,8 @@ extern "C" int irc_colsum(int dtype, const void* x, float* out, int64_t R, int64
   else if (nch > 0)
     hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3(nblk(C, 64), (unsigned)nch), dim3(64), 0,
                        st, (const float*)x, partial, R, (int)C, ldx);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(nblk(C)), dim3(256), 0, st, partial, out, (int)nch,
-                     (int)C, accumulate);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(nblk(C, 64)), dim3(256), 0, st, partial, out,
+                     (int)nch, (int)C, accumulate);
   return check_launch("colsum");
 }
 
