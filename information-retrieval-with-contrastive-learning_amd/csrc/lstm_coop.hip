@@ -392,6 +392,29 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     const int t = dir == 0 ? L - 1 - s : s;   // reverse of the forward order
     const int tp = dir == 0 ? t - 1 : t + 1;  // previous forward step
     const bool has_prev = tp >= 0 && tp < L;
+    // this step's saved gates / c / c_prev / dy: issued now, consumed after the
+    // MFMAs and the exchange (their latency hides behind both)
+    f32x4 pgv[2][4], pcv[2], pcp[2];
+    float pdy[2][4];
+    {
+      const float* gs = gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP;
+      const float* cs = csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP;
+      const float* csp =
+          has_prev ? csave + ((int64_t)(dir * ngrp_total + grp) * L + tp) * CSTEP : nullptr;
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int64_t co = (((m * NW + w) * 2 + rb) * 64 + lane) * 4;
+        pcv[rb] = *reinterpret_cast<const f32x4*>(cs + co);
+        pcp[rb] = csp ? *reinterpret_cast<const f32x4*>(csp + co) : (f32x4)0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pgv[rb][i] = *reinterpret_cast<const f32x4*>(
+              gs + ((((m * NW + w) * 2 + rb) * 4 + i) * 64 + lane) * 4);
+          const int b = b0 + rb * 16 + 4 * q4 + i;
+          pdy[rb][i] = b < B ? dy[((int64_t)b * L + t) * hld + dir * H + u] : 0.f;
+        }
+      }
+    }
     // dh from dgates of the step after (K-split partial over own gate columns)
     f32x4 dh[2];  // own cells' summed recurrent gradient
     dh[0] = dh[1] = (f32x4)0.f;
@@ -451,24 +474,14 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     }
     __syncthreads();  // all reads of dgl (MFMA) done before it is overwritten
     if (abort_lds) return;
-    const float* gs = gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP;
-    const float* cs = csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP;
-    const float* csp =
-        has_prev ? csave + ((int64_t)(dir * ngrp_total + grp) * L + tp) * CSTEP : nullptr;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
-      const int64_t co = (((m * NW + w) * 2 + rb) * 64 + lane) * 4;
-      const f32x4 cv = *reinterpret_cast<const f32x4*>(cs + co);
-      const f32x4 cp = csp ? *reinterpret_cast<const f32x4*>(csp + co) : (f32x4)0.f;
+      const f32x4 cv = pcv[rb], cp = pcp[rb];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = rb * 16 + 4 * q4 + i;
-        const f32x4 gv =
-            *reinterpret_cast<const f32x4*>(gs + ((((m * NW + w) * 2 + rb) * 4 + i) * 64 + lane) * 4);
-        const float ig = gv[0], fg = gv[1], gg = gv[2], og = gv[3];
-        int b = b0 + row;
-        const float dyv = b < B ? dy[((int64_t)b * L + t) * hld + dir * H + u] : 0.f;
-        const float dht = dyv + dh[rb][i];
+        const float ig = pgv[rb][i][0], fg = pgv[rb][i][1], gg = pgv[rb][i][2], og = pgv[rb][i][3];
+        const float dht = pdy[rb][i] + dh[rb][i];
         const float tc = tanh_f(cv[i]);
         const float dct = dht * og * (1.f - tc * tc) + dc[rb][i];
         dc[rb][i] = dct * fg;
