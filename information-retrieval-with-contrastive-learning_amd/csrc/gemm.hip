@@ -85,6 +85,32 @@ struct Args {
   float* P;          // split-K partials [batch][split][M][N] (raw sums), or null
 };
 
+// bf16 K-outer (COL / KN) slabs are kept k-major in LDS: [BK=32 k][128 rows]
+// bf16 = 256-byte k-rows with the XOR chunk swizzle of the guide's dual-use image
+// (b), and MFMA fragments come from ds_read_b64_tr_b16 (hardware transpose: a
+// 16-lane group reads 4 k-rows x 16 columns and each lane receives its column),
+// instead of scattering 2-byte LDS writes.
+__device__ __forceinline__ int kimg_off(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+typedef short v4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4s ds_tr16(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s*)(p));
+}
+// 32x32x16 operand fragment (lane r32 = column, half h = k 8h..8h+7) of the 32
+// columns starting at col0, k-step ks, from a k-major image.
+__device__ __forceinline__ bf16x8 kimg_frag(const char* img, int col0, int ks, int lane) {
+  const int g = lane >> 4, j = lane & 15, q = j >> 2, p = j & 3;
+  const int c = col0 + 16 * (g & 1);
+  const int k0 = ks * 16 + 8 * (g >> 1);
+  const int cb = c / 8 + (p >> 1), b8 = 8 * (p & 1);
+  const v4s lo = ds_tr16(img + kimg_off(k0 + q, cb) + b8);
+  const v4s hi = ds_tr16(img + kimg_off(k0 + 4 + q, cb) + b8);
+  const v4s both[2] = {lo, hi};
+  return __builtin_bit_cast(bf16x8, both);
+}
+
 // Load one [rows x BK] slab of an operand into registers (as 16-byte vectors).
 // For K-major storage (ROW) each vector = 8 (bf16) / 4 (f32) consecutive k of one
 // row; for transposed storage (COL) each vector = consecutive rows at one k.
@@ -148,6 +174,10 @@ struct Slab {
         const int r = e / (BK / VEC);
         const int kk = (e % (BK / VEC)) * VEC;
         *reinterpret_cast<u16x8*>(lds + r * PITCH + kk * (int)sizeof(T)) = v[i];
+      } else if constexpr (sizeof(T) == 2) {
+        const int kk = e / (128 / VEC);
+        const int r = (e % (128 / VEC)) * VEC;
+        *reinterpret_cast<u16x8*>(lds + kimg_off(kk, r / 8)) = v[i];  // k-major image
       } else {
         const int kk = e / (128 / VEC);
         const int r = (e % (128 / VEC)) * VEC;
@@ -220,12 +250,18 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int row = wm * 64 + i * 32 + r32;
-          fa[i] = *reinterpret_cast<const bf16x8*>(la + row * PITCH + (ks * 16 + 8 * h) * 2);
+          if constexpr (LA == COL)
+            fa[i] = kimg_frag(la, wm * 64 + i * 32, ks, lane);
+          else
+            fa[i] = *reinterpret_cast<const bf16x8*>(la + row * PITCH + (ks * 16 + 8 * h) * 2);
         }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int row = wn * 64 + j * 32 + r32;
-          fb[j] = *reinterpret_cast<const bf16x8*>(lb + row * PITCH + (ks * 16 + 8 * h) * 2);
+          if constexpr (LB == COL)
+            fb[j] = kimg_frag(lb, wn * 64 + j * 32, ks, lane);
+          else
+            fb[j] = *reinterpret_cast<const bf16x8*>(lb + row * PITCH + (ks * 16 + 8 * h) * 2);
         }
 #pragma unroll
         for (int i = 0; i < 2; ++i)

@@ -23,6 +23,8 @@ SHAPES = [  # (name, M, N, K, epilogue)
     ("lstm_xp_l12", 16384, 2048, 512, 1),
     ("lstm_dx", 16384, 512, 2048, 0),
     ("square4k", 4096, 4096, 4096, 0),
+    ("dW_ih^T", 1024, 768, 16384, -1),   # dg^T x: both operands K-outer, split-K
+    ("dW_hh^T", 1024, 256, 16384, -1),
 ]
 
 
@@ -34,6 +36,25 @@ def main():
 
     dev = torch.device("cuda:0")
     for name, M, N, K, epi in SHAPES:
+        if epi < 0:  # K-outer operands: C[M,N] = A[K,M]^T B[K,N], fp32 accumulate
+            a = torch.randn((K, M), device=dev).to(torch.bfloat16)
+            b = torch.randn((K, N), device=dev).to(torch.bfloat16)
+            out = torch.zeros((M, N), device=dev)
+            run = lambda: ops.gemm(a, b, trans_a=True, b_is_nk=False, out=out, accumulate=True)
+            for _ in range(3):
+                run()
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(args.iters):
+                run()
+            e1.record(st)
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.iters
+            tf = 2.0 * M * N * K / us / 1e6
+            print(f"{name:14s} M={M:6d} N={N:5d} K={K:5d} COLCOL  {us:9.1f} us  {tf:7.1f} TF/s  "
+                  f"{tf / 2500:.1%}", flush=True)
+            continue
         a = torch.randn((M, K), device=dev).to(torch.bfloat16)
         b = torch.randn((N, K), device=dev).to(torch.bfloat16)
         bias = torch.randn((N,), device=dev) if epi in (1, 2, 3) else None
