@@ -95,6 +95,14 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
       (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
+// Same with an explicit cache-policy immediate (aux: 0 default, 2 nt, ...).
+template <int AUX>
+__device__ __forceinline__ void glds16_pol(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)gsrc,
+      (__attribute__((address_space(3))) void*)lds_base, 16, 0, AUX);
+}
+
 // Order-preserving map fp32 -> uint32 (larger float -> larger uint).  -0.0 is
 // folded to +0.0 and NaN to 0 (lowest), matching oracle.canon_scores.
 __device__ __forceinline__ uint32_t orderable_f32(float f) {

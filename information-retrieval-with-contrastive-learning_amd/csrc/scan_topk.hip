@@ -22,6 +22,10 @@
 
 #include "irc_common.h"
 
+#ifndef IRC_SCAN_AUX
+#define IRC_SCAN_AUX 0  // cache policy of the corpus stream (0: default)
+#endif
+
 namespace irc {
 namespace scan {
 
@@ -121,7 +125,7 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
         uint32_t off = goff[t];
         if (tail && tile * TD + grow[t] >= NS)  // clamp: loaded but never kept
           off -= (uint32_t)((tile * TD + grow[t] - (NS - 1)) * row_bytes);
-        glds16(src0 + off, base + i * 1024);
+        glds16_pol<IRC_SCAN_AUX>(src0 + off, base + i * 1024);
       }
     }
   };
