@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--q", type=int, nargs="*", default=[1, 16, 64, 256])
     args = ap.parse_args()
     from irc_amd import _lib, retrieval
 
@@ -29,7 +30,7 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(2024)
     docs = torch.nn.functional.normalize(torch.randn(args.n, args.d, generator=g)).bfloat16().to(dev)
-    for q in (1, 16, 64, 256):
+    for q in args.q:
         qq = torch.nn.functional.normalize(torch.randn(q, args.d, generator=g)).bfloat16().to(dev)
         for _ in range(3):
             retrieval.scan_topk(qq, docs, args.k)
