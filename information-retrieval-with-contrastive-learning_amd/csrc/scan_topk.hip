@@ -174,6 +174,10 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
     wait_vmcnt_dyn<PW>(ahead, extra);
     wg_barrier();  // every wave's share of the tile has landed
 
+#ifdef IRC_SCAN_DMA_ONLY  // diagnostic build: the corpus stream alone
+    wg_barrier();
+    continue;
+#endif
     const char* tb = smem + (it % G::NBUF) * G::TILE_BYTES + kh * (D / KS) * 2;
     f32x16 acc = (f32x16)0.0f;
 #pragma unroll
@@ -335,6 +339,7 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
   __shared__ uint32_t roff[SEL_MAXR + 1];
   __shared__ uint64_t s_mm[2][SEL_NW];
   __shared__ uint32_t s_misc[4];  // 0: total count, 1: kr, 2: selected digit, 3: collect ctr
+  __shared__ bool s_exact;
 
   const int q = blockIdx.x;
   const int tid = threadIdx.x;
@@ -447,7 +452,10 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
     const int last_shift = (mode == SEL_THRESHOLD) ? 48 : 0;
     uint64_t pmask = first_shift >= 56 ? 0ull : (~0ull << (first_shift + 8));
     uint64_t prefix = mn & pmask;
-    if (tid == 0) s_misc[1] = (uint32_t)k;
+    if (tid == 0) {
+      s_misc[1] = (uint32_t)k;
+      s_exact = false;
+    }
     __syncthreads();
     for (int shift = first_shift; shift >= last_shift; shift -= 8) {
       for (int i = tid; i < SEL_NW * 256; i += SEL_NT) (&hist[0][0])[i] = 0;
@@ -477,21 +485,27 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
         const uint32_t above = suf - mine;  // count in digits of higher lanes
         if (suf >= kr && above < kr) {
           uint32_t acc = above;
-          int sel = 4 * lane;
+          int sel = 4 * lane, selc = 0;
           for (int j = 3; j >= 0; --j) {
             if (acc + bb[j] >= kr) {
               sel = 4 * lane + j;
+              selc = (int)bb[j];
               break;
             }
             acc += bb[j];
           }
           s_misc[2] = (uint32_t)sel;
           s_misc[1] = kr - acc;
+          s_exact = (uint32_t)selc == kr - acc;  // the bucket holds exactly the rest
         }
       }
       __syncthreads();
       prefix |= (uint64_t)s_misc[2] << shift;
       pmask |= (uint64_t)0xff << shift;
+      // Early exit: when the chosen bucket holds exactly the remaining rank, every
+      // key with this prefix is selected, so prefix (lower bits zero) is a bound
+      // that admits exactly k keys -- the lower digits are not needed.
+      if (s_exact) break;
     }
     // THRESHOLD: bits below 48 of `prefix` are zero unless the candidates share
     // their top 16 bits; mask them so the bound is the 16-bit prefix << 48.
