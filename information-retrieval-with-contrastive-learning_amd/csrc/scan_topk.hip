@@ -185,6 +185,11 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(tb + lo[kk & 7] + 256 * (kk >> 3));
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[kk], acc, 0, 0, 0);
     }
+#ifdef IRC_SCAN_MFMA_ONLY  // diagnostic build
+    if (acc[0] == 12345.f) myreg[0] = 1;  // keep the MFMAs alive
+    wg_barrier();
+    continue;
+#endif
     if (KS == 2) {
       // exchange: wave kh sends the half it does NOT finish, adds the partner's.
       float* xo = xbuf + ((g * 2 + kh) * 64 + lane) * 8;
@@ -211,6 +216,11 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
       }
     }
 
+#ifdef IRC_SCAN_NO_EPI  // diagnostic build
+    if (acc[0] == 12345.f) myreg[0] = 1;
+    wg_barrier();
+    continue;
+#endif
     // Epilogue: C[doc row][query col]; col = lane&31, row = (j&3) + 8(j>>2) + 4h.
     int nst = 0;
     const int s0row = tile * TD;
