@@ -236,10 +236,14 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
         const uint32_t gidx = idx_base + (uint32_t)s * (uint32_t)stride;
         const uint64_t key = make_key(v, gidx);
         const bool keep = ok && key >= qthr;
+#ifdef IRC_SCAN_NO_STORE  // diagnostic build: survivors counted, never stored
+        if (keep) ++nsurv;
+#else
         if (__ballot(keep)) {  // one store instruction when any lane keeps
           ++nst;
           if (keep) myreg[nsurv++] = key;
         }
+#endif
       }
     }
     nst2 = nst1;
