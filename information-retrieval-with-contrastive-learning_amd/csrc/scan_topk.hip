@@ -68,7 +68,8 @@ __device__ __forceinline__ int opaque(int x) {
 // private slice (kh*2 + h) of the (worker, query) region and counts in a
 // register -- no atomics, nothing that could drain the LDS-DMA ring.
 template <int D, int NQ, int KS, int MODE>
-__global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
+__global__ __launch_bounds__(NQ * KS * 64) __attribute__((amdgpu_waves_per_eu(1, 4)))
+void scan_tile_kernel(
     const unsigned short* __restrict__ queries, const unsigned short* __restrict__ docs, int Q,
     int Qpad, int GY, int NS, int stride, int tiles_per_worker, uint32_t idx_base,
     const uint64_t* __restrict__ thr, uint64_t* __restrict__ keys, uint32_t* __restrict__ counts,
@@ -157,6 +158,8 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
     lo[j] = r32 * (G::CH * 16) + (((cj & 15) ^ (r32 & G::SWZ)) * 16);
   }
   uint32_t nsurv = 0;
+  uint64_t sb0 = 0, sb1 = 0, sb2 = 0, sb3 = 0;  // survivor shift buffer (KEYS mode)
+  int sbn = 0;
   // Survivor store instructions issued by this wave in the last two tiles
   // (wave-uniform).  They sit between the ring's DMAs in vmcnt order, so the
   // wait for tile `it` allows them as extra younger operations.
@@ -180,10 +183,16 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
 #endif
     const char* tb = smem + (it % G::NBUF) * G::TILE_BYTES + kh * (D / KS) * 2;
     f32x16 acc = (f32x16)0.0f;
+    {
+      // every A fragment of the tile first (one LDS latency, not KKW of them:
+      // with one wave per SIMD nothing else hides it), then the MFMA chain
+      bf16x8 af[KKW];
 #pragma unroll
-    for (int kk = 0; kk < KKW; ++kk) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(tb + lo[kk & 7] + 256 * (kk >> 3));
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[kk], acc, 0, 0, 0);
+      for (int kk = 0; kk < KKW; ++kk)
+        af[kk] = *reinterpret_cast<const bf16x8*>(tb + lo[kk & 7] + 256 * (kk >> 3));
+#pragma unroll
+      for (int kk = 0; kk < KKW; ++kk)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk], bq[kk], acc, 0, 0, 0);
     }
 #ifdef IRC_SCAN_MFMA_ONLY  // diagnostic build
     if (acc[0] == 12345.f) myreg[0] = 1;  // keep the MFMAs alive
@@ -222,13 +231,21 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
     continue;
 #endif
     // Epilogue: C[doc row][query col]; col = lane&31, row = (j&3) + 8(j>>2) + 4h.
+    // The wave finishes registers jj + joff of acc (joff: wave-uniform half).
     int nst = 0;
     const int s0row = tile * TD;
+    f32x16 fin = acc;
+    int joff = 0;
+    if (KS == 2 && kh == 1) {  // uniform branch: move the upper half down
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) fin[jj] = acc[jj + 8];
+      joff = 8;
+    }
 #pragma unroll
     for (int jj = 0; jj < JPW; ++jj) {
-      const int j = (KS == 2 && kh == 1) ? jj + 8 : jj;
+      const int j = jj + joff;
       const int s = s0row + (j & 3) + 8 * (j >> 2) + 4 * h;
-      const float v = (KS == 2 && kh == 1) ? acc[jj + 8] : acc[jj];
+      const float v = fin[jj];
       const bool ok = (q < Q) && (s < NS);
       if (MODE == SCORES) {
         if (ok) scores_out[(int64_t)q * NS + s] = v;
@@ -239,9 +256,27 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
 #ifdef IRC_SCAN_NO_STORE  // diagnostic build: survivors counted, never stored
         if (keep) ++nsurv;
 #else
-        if (__ballot(keep)) {  // one store instruction when any lane keeps
-          ++nst;
-          if (keep) myreg[nsurv++] = key;
+        // Survivors wait in a per-lane 4-key shift buffer and leave 4 at a time:
+        // a store is older than the DMAs issued after it and vmcnt retires in
+        // order, so every store episode delays a later tile's wait by its
+        // write-ack latency -- 4x fewer episodes.
+        if (keep) {
+          sb3 = sb2;
+          sb2 = sb1;
+          sb1 = sb0;
+          sb0 = key;
+          ++sbn;
+        }
+        if (__ballot(sbn == 4)) {
+          nst += 4;
+          if (sbn == 4) {
+            myreg[nsurv] = sb0;
+            myreg[nsurv + 1] = sb1;
+            myreg[nsurv + 2] = sb2;
+            myreg[nsurv + 3] = sb3;
+            nsurv += 4;
+            sbn = 0;
+          }
         }
 #endif
       }
@@ -251,6 +286,12 @@ __global__ __launch_bounds__(NQ * KS * 64) void scan_tile_kernel(
     wg_barrier();  // all reads of this buffer (and of xbuf) done before reuse
   }
 
+  if (MODE == KEYS) {  // flush the shift buffer (newest first; order is irrelevant)
+    if (sbn > 0) myreg[nsurv] = sb0;
+    if (sbn > 1) myreg[nsurv + 1] = sb1;
+    if (sbn > 2) myreg[nsurv + 2] = sb2;
+    nsurv += (uint32_t)sbn;
+  }
   if (MODE == KEYS && q < Qpad)
     counts[((int64_t)worker * Qpad + q) * (2 * KS) + slice] = nsurv;
 }
