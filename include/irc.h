@@ -75,7 +75,10 @@ int irc_scan_scores(const void* queries, const void* docs, int64_t Q, int64_t N,
  * in_dtype/out_dtype: 0 = bf16, 1 = fp32 (fp32 inputs use the exact f32 MFMA).
  * a_layout: 0 = A is [M][K], 1 = A is [K][M];  b_layout: 0 = B is [N][K]
  * (nn.Linear weight), 1 = B is [K][N].  epilogue: 0 none, 1 +bias, 2 +bias->GELU(erf),
- * 3 +bias+R, 4 +R.  accumulate (fp32 C only): C += result. */
+ * 3 +bias+R, 4 +R, 5 *gelu'(R) (GELU backward, R = saved pre-activation),
+ * 6 +bias->GELU with the pre-activation ALSO written to R (R is an output here;
+ * the forward of the trainable encoder's FFN1, saving what epilogue 5 needs).
+ * accumulate (fp32 C only, epilogues 0-4): C += result. */
 int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue, int64_t M,
              int64_t N, int64_t K, float alpha, const void* A, int64_t lda, int64_t strideA,
              const void* B, int64_t ldb, int64_t strideB, const float* bias, int64_t strideBias,
@@ -101,6 +104,37 @@ int irc_layernorm(int dtype, const void* x, void* y, const float* gamma, const f
                   int64_t rows, int64_t H, float eps, irc_stream_t stream);
 int irc_attention(int dtype, const void* qkv, const int64_t* mask, void* ctx, int64_t B,
                   int64_t L, int64_t H, int64_t heads, irc_stream_t stream);
+
+/* ----------------------------------------------------- BERT encoder backward
+ * Gradients of the forward above for the trainable bi-encoder (`--model BERT`,
+ * the north star's encoder fwd/bwd; the reference runs the same HF BertModel
+ * frozen at contrastive_module.py:36-41).
+ * irc_layernorm_bwd: x = the LN input (recomputed statistics), dy [rows, H]
+ *   (dy_dtype 0 bf16 / 1 fp32; with bcast_L > 0 row r reads dy[r / bcast_L] *
+ *   dy_scale -- the mean-pool backward folded in), dx in dtype; dgamma/dbeta fp32
+ *   (+)= deterministic column sums; partial: irc_layernorm_bwd_workspace floats.
+ * irc_attention_bwd: qkv / mask / ctx as the forward, dctx [B*L, H] -> dqkv
+ *   [B*L, 3H] (same fused layout as qkv).  P is recomputed (additive key bias).
+ * irc_embed_bwd: dx = gradient of the embedding sum [B*L, H] -> dword[ids] +=
+ *   (fp32 atomics; rows with pad_id skipped, as nn.Embedding(padding_idx)),
+ *   dpos[l] += sum_b, dtype0 += sum over all rows (fixed order); workspace L*H
+ *   floats; any of dword/dpos/dtype0 may be NULL. */
+int64_t irc_layernorm_bwd_workspace(int64_t rows, int64_t H);
+int irc_layernorm_bwd(int dtype, int dy_dtype, const void* dy, const void* x, const float* gamma,
+                      void* dx, float* dgamma, float* dbeta, float* partial,
+                      int64_t partial_floats, int64_t rows, int64_t H, float eps, int64_t bcast_L,
+                      float dy_scale, int accumulate, irc_stream_t stream);
+int irc_attention_bwd(int dtype, const void* qkv, const int64_t* mask, const void* ctx,
+                      const void* dctx, void* dqkv, int64_t B, int64_t L, int64_t H,
+                      int64_t heads, irc_stream_t stream);
+/* y fp32 [rows, H] = word[ids] + type0 + pos[row % L]: the embedding-LN input
+ * (irc_embed_ln fuses it away in the forward; the backward rebuilds it). */
+int irc_embed_sum(int dtype, const int64_t* ids, const void* word, const void* pos,
+                  const void* type0, float* y, int64_t rows, int64_t L, int64_t H,
+                  irc_stream_t stream);
+int irc_embed_bwd(int dtype, const void* dx, const int64_t* ids, float* dword, float* dpos,
+                  float* dtype0, float* workspace, int64_t ws_floats, int64_t B, int64_t L,
+                  int64_t H, int64_t pad_id, irc_stream_t stream);
 
 /* --------------------------------------------------------------- BiLSTM head
  * nn.LSTM recurrences (src/model.py:16-22, 39), gate order i,f,g,o, zero state,
@@ -193,6 +227,13 @@ int irc_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const
                   float b1, float b2, float step_size, float bc2_sqrt, float eps,
                   irc_stream_t stream);
 int irc_momentum_update(float* pk, const float* pq, int64_t n, float mom, irc_stream_t stream);
+/* Same updates that also refresh a bf16 shadow of the parameters (the trainable
+ * encoder's MFMA operand copy) in the same pass. */
+int irc_adam_step_bf16(float* p, const float* g, float* m, float* v, int64_t n, const float* coef,
+                       float b1, float b2, float step_size, float bc2_sqrt, float eps,
+                       void* p_bf16, irc_stream_t stream);
+int irc_momentum_update_bf16(float* pk, const float* pq, int64_t n, float mom, void* pk_bf16,
+                             irc_stream_t stream);
 int irc_enqueue(float* queue, const float* keys, int64_t* ptr, int64_t D, int64_t K, int64_t B,
                 irc_stream_t stream);
 int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t stream);

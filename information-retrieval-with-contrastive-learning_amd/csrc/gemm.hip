@@ -28,7 +28,16 @@ namespace irc {
 namespace gemm {
 
 enum Layout { ROW = 0, COL = 1 };  // A: ROW=[M][K], COL=[K][M]; B: ROW=[N][K] (NK), COL=[K][N] (KN)
-enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RESID = 3, EPI_RESID = 4 };
+// EPI_DGELU: C = alpha acc * gelu'(R)  (GELU backward; R = saved pre-activation)
+// EPI_BIAS_GELU_SAVE: C = gelu(alpha acc + bias) and R <- alpha acc + bias (R is a
+// second OUTPUT here: the pre-activation the GELU backward needs)
+enum Epi {
+  EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RESID = 3, EPI_RESID = 4,
+  EPI_DGELU = 5, EPI_BIAS_GELU_SAVE = 6
+};
+__host__ __device__ constexpr bool epi_has_bias(int e) {
+  return e == EPI_BIAS || e == EPI_BIAS_GELU || e == EPI_BIAS_RESID || e == EPI_BIAS_GELU_SAVE;
+}
 
 constexpr int BM = 128, BN = 128, NT = 256;
 
@@ -66,6 +75,25 @@ __device__ __forceinline__ float gelu_fast(float x) {
   p = p * t + 0.254829592f;
   const float e = 1.0f - p * t * __expf(-az * az);
   return 0.5f * x * (1.0f + copysignf(e, z));
+}
+
+// d/dx GELU(x) = Phi(x) + x phi(x), Phi via the same A&S 7.1.26 erf as gelu_fast.
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * az);
+  float p = 1.061405429f;
+  p = p * t - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const float ez = __expf(-az * az);
+  const float e = 1.0f - p * t * ez;
+  return 0.5f * (1.0f + copysignf(e, z)) + x * 0.3989422804014327f * ez;
+}
+__device__ __forceinline__ float gelu_grad_erf(float x) {
+  return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) +
+         x * 0.3989422804014327f * __expf(-0.5f * x * x);
 }
 
 struct Args {
@@ -327,8 +355,7 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
   for (int j = 0; j < 2; ++j) {
     const int col = n0 + wn * 64 + j * 32 + r32;
     if (col >= g.N) continue;
-    const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESID) ? bias[col]
-                                                                                        : 0.f;
+    const float bv = epi_has_bias(EPI) ? bias[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -337,11 +364,21 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
         if (row >= g.M) continue;
         float v = acc[i][j][e] * g.alpha + bv;
         if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
-        if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
+        if (EPI == EPI_BIAS_GELU_SAVE) {
+          TO* pre = const_cast<TO*>(R) + (int64_t)row * g.ldr + col;
           if constexpr (sizeof(TO) == 2)
-            v += bf16_to_f32(reinterpret_cast<const unsigned short*>(R)[(int64_t)row * g.ldr + col]);
+            *reinterpret_cast<unsigned short*>(pre) = f32_to_bf16(v);
           else
-            v += reinterpret_cast<const float*>(R)[(int64_t)row * g.ldr + col];
+            *reinterpret_cast<float*>(pre) = v;
+          v = gelu_erf(v);
+        }
+        if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
+          float r;
+          if constexpr (sizeof(TO) == 2)
+            r = bf16_to_f32(reinterpret_cast<const unsigned short*>(R)[(int64_t)row * g.ldr + col]);
+          else
+            r = reinterpret_cast<const float*>(R)[(int64_t)row * g.ldr + col];
+          v = EPI == EPI_DGELU ? v * gelu_grad_erf(r) : v + r;
         }
         TO* dst = C + (int64_t)row * g.ldc + col;
         if constexpr (sizeof(TO) == 2) {
@@ -510,8 +547,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 #pragma unroll
     for (int j = 0; j < WNB; ++j) {
       const int col = cbase + j * 32 + r32;
-      bv[j] = (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESID) && col < g.N
-                  ? bias[col] : 0.f;
+      bv[j] = epi_has_bias(EPI) && col < g.N ? bias[col] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -538,11 +574,23 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
           const f32x4 v0 = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c8]);
           const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c8 + 4]);
           float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
+          if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
             const u16x8 rr = *reinterpret_cast<const u16x8*>(
                 reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col);
 #pragma unroll
-            for (int t = 0; t < 8; ++t) v[t] += bf16_to_f32(rr[t]);
+            for (int t = 0; t < 8; ++t)
+              v[t] = EPI == EPI_DGELU ? v[t] * gelu_grad_fast(bf16_to_f32(rr[t]))
+                                      : v[t] + bf16_to_f32(rr[t]);
+          }
+          if (EPI == EPI_BIAS_GELU_SAVE) {
+            u16x8 pre;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              pre[t] = f32_to_bf16(v[t]);
+              v[t] = gelu_fast(v[t]);
+            }
+            *reinterpret_cast<u16x8*>(const_cast<unsigned short*>(
+                reinterpret_cast<const unsigned short*>(R)) + (int64_t)row * g.ldr + col) = pre;
           }
           u16x8 o;
 #pragma unroll
@@ -559,9 +607,18 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
           const int row = rbase + rl, col = cbase + c4;
           if (row >= g.M || col >= g.N) continue;
           f32x4 v = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c4]);
-          if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID)
-            v += *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(R) +
-                                                (int64_t)row * g.ldr + col);
+          if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
+            const f32x4 r = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(R) +
+                                                            (int64_t)row * g.ldr + col);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] = EPI == EPI_DGELU ? v[t] * gelu_grad_fast(r[t]) : v[t] + r[t];
+          }
+          if (EPI == EPI_BIAS_GELU_SAVE) {
+            *reinterpret_cast<f32x4*>(const_cast<float*>(reinterpret_cast<const float*>(R)) +
+                                      (int64_t)row * g.ldr + col) = v;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] = gelu_fast(v[t]);
+          }
           float* dst = reinterpret_cast<float*>(C) + (int64_t)row * g.ldc + col;
           if (g.accumulate) v += *reinterpret_cast<const f32x4*>(dst);
           *reinterpret_cast<f32x4*>(dst) = v;
@@ -576,8 +633,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
   for (int j = 0; j < WNB; ++j) {
     const int col = n0 + wn * WCOLS + j * 32 + r32;
     if (col >= g.N) continue;
-    const float bv = (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RESID) ? bias[col]
-                                                                                        : 0.f;
+    const float bv = epi_has_bias(EPI) ? bias[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -586,11 +642,21 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
         if (row >= g.M) continue;
         float v = acc[i][j][e] * g.alpha + bv;
         if (EPI == EPI_BIAS_GELU) v = gelu_fast(v);
-        if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID) {
+        if (EPI == EPI_BIAS_GELU_SAVE) {
+          TO* pre = const_cast<TO*>(R) + (int64_t)row * g.ldr + col;
           if constexpr (sizeof(TO) == 2)
-            v += bf16_to_f32(reinterpret_cast<const unsigned short*>(R)[(int64_t)row * g.ldr + col]);
+            *reinterpret_cast<unsigned short*>(pre) = f32_to_bf16(v);
           else
-            v += reinterpret_cast<const float*>(R)[(int64_t)row * g.ldr + col];
+            *reinterpret_cast<float*>(pre) = v;
+          v = gelu_fast(v);
+        }
+        if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
+          float r;
+          if constexpr (sizeof(TO) == 2)
+            r = bf16_to_f32(reinterpret_cast<const unsigned short*>(R)[(int64_t)row * g.ldr + col]);
+          else
+            r = reinterpret_cast<const float*>(R)[(int64_t)row * g.ldr + col];
+          v = EPI == EPI_DGELU ? v * gelu_grad_fast(r) : v + r;
         }
         TO* dst = C + (int64_t)row * g.ldc + col;
         if constexpr (sizeof(TO) == 2) {
@@ -662,6 +728,8 @@ static int by_epi(int epi, const Args& g, int batch, int splits, hipStream_t st)
     case EPI_BIAS_GELU: return launch<TI, TO, LA, LB, EPI_BIAS_GELU>(g, batch, 1, st);
     case EPI_BIAS_RESID: return launch<TI, TO, LA, LB, EPI_BIAS_RESID>(g, batch, 1, st);
     case EPI_RESID: return launch<TI, TO, LA, LB, EPI_RESID>(g, batch, 1, st);
+    case EPI_DGELU: return launch<TI, TO, LA, LB, EPI_DGELU>(g, batch, 1, st);
+    case EPI_BIAS_GELU_SAVE: return launch<TI, TO, LA, LB, EPI_BIAS_GELU_SAVE>(g, batch, 1, st);
   }
   set_error("gemm: bad epilogue %d", epi);
   return IRC_E_INVALID;
@@ -700,9 +768,11 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
   IRC_REQUIRE(in_dtype == 0 || in_dtype == 1, "gemm: in_dtype must be 0 (bf16) or 1 (fp32)");
   IRC_REQUIRE(out_dtype == 0 || out_dtype == 1, "gemm: out_dtype must be 0 (bf16) or 1 (fp32)");
   IRC_REQUIRE(!(accumulate && out_dtype == 0), "gemm: accumulate needs fp32 C");
-  IRC_REQUIRE(epilogue >= 0 && epilogue <= 4, "gemm: bad epilogue");
-  IRC_REQUIRE(!(epilogue >= 1 && epilogue <= 3) || bias, "gemm: epilogue needs bias");
-  IRC_REQUIRE(!(epilogue == 3 || epilogue == 4) || R, "gemm: epilogue needs residual");
+  IRC_REQUIRE(epilogue >= 0 && epilogue <= 6, "gemm: bad epilogue");
+  IRC_REQUIRE(!gemm::epi_has_bias(epilogue) || bias, "gemm: epilogue needs bias");
+  IRC_REQUIRE(!(epilogue >= 3 && epilogue != 1 && epilogue != 2) || R,
+              "gemm: epilogue needs R (residual / pre-activation)");
+  IRC_REQUIRE(!(accumulate && epilogue >= 5), "gemm: accumulate with a GELU epilogue");
   // 16-byte vector staging needs every row start 16-byte aligned; otherwise the
   // operand is staged element by element (same results, slower).
   const int vec = in_dtype == 0 ? 8 : 4;

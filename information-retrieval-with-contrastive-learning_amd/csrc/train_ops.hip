@@ -194,10 +194,11 @@ __global__ void finalize_kernel(const float* __restrict__ partial, int np, float
 
 // Adam (torch.optim.Adam, weight_decay 0, amsgrad False) with the clip coefficient
 // applied to the gradient: g' = g * coef[1].
+// pb (may be null): bf16 shadow of the updated parameters (the MFMA operand copy).
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                             float* __restrict__ m, float* __restrict__ v, int64_t n,
                             const float* __restrict__ coef, float b1, float b2, float step_size,
-                            float bc2_sqrt, float eps) {
+                            float bc2_sqrt, float eps, unsigned short* __restrict__ pb) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float c = coef ? coef[1] : 1.f;
@@ -207,13 +208,18 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
   m[i] = mi;
   v[i] = vi;
   const float denom = sqrtf(vi) / bc2_sqrt + eps;
-  p[i] = p[i] - step_size * (mi / denom);
+  const float np = p[i] - step_size * (mi / denom);
+  p[i] = np;
+  if (pb) pb[i] = f32_to_bf16(np);
 }
 
 __global__ void momentum_kernel(float* __restrict__ pk, const float* __restrict__ pq, int64_t n,
-                                float mom) {
+                                float mom, unsigned short* __restrict__ pb) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) pk[i] = pk[i] * mom + pq[i] * (1.f - mom);
+  if (i >= n) return;
+  const float v = pk[i] * mom + pq[i] * (1.f - mom);
+  pk[i] = v;
+  if (pb) pb[i] = f32_to_bf16(v);
 }
 
 // queue[d, ptr + b] = keys[b, d]
@@ -437,15 +443,32 @@ extern "C" int irc_adam_step(float* p, const float* g, float* m, float* v, int64
                              float bc2_sqrt, float eps, irc_stream_t stream) {
   if (n == 0) return IRC_OK;
   hipLaunchKernelGGL(adam_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), p, g, m, v, n,
-                     coef, b1, b2, step_size, bc2_sqrt, eps);
+                     coef, b1, b2, step_size, bc2_sqrt, eps, nullptr);
   return check_launch("adam");
+}
+
+extern "C" int irc_adam_step_bf16(float* p, const float* g, float* m, float* v, int64_t n,
+                                  const float* coef, float b1, float b2, float step_size,
+                                  float bc2_sqrt, float eps, void* p_bf16, irc_stream_t stream) {
+  if (n == 0) return IRC_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), p, g, m, v, n,
+                     coef, b1, b2, step_size, bc2_sqrt, eps, (unsigned short*)p_bf16);
+  return check_launch("adam_bf16");
+}
+
+extern "C" int irc_momentum_update_bf16(float* pk, const float* pq, int64_t n, float mom,
+                                        void* pk_bf16, irc_stream_t stream) {
+  if (n == 0) return IRC_OK;
+  hipLaunchKernelGGL(momentum_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), pk, pq, n,
+                     mom, (unsigned short*)pk_bf16);
+  return check_launch("momentum_bf16");
 }
 
 extern "C" int irc_momentum_update(float* pk, const float* pq, int64_t n, float mom,
                                    irc_stream_t stream) {
   if (n == 0) return IRC_OK;
   hipLaunchKernelGGL(momentum_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), pk, pq, n,
-                     mom);
+                     mom, nullptr);
   return check_launch("momentum");
 }
 

@@ -36,6 +36,12 @@ SIGNATURES = {
     "irc_embed_ln": (I32, [I32, P, P, P, P, P, P, P, I64, I64, I64, F32, P]),
     "irc_layernorm": (I32, [I32, P, P, P, P, I64, I64, F32, P]),
     "irc_attention": (I32, [I32, P, P, P, I64, I64, I64, I64, P]),
+    "irc_layernorm_bwd_workspace": (I64, [I64, I64]),
+    "irc_layernorm_bwd": (I32, [I32, I32, P, P, P, P, P, P, P, I64, I64, I64, F32, I64, F32, I32,
+                                P]),
+    "irc_attention_bwd": (I32, [I32, P, P, P, P, P, I64, I64, I64, I64, P]),
+    "irc_embed_sum": (I32, [I32, P, P, P, P, P, I64, I64, I64, P]),
+    "irc_embed_bwd": (I32, [I32, P, P, P, P, P, P, I64, I64, I64, I64, I64, P]),
     "irc_lstm_fwd": (I32, [I32, P, P, P, P, P, P, I64, I64, I64, I64, P]),
     "irc_lstm_bwd": (I32, [I32, P, P, P, P, P, I64, I64, I64, I64, P]),
     "irc_lstm_mfma_supported": (I32, [I64]),
@@ -60,6 +66,8 @@ SIGNATURES = {
     "irc_grad_norm_clip": (I32, [P, I64, F32, P, P, P]),
     "irc_adam_step": (I32, [P, P, P, P, I64, P, F32, F32, F32, F32, F32, P]),
     "irc_momentum_update": (I32, [P, P, I64, F32, P]),
+    "irc_adam_step_bf16": (I32, [P, P, P, P, I64, P, F32, F32, F32, F32, F32, P, P]),
+    "irc_momentum_update_bf16": (I32, [P, P, I64, F32, P, P]),
     "irc_enqueue": (I32, [P, P, P, I64, I64, I64, P]),
     "irc_cast_bf16": (I32, [P, P, I64, P]),
     "irc_cast_bf16_t": (I32, [P, P, I64, I64, P]),

@@ -1,0 +1,397 @@
+"""Trainable BERT bi-encoder (``--model BERT``): forward with saved activations and
+a full backward on the irc HIP kernels.
+
+The reference trains only the BiLSTM head over a frozen HF BertModel
+(src/contrastor/contrastive_module.py:30-41, src/model.py:61-70).  The north star
+adds the encoder forward/backward: this module is the same BERT forward as
+``irc_amd.bert`` (HF BertModel semantics, eval mode, no dropout) made
+trainable, with seq2vec = mean over ALL L positions (PAD included, as the
+reference's ``seq2vec``, contrastive_module.py:102-112) + F.normalize, so the
+embedding dim is the hidden size.
+
+Parameters live in ONE flat fp32 buffer with HF-named views (``state_dict()``
+keys are HF's ``embeddings.*`` / ``encoder.layer.N.*`` / ``pooler.*``), the
+gradients in a parallel flat buffer, so clip + Adam + the momentum update are
+single fused launches (irc_amd.optim / contrastive_module), exactly as for the
+LSTM head.  In bf16 mode the MFMA operands come from a flat bf16 shadow that the
+Adam / momentum kernels rewrite in the same pass, plus transposed bf16 copies of
+the weight matrices for the dX GEMMs (so they take the big-tile A[M][K].B[N][K]
+path); fp32 mode (parity) runs every GEMM on the exact-fp32 MFMA.
+
+Per layer, forward (saved for backward in brackets):
+  qkv = x Wqkv^T + b [qkv] -> ctx = attention(qkv) [ctx] -> s1 = ctx Wo^T + bo + x
+  [s1] -> a = LN1(s1) [a] -> g = gelu(u), u = a W1^T + b1 [u, g] -> s2 = g W2^T + b2
+  + a [s2] -> y = LN2(s2) (next layer's x [x]).
+Backward mirrors it: LN bwd (recomputed statistics) -> dW / db (side stream) and
+dX GEMMs with fused residual / GELU' epilogues -> attention bwd -> ... -> the
+embedding LN bwd and the word / position / token-type scatter.
+"""
+from __future__ import annotations
+
+import copy
+import math
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._torch import side_stream
+from .bert import BERT_BASE, PRESETS, BertConfig, BertModel
+from .precision import compute_dtype
+
+ALIGN = 16  # floats per slice start (16-byte-aligned bf16 shadow slices)
+
+
+def bert_param_specs(c: BertConfig):
+    """(name, shape) in HF BertModel.named_parameters() order, except that each
+    layer's query/key/value weights (and biases) are listed adjacently so the
+    fused [3H, H] QKV operand is a view of the flat buffer."""
+    H, I = c.hidden_size, c.intermediate_size
+    s = [("embeddings.word_embeddings.weight", (c.vocab_size, H)),
+         ("embeddings.position_embeddings.weight", (c.max_position_embeddings, H)),
+         ("embeddings.token_type_embeddings.weight", (c.type_vocab_size, H)),
+         ("embeddings.LayerNorm.weight", (H,)), ("embeddings.LayerNorm.bias", (H,))]
+    for l in range(c.num_hidden_layers):
+        p = f"encoder.layer.{l}."
+        s += [(p + "attention.self.query.weight", (H, H)),
+              (p + "attention.self.key.weight", (H, H)),
+              (p + "attention.self.value.weight", (H, H)),
+              (p + "attention.self.query.bias", (H,)),
+              (p + "attention.self.key.bias", (H,)),
+              (p + "attention.self.value.bias", (H,)),
+              (p + "attention.output.dense.weight", (H, H)),
+              (p + "attention.output.dense.bias", (H,)),
+              (p + "attention.output.LayerNorm.weight", (H,)),
+              (p + "attention.output.LayerNorm.bias", (H,)),
+              (p + "intermediate.dense.weight", (I, H)), (p + "intermediate.dense.bias", (I,)),
+              (p + "output.dense.weight", (H, I)), (p + "output.dense.bias", (H,)),
+              (p + "output.LayerNorm.weight", (H,)), (p + "output.LayerNorm.bias", (H,))]
+    s += [("pooler.dense.weight", (H, H)), ("pooler.dense.bias", (H,))]
+    return s
+
+
+class BertEncoder(nn.Module):
+    """Trainable BERT + mean-pool bi-encoder (the ``--model BERT`` base encoder)."""
+
+    def __init__(self, config: BertConfig | dict | None = None, name: str = "bert-base-uncased",
+                 seed: int | None = 0, init_from: BertModel | None = None):
+        super().__init__()
+        if isinstance(config, dict):
+            config = BertConfig.from_dict(config)
+        self.config = config or PRESETS.get(name, BERT_BASE)
+        c = self.config
+        if c.hidden_size % c.num_attention_heads:
+            raise ValueError("hidden_size % num_attention_heads != 0")
+        if c.hidden_size % ALIGN:
+            raise ValueError(f"hidden_size must be a multiple of {ALIGN}")
+        self.specs = bert_param_specs(c)
+        self.offsets, o = {}, 0
+        for n, shp in self.specs:
+            o = (o + ALIGN - 1) // ALIGN * ALIGN
+            self.offsets[n] = o
+            o += math.prod(shp)
+        self.numel_flat = (o + ALIGN - 1) // ALIGN * ALIGN
+        for l in range(c.num_hidden_layers):  # fused QKV operand = one view
+            p = f"encoder.layer.{l}.attention.self."
+            H = c.hidden_size
+            assert self.offsets[p + "key.weight"] == self.offsets[p + "query.weight"] + H * H
+            assert self.offsets[p + "value.weight"] == self.offsets[p + "key.weight"] + H * H
+            assert self.offsets[p + "key.bias"] == self.offsets[p + "query.bias"] + H
+            assert self.offsets[p + "value.bias"] == self.offsets[p + "key.bias"] + H
+        self.flat = nn.Parameter(torch.zeros(self.numel_flat), requires_grad=True)
+        self.register_buffer("flat_grad", torch.zeros(self.numel_flat), persistent=False)
+        self._shadow = None      # bf16 mirror of flat (MFMA operands)
+        self._shadow_t = None    # {name: bf16 transposed weight} (dX GEMM operands)
+        self._shadow_ok = False
+        self._shadow_t_ok = False
+        self._wgrad_pending = None
+        if init_from is not None:
+            self.load_from_bert(init_from)
+        else:
+            self.load_from_bert(BertModel(c, seed=seed))
+
+    # ---- parameter plumbing (same interface as LSTMHead: view / specs / flat) ----
+    def view(self, name, buf=None):
+        buf = self.flat if buf is None else buf
+        shape = dict(self.specs)[name]
+        o = self.offsets[name]
+        return buf.detach()[o:o + math.prod(shape)].view(shape)
+
+    def _span(self, first, n, buf=None):
+        buf = self.flat if buf is None else buf
+        o = self.offsets[first]
+        return buf.detach()[o:o + n]
+
+    def named_flat_params(self):
+        return [(n, self.view(n)) for n, _ in self.specs]
+
+    @torch.no_grad()
+    def load_from_bert(self, bert: BertModel):
+        sd = bert.state_dict()
+        for n, shape in self.specs:
+            self.view(n).copy_(sd[n].reshape(shape).to(self.flat.device, torch.float32))
+        self.invalidate_shadow()
+
+    def invalidate_shadow(self):
+        self._shadow_ok = False
+        self._shadow_t_ok = False
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        for n, _ in self.specs:
+            destination[prefix + n] = self.view(n).clone()
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        with torch.no_grad():
+            for n, shape in self.specs:
+                k = prefix + n
+                if k in state_dict:
+                    self.view(n).copy_(state_dict[k].reshape(shape))
+                elif strict:
+                    missing_keys.append(k)
+        for k in state_dict:
+            if k.startswith(prefix) and k[len(prefix):] not in self.offsets and strict \
+                    and not k.endswith("position_ids"):
+                unexpected_keys.append(k)
+        self.invalidate_shadow()
+
+    def _apply(self, fn, *a, **k):
+        r = super()._apply(fn, *a, **k)
+        self._shadow = self._shadow_t = None
+        self.invalidate_shadow()
+        return r
+
+    # ---- bf16 shadows ----
+    def shadow(self):
+        """bf16 mirror of the flat buffer (rebuilt when invalid; otherwise kept
+        current by the Adam / momentum kernels, which write it in their pass)."""
+        if self._shadow is None or self._shadow.device != self.flat.device:
+            self._shadow = torch.empty(self.numel_flat, dtype=torch.bfloat16,
+                                       device=self.flat.device)
+            self._shadow_ok = False
+        if not self._shadow_ok:
+            ops.cast_bf16_into(self.flat.detach(), self._shadow)
+            self._shadow_ok = True
+        return self._shadow
+
+    def shadow_buffer(self):
+        """The bf16 shadow storage for an update kernel that rewrites all of it
+        (None in fp32 mode, where no shadow is used)."""
+        if compute_dtype() != torch.bfloat16:
+            return None
+        if self._shadow is None or self._shadow.device != self.flat.device:
+            self._shadow = torch.empty(self.numel_flat, dtype=torch.bfloat16,
+                                       device=self.flat.device)
+        return self._shadow
+
+    def _matrices(self):
+        c = self.config
+        H = c.hidden_size
+        out = []
+        for l in range(c.num_hidden_layers):
+            p = f"encoder.layer.{l}."
+            out += [(p + "attention.self.query.weight", (3 * H, H)),
+                    (p + "attention.output.dense.weight", (H, H)),
+                    (p + "intermediate.dense.weight", (c.intermediate_size, H)),
+                    (p + "output.dense.weight", (H, c.intermediate_size))]
+        return out
+
+    def shadow_t(self):
+        """{weight name: bf16 W^T} for the dX GEMMs (rebuilt after each update)."""
+        if self._shadow_t is None or next(iter(self._shadow_t.values())).device != \
+                self.flat.device:
+            self._shadow_t = {n: torch.empty((s[1], s[0]), dtype=torch.bfloat16,
+                                             device=self.flat.device)
+                              for n, s in self._matrices()}
+            self._shadow_t_ok = False
+        if not self._shadow_t_ok:
+            flat = self.flat.detach()
+            for n, (r, cc) in self._matrices():
+                o = self.offsets[n]
+                ops.cast_bf16_t_into(flat[o:o + r * cc].view(r, cc), self._shadow_t[n])
+            self._shadow_t_ok = True
+        return self._shadow_t
+
+    def after_update(self, shadow_written: bool):
+        """Called by the optimizer / momentum update after the flat buffer moved."""
+        self._shadow_ok = bool(shadow_written) and self._shadow is not None
+        self._shadow_t_ok = False
+
+    def _weights(self, dt, with_t=False):
+        """Per-layer operand views in the compute dtype."""
+        c = self.config
+        H, I = c.hidden_size, c.intermediate_size
+        src = self.shadow() if dt == torch.bfloat16 else self.flat.detach()
+        f32 = self.flat.detach()
+        sT = self.shadow_t() if (with_t and dt == torch.bfloat16) else None
+
+        def v(buf, name, shape):
+            o = self.offsets[name]
+            return buf[o:o + math.prod(shape)].view(shape)
+
+        w = {"word": v(src, "embeddings.word_embeddings.weight", (c.vocab_size, H)),
+             "pos": v(src, "embeddings.position_embeddings.weight",
+                      (c.max_position_embeddings, H)),
+             "type0": v(src, "embeddings.token_type_embeddings.weight", (c.type_vocab_size, H))[0],
+             "ln_g": self.view("embeddings.LayerNorm.weight"),
+             "ln_b": self.view("embeddings.LayerNorm.bias"), "layers": []}
+        for l in range(c.num_hidden_layers):
+            p = f"encoder.layer.{l}."
+            lw = {"wqkv": v(src, p + "attention.self.query.weight", (3 * H, H)),
+                  "bqkv": v(f32, p + "attention.self.query.bias", (3 * H,)),
+                  "wo": v(src, p + "attention.output.dense.weight", (H, H)),
+                  "bo": self.view(p + "attention.output.dense.bias"),
+                  "ln1_g": self.view(p + "attention.output.LayerNorm.weight"),
+                  "ln1_b": self.view(p + "attention.output.LayerNorm.bias"),
+                  "w1": v(src, p + "intermediate.dense.weight", (I, H)),
+                  "b1": self.view(p + "intermediate.dense.bias"),
+                  "w2": v(src, p + "output.dense.weight", (H, I)),
+                  "b2": self.view(p + "output.dense.bias"),
+                  "ln2_g": self.view(p + "output.LayerNorm.weight"),
+                  "ln2_b": self.view(p + "output.LayerNorm.bias")}
+            if with_t:
+                if sT is not None:
+                    lw["wqkvT"] = sT[p + "attention.self.query.weight"]
+                    lw["woT"] = sT[p + "attention.output.dense.weight"]
+                    lw["w1T"] = sT[p + "intermediate.dense.weight"]
+                    lw["w2T"] = sT[p + "output.dense.weight"]
+                else:  # fp32: the KN operand layout directly (no transposed copies)
+                    lw["wqkvT"] = lw["woT"] = lw["w1T"] = lw["w2T"] = None
+            w["layers"].append(lw)
+        return w
+
+    # ---- compute ----
+    def flops_per_sequence(self, L: int) -> float:
+        c = self.config
+        H, I = c.hidden_size, c.intermediate_size
+        return c.num_hidden_layers * (2 * L * (4 * H * H + 2 * H * I) + 4 * L * L * H)
+
+    def _dx_gemm(self, dY, w, wT, **kw):
+        """dX = dY . W (W = nn.Linear weight [out, in]); big-tile path via W^T in bf16."""
+        if wT is not None:
+            return ops.gemm(dY, wT, **kw)
+        return ops.gemm(dY, w, b_is_nk=False, **kw)
+
+    def forward_compute(self, input_ids: torch.Tensor, attention_mask: torch.Tensor, save: bool):
+        """ids/mask [B, L] -> (emb [B, H] fp32 unit-norm, saved state or None)."""
+        c = self.config
+        ids = input_ids.to(torch.int64).contiguous()
+        mask = attention_mask.to(torch.int64).contiguous()
+        B, L = ids.shape
+        if L > c.max_position_embeddings:
+            raise ValueError(f"sequence length {L} > max_position_embeddings")
+        H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
+        dt = compute_dtype()
+        w = self._weights(dt, with_t=save)
+        x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
+        layers = []
+        for lw in w["layers"]:
+            qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
+            ctx = ops.attention(qkv, mask, B, L, H, heads)
+            s1 = ops.gemm(ctx, lw["wo"], bias=lw["bo"], residual=x, epilogue=ops.EPI_BIAS_RESID)
+            a = ops.layernorm(s1, lw["ln1_g"], lw["ln1_b"], eps, out=None if save else s1)
+            if save:
+                g, u = ops.gemm_gelu_save(a, lw["w1"], lw["b1"])
+            else:
+                g, u = ops.gemm(a, lw["w1"], bias=lw["b1"], epilogue=ops.EPI_BIAS_GELU), None
+            s2 = ops.gemm(g, lw["w2"], bias=lw["b2"], residual=a, epilogue=ops.EPI_BIAS_RESID)
+            y = ops.layernorm(s2, lw["ln2_g"], lw["ln2_b"], eps, out=None if save else s2)
+            if save:
+                layers.append((x, qkv, ctx, s1, a, u, g, s2))
+            x = y
+        m = ops.mean_rows(x, B, L, H)  # [B, H] fp32, PAD positions included
+        emb, nrm = ops.l2norm_fwd(m)
+        saved = (ids, mask, B, L, w, layers, emb, nrm) if save else None
+        return emb, saved
+
+    def backward_compute(self, saved, demb: torch.Tensor):
+        """Accumulate d(loss)/d(params) into self.flat_grad."""
+        ids, mask, B, L, w, layers, emb, nrm = saved
+        c = self.config
+        H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
+        g = self.flat_grad
+        dev = g.device
+        dm = ops.l2norm_bwd(demb.float().contiguous(), emb, nrm)  # [B, H] fp32
+        cur = torch.cuda.current_stream(dev)
+        side = side_stream(dev, "bert_wgrad")
+        dy, bcast = dm, L  # top layer: the mean-pool backward folded into LN2's
+        for l in range(c.num_hidden_layers - 1, -1, -1):
+            x, qkv, ctx, s1, a, u, gg, s2 = layers[l]
+            lw = w["layers"][l]
+            p = f"encoder.layer.{l}."
+            ds2 = ops.layernorm_bwd(dy, s2, lw["ln2_g"], self.view(p + "output.LayerNorm.weight", g),
+                                    self.view(p + "output.LayerNorm.bias", g), eps,
+                                    bcast_L=bcast, dy_scale=1.0 / L if bcast else 1.0)
+            bcast = 0
+            du = self._dx_gemm(ds2, lw["w2"], lw.get("w2T"), epilogue=ops.EPI_DGELU, residual=u)
+            self._wgrad(side, cur, ds2, gg, p + "output.dense")
+            da = self._dx_gemm(du, lw["w1"], lw.get("w1T"), epilogue=ops.EPI_RESID, residual=ds2)
+            self._wgrad(side, cur, du, a, p + "intermediate.dense")
+            ds1 = ops.layernorm_bwd(da, s1, lw["ln1_g"],
+                                    self.view(p + "attention.output.LayerNorm.weight", g),
+                                    self.view(p + "attention.output.LayerNorm.bias", g), eps)
+            dctx = self._dx_gemm(ds1, lw["wo"], lw.get("woT"))
+            self._wgrad(side, cur, ds1, ctx, p + "attention.output.dense")
+            dqkv = ops.attention_bwd(qkv, mask, ctx, dctx, B, L, H, heads)
+            self._wgrad(side, cur, dqkv, x, p + "attention.self.query")  # fused [3H, H]
+            dy = self._dx_gemm(dqkv, lw["wqkv"], lw.get("wqkvT"), epilogue=ops.EPI_RESID,
+                               residual=ds1)
+        # embeddings: LN backward on the rebuilt fp32 sum, then the table scatter
+        e = ops.embed_sum(ids, w["word"], w["pos"], w["type0"])
+        de = ops.layernorm_bwd(dy, e, w["ln_g"], self.view("embeddings.LayerNorm.weight", g),
+                               self.view("embeddings.LayerNorm.bias", g), eps)
+        ops.embed_bwd(de, ids, self.view("embeddings.word_embeddings.weight", g),
+                      self.view("embeddings.position_embeddings.weight", g),
+                      self.view("embeddings.token_type_embeddings.weight", g)[0],
+                      c.pad_token_id)
+        cur.wait_stream(side)
+
+    def _wgrad(self, side, cur, dY, X, prefix):
+        """dW += dY^T X and db += colsum(dY) on the side stream (overlaps the dX
+        chain, which is the critical path)."""
+        g = self.flat_grad
+        wname, bname = prefix + ".weight", prefix + ".bias"
+        out_n, in_n = dY.shape[1], X.shape[1]
+        ow, ob = self.offsets[wname], self.offsets[bname]
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            ops.gemm(dY, X, trans_a=True, b_is_nk=False, accumulate=True,
+                     out=g.detach()[ow:ow + out_n * in_n].view(out_n, in_n),
+                     out_dtype=torch.float32)
+            ops.colsum(dY, out=g.detach()[ob:ob + out_n], accumulate=True)
+        dY.record_stream(side)
+        X.record_stream(side)
+
+    def encode(self, input_ids, attention_mask):
+        """last_hidden_state-free embedding path (no grad): [B, H] unit-norm."""
+        with torch.no_grad():
+            emb, _ = self.forward_compute(input_ids, attention_mask, save=False)
+        return emb
+
+
+class _EncodeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, mask, flat, enc):
+        emb, saved = enc.forward_compute(ids, mask, save=True)
+        ctx.enc = enc
+        ctx.saved = saved
+        return emb
+
+    @staticmethod
+    def backward(ctx, demb):
+        ctx.enc.backward_compute(ctx.saved, demb)
+        ctx.saved = None
+        return None, None, None, None
+
+
+def seq2vec_ids(enc: BertEncoder, input_ids, attention_mask, grad: bool) -> torch.Tensor:
+    """normalize(mean_L(BERT(ids))) with grads accumulated into enc.flat_grad."""
+    if grad and torch.is_grad_enabled():
+        return _EncodeFn.apply(input_ids, attention_mask, enc.flat, enc)
+    return enc.encode(input_ids, attention_mask)
+
+
+def clone_encoder(enc: BertEncoder) -> BertEncoder:
+    k = copy.deepcopy(enc)
+    k.invalidate_shadow()
+    return k

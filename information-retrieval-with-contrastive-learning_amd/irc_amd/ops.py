@@ -353,3 +353,93 @@ def colsum(x, out=None, accumulate=False):
     _lib.call("irc_colsum", _code(x), ptr(x), ptr(out), R, C, x.stride(0), 1 if accumulate else 0,
               ptr(partial), stream_ptr(x.device))
     return out
+
+
+# ---------------------------------------------------------------- encoder backward
+EPI_DGELU, EPI_BIAS_GELU_SAVE = 5, 6
+
+
+def gemm_gelu_save(a, b, bias, out=None, pre=None):
+    """(gelu(a @ b.T + bias), a @ b.T + bias): FFN1 forward that also keeps the
+    pre-activation for the GELU backward (epilogue 6 writes both)."""
+    require_hip(a, b, bias)
+    M, N = a.shape[0], b.shape[0]
+    out = torch.empty((M, N), dtype=a.dtype, device=a.device) if out is None else out
+    pre = torch.empty_like(out) if pre is None else pre
+    return gemm(a, b, bias=bias, epilogue=EPI_BIAS_GELU_SAVE, residual=pre, out=out), pre
+
+
+def layernorm_bwd(dy, x, gamma, dgamma, dbeta, eps=1e-12, bcast_L=0, dy_scale=1.0,
+                  accumulate=True, out_dtype=None):
+    """dL/dx of y = LN(x) * gamma + beta (statistics recomputed from x); dgamma /
+    dbeta (+)= their deterministic column sums.  With bcast_L > 0, dy is [rows /
+    bcast_L, H] and row r of the gradient is dy[r // bcast_L] * dy_scale."""
+    require_hip(dy, x, gamma, dgamma, dbeta)
+    H = x.shape[-1]
+    rows = x.numel() // H
+    dx = torch.empty((rows, H), dtype=out_dtype or x.dtype, device=x.device)
+    if dx.dtype != x.dtype:
+        raise TypeError("layernorm_bwd: dx dtype must match x")
+    nws = int(_lib.load().irc_layernorm_bwd_workspace(rows, H))
+    ws = torch.empty((nws,), dtype=F32, device=x.device)
+    _lib.call("irc_layernorm_bwd", _code(x), _code(dy), ptr(dy), ptr(x), ptr(gamma), ptr(dx),
+              ptr(dgamma), ptr(dbeta), ptr(ws), nws, rows, H, float(eps), int(bcast_L),
+              float(dy_scale), 1 if accumulate else 0, stream_ptr(x.device))
+    return dx
+
+
+def attention_bwd(qkv, mask, ctx, dctx, B, L, H, heads):
+    """dqkv [B*L, 3H] of the fused-QKV masked self-attention (P recomputed)."""
+    require_hip(qkv, mask, ctx, dctx)
+    dqkv = torch.empty_like(qkv)
+    _lib.call("irc_attention_bwd", _code(qkv), ptr(qkv), ptr(mask), ptr(ctx), ptr(dctx),
+              ptr(dqkv), B, L, H, heads, stream_ptr(qkv.device))
+    return dqkv
+
+
+def embed_sum(ids, word, pos, type0):
+    """fp32 [B*L, H] = word[ids] + type0 + pos[l]: the embedding-LN input, rebuilt
+    for its backward (the forward fuses it into irc_embed_ln)."""
+    require_hip(ids, word, pos, type0)
+    B, L = ids.shape
+    H = word.shape[1]
+    y = torch.empty((B * L, H), dtype=F32, device=word.device)
+    _lib.call("irc_embed_sum", _code(word), ptr(ids), ptr(word), ptr(pos), ptr(type0), ptr(y),
+              B * L, L, H, stream_ptr(word.device))
+    return y
+
+
+def embed_bwd(dx, ids, dword, dpos, dtype0, pad_id):
+    require_hip(dx, ids, dword, dpos, dtype0)
+    B, L = ids.shape
+    H = dx.shape[-1]
+    ws = torch.empty((L * H,), dtype=F32, device=dx.device)
+    _lib.call("irc_embed_bwd", _code(dx), ptr(dx), ptr(ids), ptr(dword), ptr(dpos), ptr(dtype0),
+              ptr(ws), L * H, B, L, H, int(pad_id), stream_ptr(dx.device))
+
+
+def adam_step_bf16(p, g, m, v, coef, b1, b2, step_size, bc2_sqrt, eps, shadow):
+    require_hip(p, g, m, v, coef, shadow)
+    _lib.call("irc_adam_step_bf16", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(coef),
+              float(b1), float(b2), float(step_size), float(bc2_sqrt), float(eps), ptr(shadow),
+              stream_ptr(p.device))
+
+
+def momentum_update_bf16(pk, pq, mom, shadow):
+    require_hip(pk, pq, shadow)
+    _lib.call("irc_momentum_update_bf16", ptr(pk), ptr(pq), pk.numel(), float(mom), ptr(shadow),
+              stream_ptr(pk.device))
+
+
+def cast_bf16_t_into(x, y):
+    """y bf16 [C, R] (a view is fine if contiguous) <- transpose of x fp32 [R, C]."""
+    require_hip(x, y)
+    R, C = x.shape
+    _lib.call("irc_cast_bf16_t", ptr(x), ptr(y), R, C, stream_ptr(x.device))
+    return y
+
+
+def cast_bf16_into(x, y):
+    require_hip(x, y)
+    _lib.call("irc_cast_bf16", ptr(x), ptr(y), x.numel(), stream_ptr(x.device))
+    return y

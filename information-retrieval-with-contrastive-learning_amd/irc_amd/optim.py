@@ -55,8 +55,19 @@ class FusedAdam:
         t = self.step_count
         bc1 = 1 - self.b1 ** t
         bc2 = 1 - self.b2 ** t
-        ops.adam_step(self.head.flat.detach(), g, m, v, coef if max_norm is not None else None,
-                      self.b1, self.b2, self.lr / bc1, math.sqrt(bc2), self.eps)
+        shadow = self.head.shadow_buffer() if hasattr(self.head, "shadow_buffer") else None
+        if shadow is not None:
+            # trainable encoder: the bf16 MFMA-operand shadow is rewritten in the same pass
+            ops.adam_step_bf16(self.head.flat.detach(), g, m, v,
+                               coef if max_norm is not None else None, self.b1, self.b2,
+                               self.lr / bc1, math.sqrt(bc2), self.eps, shadow)
+            self.head.after_update(True)
+        else:
+            ops.adam_step(self.head.flat.detach(), g, m, v,
+                          coef if max_norm is not None else None, self.b1, self.b2,
+                          self.lr / bc1, math.sqrt(bc2), self.eps)
+            if hasattr(self.head, "after_update"):
+                self.head.after_update(False)
         return coef
 
     def step(self):
@@ -73,7 +84,7 @@ class FusedAdam:
                 "param_groups": [{"lr": self.lr, "betas": (self.b1, self.b2), "eps": self.eps,
                                   "weight_decay": 0, "amsgrad": False, "params": [0]}]}
 
-    def load_state_dict(self, sd):
+    def load_state_dict(self, sd):  # noqa: C901
         """Accepts this class's dict, or a reference torch.optim.Adam dict whose
         parameter indices 0..n-1 are encoder_q's parameters in nn.LSTM order."""
         m, v = self._moments()

@@ -13,6 +13,12 @@ are ignored in favour of loss_config (contrastive_module.py:12-13).
 Extension (superset): the BERT source/config/tokenizer come from the optional
 ``bert`` section of config.yaml; offline, a preset name builds the architecture
 with seeded random weights instead of fetching 'bert-base-uncased'.
+
+``--model BERT`` (the north star's trainable encoder, irc_amd.bert_train): the
+base encoder IS the BERT, run on the jointly tokenised/padded batch (the same
+tokenisation as bert_extract), so there is no separate frozen ``bert_model``
+(None); emb = normalize(mean_L(BERT(ids))) with D = hidden size; encoder_k is its
+momentum copy, and the loss / queue / enqueue tail is shared with the LSTM path.
 """
 import copy
 
@@ -23,6 +29,7 @@ from irc_amd import ops
 from irc_amd._torch import side_stream
 from irc_amd.dist import gather_rows
 from irc_amd.bert import BertModel
+from irc_amd.bert_train import BertEncoder, seq2vec_ids
 from irc_amd.lstm_head import LSTMHead, seq2vec as head_seq2vec
 from irc_amd.tokenizer import load_tokenizer
 
@@ -43,6 +50,8 @@ class RetrievalModelWrapper(nn.Module):
             with torch.no_grad():
                 self.encoder_k.flat.copy_(self.encoder_q.flat)
             self.encoder_k.flat.requires_grad_(False)
+            if hasattr(self.encoder_k, "invalidate_shadow"):
+                self.encoder_k.invalidate_shadow()
 
         if self.use_queue:
             self.register_buffer("queue", torch.randn(self.loss_config["dim"],
@@ -53,10 +62,15 @@ class RetrievalModelWrapper(nn.Module):
 
         bc = dict(bert_config or {})
         name = bc.get("name", "bert-base-uncased")
-        self.bert_model = BertModel.from_pretrained(name, config=bc.get("config"),
-                                                    seed=int(bc.get("seed", 0)))
-        self.bert_tokenizer = load_tokenizer(bc.get("vocab"), self.bert_model.config.vocab_size)
-        self.bert_model.eval()
+        if use_LSTM:
+            self.bert_model = BertModel.from_pretrained(name, config=bc.get("config"),
+                                                        seed=int(bc.get("seed", 0)))
+            self.bert_model.eval()
+            vocab_size = self.bert_model.config.vocab_size
+        else:  # --model BERT: the trainable encoder is the BERT
+            self.bert_model = None
+            vocab_size = self.encoder_q.config.vocab_size
+        self.bert_tokenizer = load_tokenizer(bc.get("vocab"), vocab_size)
         # data-parallel group for global in-batch negatives (None: single process)
         self.dist_group = None
 
@@ -75,9 +89,19 @@ class RetrievalModelWrapper(nn.Module):
 
     @torch.no_grad()
     def _momentum_update_key_encoder(self):
-        """theta_k <- m theta_k + (1 - m) theta_q: one fused launch over the flat buffers."""
-        ops.momentum_update(self.encoder_k.flat.detach(), self.encoder_q.flat.detach(),
-                            float(self.loss_config["momentum"]))
+        """theta_k <- m theta_k + (1 - m) theta_q: one fused launch over the flat buffers
+        (for the trainable BERT also rewriting encoder_k's bf16 operand shadow)."""
+        mom = float(self.loss_config["momentum"])
+        shadow = self.encoder_k.shadow_buffer() if hasattr(self.encoder_k, "shadow_buffer") \
+            else None
+        if shadow is not None:
+            ops.momentum_update_bf16(self.encoder_k.flat.detach(), self.encoder_q.flat.detach(),
+                                     mom, shadow)
+            self.encoder_k.after_update(True)
+        else:
+            ops.momentum_update(self.encoder_k.flat.detach(), self.encoder_q.flat.detach(), mom)
+            if hasattr(self.encoder_k, "after_update"):
+                self.encoder_k.after_update(False)
 
     @torch.no_grad()
     def _dequeue_and_enqueue(self, keys):
@@ -85,11 +109,39 @@ class RetrievalModelWrapper(nn.Module):
         if self.loss_config["queue_size"] % batch_size == 0:  # reference rule (:59)
             ops.enqueue(self.queue, keys.float().contiguous(), self.queue_ptr)
 
+    def tokenize(self, texts, device):
+        t = self.bert_tokenizer(list(texts), padding=True, truncation=True, return_tensors="pt")
+        return t["input_ids"].to(device), t["attention_mask"].to(device)
+
     def forward(self, anchor_sample, positive_sample, device, cluster_result=None, indexes=None):
         if indexes is not None:
             indexes = indexes.view(-1)
+        if not self.use_LSTM:  # --model BERT: joint tokenisation as bert_extract, then encode
+            ids, mask = self.tokenize(list(anchor_sample) + list(positive_sample), device)
+            return self.forward_ids(ids, mask, len(anchor_sample), cluster_result, indexes)
         anchor_sample, positive_sample = self.bert_extract(anchor_sample, positive_sample, device)
         return self.forward_features(anchor_sample, positive_sample, cluster_result, indexes)
+
+    def forward_ids(self, input_ids, attention_mask, n_anchor, cluster_result=None, indexes=None):
+        """--model BERT forward from a jointly padded token batch (anchors first)."""
+        qi, qm = input_ids[:n_anchor], attention_mask[:n_anchor]
+        ki, km = input_ids[n_anchor:], attention_mask[n_anchor:]
+        if self.use_momentum and input_ids.is_cuda:
+            cur = torch.cuda.current_stream(input_ids.device)
+            side = side_stream(input_ids.device, "key_encoder")
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                emb_k = seq2vec_ids(self.encoder_k, ki, km, grad=False)
+            input_ids.record_stream(side)
+            attention_mask.record_stream(side)
+            emb_q = seq2vec_ids(self.encoder_q, qi, qm, grad=True)
+            cur.wait_stream(side)
+            emb_k.record_stream(cur)
+        else:
+            emb_q = seq2vec_ids(self.encoder_q, qi, qm, grad=True)
+            enc = self.encoder_k if self.use_momentum else self.encoder_q
+            emb_k = seq2vec_ids(enc, ki, km, grad=not self.use_momentum)
+        return self._loss_tail(emb_q, emb_k, cluster_result, indexes)
 
     def forward_features(self, anchor_feat, positive_feat, cluster_result=None, indexes=None):
         """forward() from BERT features on: heads, loss, enqueue."""
@@ -109,6 +161,10 @@ class RetrievalModelWrapper(nn.Module):
             emb_q = self.seq2vec(anchor_feat)
             emb_k = self.seq2vec(positive_feat, query=False) if self.use_momentum else \
                 self.seq2vec(positive_feat)
+        return self._loss_tail(emb_q, emb_k, cluster_result, indexes)
+
+    def _loss_tail(self, emb_q, emb_k, cluster_result, indexes):
+        """contrastive_module.py:85-92: (global negatives,) loss, enqueue."""
         group = getattr(self, "dist_group", None)
         if group is not None:  # global in-batch negatives (irc_amd.dist)
             emb_q = gather_rows(emb_q, group)
@@ -120,8 +176,10 @@ class RetrievalModelWrapper(nn.Module):
         return loss
 
     def ctx2vec(self, context, device):
-        t = self.bert_tokenizer(list(context), padding=True, truncation=True, return_tensors="pt")
-        out = self.bert_model.encode(t["input_ids"].to(device), t["attention_mask"].to(device))
+        ids, mask = self.tokenize(context, device)
+        if not self.use_LSTM:
+            return seq2vec_ids(self.encoder_q, ids, mask, grad=True)
+        out = self.bert_model.encode(ids, mask)
         return self.seq2vec(out)
 
     def seq2vec(self, seq, query=True):
@@ -131,4 +189,4 @@ class RetrievalModelWrapper(nn.Module):
         return head_seq2vec(self.encoder_k, seq, grad=False)
 
 
-__all__ = ["RetrievalModelWrapper", "LSTMHead"]
+__all__ = ["RetrievalModelWrapper", "LSTMHead", "BertEncoder"]

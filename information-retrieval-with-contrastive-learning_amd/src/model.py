@@ -8,6 +8,7 @@
 """
 import torch
 
+from irc_amd.bert_train import BertEncoder
 from irc_amd.lstm_head import LSTMHead
 from irc_amd.optim import FusedAdam
 from src.contrastor.contrastive_loss import NCELoss
@@ -16,6 +17,17 @@ from src.contrastor.contrastive_module import RetrievalModelWrapper
 
 class LSTM(LSTMHead):
     """nn.LSTM(input, hidden, layers, batch_first, bidirectional) + Linear + Identity."""
+
+
+class BERT(BertEncoder):
+    """``--model BERT``: the trainable BERT bi-encoder (mean-pool, D = hidden size).
+    Architecture from config ``model.BERT`` ({name: preset, config: {...}, seed}) or,
+    failing that, the ``bert`` section; bert-base-uncased by default."""
+
+    def __init__(self, config, **kwargs):
+        c = dict((config.get("model") or {}).get("BERT") or config.get("bert") or {})
+        super().__init__(c.get("config"), name=c.get("name", "bert-base-uncased"),
+                         seed=int(c.get("seed", 0)))
 
 
 def get_optimizer(args, model):
@@ -29,13 +41,18 @@ def get_optimizer(args, model):
 def build_model(args):
     print("[Runner] - Building contrastive model")
     loss_config = args.config["loss"][f"{args.loss}"]
-    loss_config["dim"] = args.config["model"]["LSTM"]["output_size"]
+    if args.model == "LSTM":
+        bk_model = LSTM(args.config)
+        loss_config["dim"] = args.config["model"]["LSTM"]["output_size"]
+    elif args.model == "BERT":
+        bk_model = BERT(args.config)
+        loss_config["dim"] = bk_model.config.hidden_size
+    else:
+        raise ValueError(f"unknown model {args.model!r} (LSTM or BERT)")
     if args.loss in ["InfoNCE", "ProtoNCE", "HProtoNCE"]:
         criterion = NCELoss(loss_config)
-    if args.model != "LSTM":
-        raise ValueError(f"unknown model {args.model!r}")
-    bk_model = LSTM(args.config)
-    return RetrievalModelWrapper(bk_model, criterion, loss_config, use_LSTM=True,
+    use_LSTM = isinstance(bk_model, LSTM)
+    return RetrievalModelWrapper(bk_model, criterion, loss_config, use_LSTM=use_LSTM,
                                  bert_config=args.config.get("bert"))
 
 

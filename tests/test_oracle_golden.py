@@ -65,6 +65,21 @@ def test_bert_forward():
     np.testing.assert_allclose(out, g["last_hidden_state"], rtol=1e-4, atol=1e-4)
 
 
+def test_bert_ref_matches_golden():
+    """The torch fp32 BERT used as the trainable encoder's gradient reference
+    (tests/bert_ref.py) reproduces the reference's own HF last_hidden_state."""
+    import torch
+
+    from bert_ref import bert_hidden
+
+    g = load_golden("bert_tiny.npz")
+    P = {k[2:]: torch.from_numpy(v).float() for k, v in g.items() if k.startswith("w_")}
+    vocab, hid, nl, nh, inter, maxpos = (int(x) for x in g["cfg"])
+    out = bert_hidden(P, torch.from_numpy(g["input_ids"]).long(),
+                      torch.from_numpy(g["attention_mask"]).long(), nl, nh)
+    np.testing.assert_allclose(out.numpy(), g["last_hidden_state"], rtol=1e-4, atol=1e-4)
+
+
 def test_scan_grid_matches_reference_closest_docs():
     g = load_golden("scan.npz")
     q = g["grid_q"].astype(np.float32) / 128
