@@ -178,6 +178,75 @@ def run_train(args, rank, world, dev):
     }
 
 
+def run_train_bert(args, rank, world, dev):
+    """--model BERT (the north star's trainable encoder): BERT-base fwd+bwd on the
+    256 anchors, momentum-encoder fwd on the 256 positives, InfoNCE (D=768) with the
+    12544-key queue, clip + Adam (110M params, bf16 shadow refresh), momentum update."""
+    from irc_amd import _lib
+    from src.model import build_model, get_optimizer
+    from src.train import TrainState
+
+    lib = _lib.load()
+    cfg = c2_config()
+    ns = argparse.Namespace(config=cfg, loss="InfoNCE", model="BERT", opt="adam",
+                            sample="uniform")
+    torch.manual_seed(1337)
+    model = build_model(ns).to(dev).train()
+    model.add_queue_to_loss = True
+    opt = get_optimizer(ns, model)
+    st = TrainState(ns, model, opt)
+    if world > 1:
+        st.set_process_group(dist.group.WORLD)
+    ids, mask = synthetic_batch(2 * TRAIN_B, TRAIN_L, 1337 + rank)
+    ids, mask = ids.to(dev), mask.to(dev)
+
+    def step():
+        st.micro_batch(TRAIN_B, lambda: model.forward_ids(ids, mask, TRAIN_B), sync_loss=False)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    lib.irc_prof_reset()
+    lib.irc_prof_enable(1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    lib.irc_prof_enable(0)
+    dt = _max_over_ranks(dt, dev, world)
+    g_s, g_n, g_flops = _prof(lib, "gemm_bf16")
+    enc = model.encoder_q
+    D, K = enc.config.hidden_size, cfg["loss"]["InfoNCE"]["queue_size"]
+    loss_flops = 3 * (2 * (2 * TRAIN_B) ** 2 * D + 2 * TRAIN_B * D * K) / TRAIN_B
+    flops_pair = 4 * enc.flops_per_sequence(TRAIN_L) + loss_flops
+    pairs = TRAIN_B * args.steps * world
+    achieved = g_flops / g_s / 1e12 if g_s > 0 else None
+    loss = float(st.loss_record[-1]) if st.loss_record else None
+    step_tflops = pairs * flops_pair / dt / 1e12
+    return {
+        "pairs_per_s": pairs / dt,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "loss_last": loss,
+        "flops_per_pair": flops_pair,
+        "step_tflops": step_tflops,
+        "step_mfma_frac": step_tflops / BF16_PEAK_TFS,
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS,
+                     "unit": "TFLOP/s", "frac": achieved / BF16_PEAK_TFS if achieved else None,
+                     "traffic": _pmc_traffic("gemm_bf16_bert"),
+                     "kernel": "gemm kernels, bf16 operands (all GEMM launches of the timed "
+                               "steps: fwd, dX, dW)",
+                     "launches_per_step": g_n / args.steps,
+                     "gemm_ms_per_step": g_s * 1e3 / args.steps,
+                     "alg_flops_per_step": g_flops / args.steps},
+    }
+
+
 def _lstm_flops_per_pair(cfg):
     c = cfg["model"]["LSTM"]
     H, In, nl = c["hidden_size"], c["input_size"], c["num_layers"]
@@ -305,7 +374,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--part", default="all", choices=["all", "train", "scan"])
+    ap.add_argument("--part", default="all", choices=["all", "train", "scan", "bert"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
@@ -323,6 +392,9 @@ def main():
     model = None
     if args.part in ("all", "train"):
         model, train = run_train(args, rank, world, dev)
+    bert = None
+    if args.part in ("all", "bert"):
+        bert = run_train_bert(args, rank, world, dev)
     if args.part in ("all", "scan"):
         scan = run_scan(args, rank, world, dev)
     cpu_t = cpu_s = None
@@ -338,6 +410,10 @@ def main():
             head = {"value": train["pairs_per_s"], "unit": "pairs/s",
                     "ms_per_step": train["ms_per_step"], "roofline": train["roofline"],
                     "cpu_baseline": cpu_t}
+        elif bert is not None:
+            head = {"value": bert["pairs_per_s"], "unit": "pairs/s",
+                    "ms_per_step": bert["ms_per_step"], "roofline": bert["roofline"],
+                    "cpu_baseline": None}
         else:
             head = {"value": scan["value"], "unit": "queries/s",
                     "ms_per_step": scan["ms_per_batch"], "roofline": scan["roofline"],
@@ -359,6 +435,8 @@ def main():
         if train is not None:
             line["train"] = {k: train[k] for k in ("pairs_per_s", "ms_per_step", "step_tflops",
                                                    "flops_per_pair", "loss_last")}
+        if bert is not None:
+            line["train_bert"] = bert
         if scan is not None:
             line["retrieval"] = scan
         print(json.dumps(line), flush=True)

@@ -246,6 +246,15 @@ int irc_axpby(float* out, const float* x, const float* y, float a, float b, int6
 int irc_colsum(int dtype, const void* x, float* out, int64_t R, int64_t C, int64_t ldx,
                int accumulate, float* partial, irc_stream_t stream);
 
+/* Batched column sums: out[b * so + c] (+)= sum_r x[b * sx + r * ldx + c] for b < batch
+ * (dtype 0 bf16 / 1 fp32 rows, 16-byte aligned) -- the per-layer bias gradients of
+ * the trainable encoder's layer-batched weight-gradient pass; deterministic
+ * (fixed-order two-pass).  partial: irc_colsum_batched_workspace floats. */
+int64_t irc_colsum_batched_workspace(int64_t batch, int64_t R, int64_t C);
+int irc_colsum_batched(int dtype, const void* x, int64_t batch, int64_t R, int64_t C, int64_t ldx,
+                       int64_t sx, float* out, int64_t so, int accumulate, float* partial,
+                       int64_t partial_floats, irc_stream_t stream);
+
 /* ------------------------------------------------------------------ profiling
  * HIP-event timing of the dominant kernel of each entry point, recorded on the
  * caller's stream (bench.py's roofline "achieved" figure), with the launches'

@@ -254,14 +254,27 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const TD* __restrict__ 
     partial[(int64_t)blockIdx.x * 2 * H + c] = sred[c];
 }
 
-// dgamma[c] (+)= sum_blk partial[blk][c]; dbeta[c] (+)= sum_blk partial[blk][H + c]
-__global__ void ln_bwd_final_kernel(const float* __restrict__ partial, int nblk, int H,
+// Two-stage fixed-order reduction of the per-block partials [nblk][2H]:
+// stage 1: partial2[j][c] = sum of rows j*per .. j*per+per-1 (grid (2H/256, S));
+// stage 2: dgamma[c] / dbeta[c] (+)= sum_j partial2[j][c] (j ascending).
+constexpr int LNF_S = 32;
+__global__ void ln_bwd_stage1_kernel(const float* __restrict__ partial, int nblk, int H, int per,
+                                     float* __restrict__ partial2) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * H) return;
+  const int b0 = blockIdx.y * per, b1 = min(nblk, b0 + per);
+  float s = 0.f;
+  for (int b = b0; b < b1; ++b) s += partial[(int64_t)b * 2 * H + c];
+  partial2[(int64_t)blockIdx.y * 2 * H + c] = s;
+}
+
+__global__ void ln_bwd_final_kernel(const float* __restrict__ partial2, int ns, int H,
                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
                                     int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= 2 * H) return;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partial[(int64_t)b * 2 * H + c];
+  for (int j = 0; j < ns; ++j) s += partial2[(int64_t)j * 2 * H + c];
   float* out = c < H ? dgamma + c : dbeta + (c - H);
   *out = accumulate ? *out + s : s;
 }
@@ -663,7 +676,7 @@ static unsigned nblocks(int64_t n, int per) { return (unsigned)((n + per - 1) / 
 // Enough for either kernel (the generic one takes fewer rows per block).
 extern "C" int64_t irc_layernorm_bwd_workspace(int64_t rows, int64_t H) {
   const int64_t nb = (rows + encb::LNB_ROWS - 1) / encb::LNB_ROWS;
-  return (nb > 0 ? nb : 1) * 2 * H;
+  return ((nb > 0 ? nb : 1) + encb::LNF_S) * 2 * H;  // block partials + stage-1 partials
 }
 
 extern "C" int irc_layernorm_bwd(int dtype, int dy_dtype, const void* dy, const void* x,
@@ -683,7 +696,7 @@ extern "C" int irc_layernorm_bwd(int dtype, int dy_dtype, const void* dy, const 
   const bool vec = dtype == 0 && al && (H == 512 || H == 768 || H == 1024);
   const int per = vec ? encb::LNV_ROWS : encb::LNB_ROWS;
   const int64_t nb = (rows + per - 1) / per;
-  const int64_t need = (int64_t)nb * 2 * H;
+  const int64_t need = ((int64_t)nb + encb::LNF_S) * 2 * H;
   IRC_REQUIRE(partial != nullptr && partial_floats >= need,
               "layernorm_bwd: workspace %lld < %lld floats", (long long)partial_floats,
               (long long)need);
@@ -728,8 +741,13 @@ extern "C" int irc_layernorm_bwd(int dtype, int dy_dtype, const void* dy, const 
   }
   int rc = check_launch("layernorm_bwd");
   if (rc) return rc;
+  const int per2 = (int)((nb + encb::LNF_S - 1) / encb::LNF_S);
+  const int ns = (int)((nb + per2 - 1) / per2);
+  float* partial2 = partial + nb * 2 * H;
+  hipLaunchKernelGGL(encb::ln_bwd_stage1_kernel, dim3(nblocks(2 * H, 256), (unsigned)ns),
+                     dim3(256), 0, st, partial, (int)nb, (int)H, per2, partial2);
   hipLaunchKernelGGL(encb::ln_bwd_final_kernel, dim3(nblocks(2 * H, 256)), dim3(256), 0, st,
-                     partial, (int)nb, (int)H, dgamma, dbeta, accumulate);
+                     partial2, ns, (int)H, dgamma, dbeta, accumulate);
   prof_end("layernorm_bwd", st, (double)rows * H * (dtype == 0 ? 2.0 : 4.0) * 3.0);
   return check_launch("layernorm_bwd_final");
 }

@@ -22,7 +22,7 @@
 // along M/N and scattered into the [row][k] LDS image.  Blocks are remapped so
 // each XCD walks a contiguous band of output tiles (neighbours share A/B panels
 // in that XCD's L2).
-#include "irc_common.h"
+#include "gemm_pp.h"
 
 namespace irc {
 namespace gemm {
@@ -749,9 +749,22 @@ static int by_layout(int la, int lb, int epi, const Args& g, int batch, int spli
 
 using namespace irc;
 
+// IRC_GEMM_PP=0 disables the ping-pong path (A/B experiments; read once).
+static bool pp_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("IRC_GEMM_PP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M,
                                       int64_t N, int64_t K, int64_t batch) {
-  const int s = gemm::split_count(in_dtype == 0 ? 2 : 4, out_dtype == 1, epilogue, M, N, K, batch);
+  int s = gemm::split_count(in_dtype == 0 ? 2 : 4, out_dtype == 1, epilogue, M, N, K, batch);
+  if (in_dtype == 0 && pp_enabled()) {
+    const int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch);
+    if (sp > s) s = sp;
+  }
   return s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
 }
 
@@ -794,6 +807,29 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
                vec_c, 0, splits > 1 ? static_cast<float*>(workspace) : nullptr};
   hipStream_t st = as_stream(stream);
   const int nb = (int)batch;
+  if (in_dtype == 0 && pp_enabled()) {
+    int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch);
+    if (sp > 1 && (workspace == nullptr ||
+                   workspace_bytes < (int64_t)sp * M * N * batch * (int64_t)sizeof(float)))
+      sp = 1;
+    if (gpp::qualifies(a_layout, b_layout, M, N, K, A, lda, strideA, B, ldb, strideB, batch, sp)) {
+      gpp::PArgs pa{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B),
+                    C, bias, R, sp > 1 ? static_cast<float*>(workspace) : nullptr, (int)M, (int)N,
+                    (int)K, sp > 1 ? (int)(((K + sp - 1) / sp + 63) / 64 * 64) : (int)K,
+                    lda, ldb, ldc, ldr, strideA, strideB, strideC, strideR, strideBias, alpha,
+                    accumulate, vec_c};
+      prof_begin(st);
+      gpp::run(out_dtype == 1, a_layout, b_layout, epilogue, pa, batch, sp, st);
+      if (sp > 1) {
+        const int64_t n = M * N * batch;
+        hipLaunchKernelGGL(gemm::splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                           0, st, pa.P, static_cast<float*>(C), (int)M, (int)N, sp, ldc, strideC,
+                           nb, alpha, accumulate);
+      }
+      prof_end("gemm_bf16", st, 2.0 * M * N * K * batch);
+      return check_launch("gemm_pp_kernel");
+    }
+  }
   if (in_dtype == 0 && out_dtype == 0)
     return gemm::by_layout<unsigned short, unsigned short>(a_layout, b_layout, epilogue, g, nb,
                                                            1, st);

@@ -1,0 +1,30 @@
+// Host interface of the ping-pong bf16 GEMM (gemm_pp.hip), used by irc_gemm.
+#pragma once
+#include "irc_common.h"
+
+namespace irc {
+namespace gpp {
+
+struct PArgs {
+  const unsigned short* A;
+  const unsigned short* B;
+  void* C;
+  const float* bias;
+  const void* R;
+  float* P;  // split-K slabs [batch][split][M][N] or null
+  int M, N, K, kchunk;
+  int64_t lda, ldb, ldc, ldr;
+  int64_t sA, sB, sC, sR, sBias;
+  float alpha;
+  int accumulate;
+  int vec_c;
+};
+
+int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t batch);
+bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+               int64_t sA, const void* B, int64_t ldb, int64_t sB, int64_t batch, int splits);
+void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, int splits,
+         hipStream_t st);
+
+}  // namespace gpp
+}  // namespace irc

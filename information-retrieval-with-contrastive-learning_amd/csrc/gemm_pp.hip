@@ -1,0 +1,470 @@
+// Ping-pong 256x256x64 bf16 GEMM for gfx950 (the large-shape path of irc_gemm).
+//
+//   C[M, N] (=|+=) alpha * op(A) . op(B) (+ bias) (-> GELU / GELU' / residual)
+//
+// Used for every big bf16 GEMM of the path: the BERT forward projections
+// (contrastive_module.py:39 -> HF modeling_bert), the trainable encoder's dX and
+// dW products, the LSTM input projections (src/model.py:16-26) -- all four operand
+// layouts: A [M][K] or [K][M], B [N][K] or [K][N].
+//
+// Structure (cdna_hip_programming.md §5, "ping-pong" of two wave groups):
+//  * 8 waves = 2 groups of 4.  Group g owns output rows 128g..128g+127 of the
+//    block tile; wave (g, wn) a 128 x 64 sub-tile = 8 x 4 accumulators of
+//    v_mfma_f32_16x16x32_bf16 (128 VGPRs).
+//  * The K loop alternates two sections per 64-deep K-tile: L (read the tile's
+//    fragments from LDS into registers, issue the LDS-DMA of the NEXT tile's
+//    halves this group owns) and M (64 MFMAs from registers).  Group 1 starts one
+//    section late (an extra barrier), so at every moment one group runs MFMAs
+//    while the other reads LDS / issues DMA: each SIMD hosts one wave of each
+//    group and its matrix pipe alternates between them.
+//  * LDS: 2 K-tile buffers x {A rows 0-127, A rows 128-255, B cols 0-127,
+//    B cols 128-255} x 16-17 KB = 128-136 KB, filled by global_load_lds_dwordx4 (no
+//    VGPR staging).  Group g DMAs A half g and B half g.  Waits are per-group
+//    vmcnt(0) placed where that group's DMA has had a full section to land; all
+//    barriers are raw s_barrier (no vmcnt drain).
+//  * K-major tiles ([rows][64 k], 128-B rows) use the 16-B chunk XOR (row & 7),
+//    applied on the DMA SOURCE address (the DMA destination is lane-linear), and
+//    are read with ds_read_b128; K-outer tiles are stored column-chunk-major
+//    (8 columns x 64 k per 1-KB chunk, padded) and read with ds_read_b64_tr_b16
+//    (hardware transpose) at base + immediate addresses.
+//  * Epilogue through LDS (per wave, 32-row passes) -> 16-byte coalesced stores,
+//    fused bias / GELU / GELU' / residual / pre-activation save / fp32 accumulate,
+//    or raw fp32 split-K slabs reduced afterwards in a fixed order.
+#include "gemm_pp.h"
+
+namespace irc {
+namespace gemm {
+// shared with gemm.hip
+enum Epi {
+  EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RESID = 3, EPI_RESID = 4,
+  EPI_DGELU = 5, EPI_BIAS_GELU_SAVE = 6
+};
+}  // namespace gemm
+
+namespace gpp {
+using namespace irc::gemm;
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+// K-outer half-tile image: 16 blocks of 4 k-rows, each block = [16 column chunks]
+// [4 k-rows][16 B] (1 KB) + a 64-B pad (BPITCH).  One DMA wave-instruction fills
+// one block from 4 whole 256-B k-rows of global memory; a fragment's transpose
+// reads sit at base + immediate offsets (+128 B per 16 columns, +BPITCH per 4
+// k-rows), and the two 16-lane groups of a 32-lane half (k-rows 8 apart = 2
+// blocks apart) land on disjoint bank halves thanks to the pad.  K-major images
+// are 128 rows x 128 B.
+constexpr int BPITCH = 1024 + 64;
+// half-tile slot bytes of a K-major / K-outer operand; one K-tile = A0 A1 B0 B1
+constexpr int slot_bytes(bool kmajor) { return kmajor ? 16384 : 16 * BPITCH; }
+constexpr int buf_bytes(bool ak, bool bk) { return 2 * slot_bytes(ak) + 2 * slot_bytes(bk); }
+constexpr int LDS_BYTES = 2 * buf_bytes(false, false);  // 136 KB (allocation for all variants)
+constexpr int EP_PITCH = 68;          // epilogue staging row pitch (floats)
+
+__device__ __forceinline__ float gelu_f(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * az);
+  float p = 1.061405429f;
+  p = p * t - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const float e = 1.0f - p * t * __expf(-az * az);
+  return 0.5f * x * (1.0f + copysignf(e, z));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float z = x * 0.70710678118654752f;
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * az);
+  float p = 1.061405429f;
+  p = p * t - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const float ez = __expf(-az * az);
+  const float e = 1.0f - p * t * ez;
+  return 0.5f * (1.0f + copysignf(e, z)) + x * 0.3989422804014327f * ez;
+}
+
+__device__ __forceinline__ bool has_bias(int e) {
+  return e == EPI_BIAS || e == EPI_BIAS_GELU || e == EPI_BIAS_RESID || e == EPI_BIAS_GELU_SAVE;
+}
+
+// DMA one half-tile (128 rows/cols x 64 k) of operand X into `img`, by the 256
+// threads (4 waves, wave index wq) of one group: 4 wave-instructions each.
+//  KMAJOR: X[r][k] (row stride ld) rows r0..r0+127 (clamped to < nrows), k0..k0+63.
+//  else:   X[k][c] (row stride ld) k-rows k0..k0+63, columns c0..c0+127 in 16-B
+//          chunks, 4 whole k-rows per wave-instruction (chunks past ncols clamped
+//          to the last whole chunk; never stored).
+template <bool KMAJOR>
+__device__ __forceinline__ void stage_half(const unsigned short* __restrict__ X, int64_t ld,
+                                           int r0, int nrows, int k0, char* img, int wq,
+                                           int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = (i * 4 + wq) * 64 + lane;  // 16-B LDS chunk index (lane-linear)
+    if constexpr (KMAJOR) {
+      const int row = p >> 3;
+      const int c = (p & 7) ^ (row & 7);
+      int gr = r0 + row;
+      gr = gr < nrows ? gr : nrows - 1;
+      glds16(X + (int64_t)gr * ld + k0 + c * 8, img + (i * 4 + wq) * 1024);
+    } else {
+      const int blk = i * 4 + wq;  // 4 k-rows; lane -> (chunk lane >> 2, k-row lane & 3)
+      int gc = r0 + (lane >> 2) * 8;
+      gc = gc + 8 <= nrows ? gc : nrows - 8;
+      glds16(X + (int64_t)(k0 + 4 * blk + (lane & 3)) * ld + gc, img + blk * BPITCH);
+    }
+  }
+}
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4s ds_tr16(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+// 16x16x32 operand fragment: lane l gets X[row0 + (l & 15)][32 s + 8 (l >> 4) + j], j < 8.
+template <bool KMAJOR>
+__device__ __forceinline__ bf16x8 frag(const char* img, int row0, int s, int lane) {
+  if constexpr (KMAJOR) {
+    const int row = row0 + (lane & 15);
+    const int c = 4 * s + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * (c ^ (row & 7)));
+  } else {
+    // 16-lane group q reads k-rows 32s+8q+{0..3} then +{4..7}; lane 4a+b of the
+    // group addresses row a, columns row0 + 4b .. +3
+    const int q = lane >> 4, a = (lane >> 2) & 3, b = lane & 3;
+    const int col = row0 + 4 * b;
+    const char* p = img + (8 * s + 2 * q) * BPITCH + (col >> 3) * 64 + a * 16 + (col & 7) * 2;
+    const v4s lo = ds_tr16(p);            // k-rows 32s + 8q + a
+    const v4s hi = ds_tr16(p + BPITCH);   // k-rows 32s + 8q + 4 + a
+    const v4s both[2] = {lo, hi};
+    return __builtin_bit_cast(bf16x8, both);
+  }
+}
+
+template <bool AK, bool BK_, typename TO, int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
+  const int tiles_m = (g.M + BM - 1) / BM;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {  // XCD-aware bijective remap: blocks sharing an XCD walk consecutive tiles
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int batch = blockIdx.y;
+  const int kbeg = blockIdx.z * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const int nk = (kend - kbeg) / BK;
+  const unsigned short* A = g.A + batch * g.sA;
+  const unsigned short* B = g.B + batch * g.sB;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wave >> 2, wq = wave & 3;  // group = row half; wq = wave within group
+  const int wn = wq;                          // 64-column slab of the tile
+  const int bh = wn >> 1, bcol = 64 * (wn & 1);
+
+  // group g stages A rows/cols [128g, +128) and B rows/cols [128g, +128)
+  constexpr int SA = slot_bytes(AK), SB = slot_bytes(BK_), BUF = buf_bytes(AK, BK_);
+  auto stage = [&](int kt, int buf) {
+    char* base = lds + buf * BUF;
+    const int k0 = kbeg + kt * BK;
+    if constexpr (AK)
+      stage_half<true>(A, g.lda, m0 + 128 * grp, g.M, k0, base + grp * SA, wq, lane);
+    else
+      stage_half<false>(A, g.lda, m0 + 128 * grp, g.M, k0, base + grp * SA, wq, lane);
+    if constexpr (BK_)
+      stage_half<true>(B, g.ldb, n0 + 128 * grp, g.N, k0, base + 2 * SA + grp * SB, wq, lane);
+    else
+      stage_half<false>(B, g.ldb, n0 + 128 * grp, g.N, k0, base + 2 * SA + grp * SB, wq, lane);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)0.0f;
+
+  if (nk > 0) {
+    stage(0, 0);
+    wait_vmcnt<0>();
+    wg_barrier();
+    if (grp == 1) wg_barrier();  // group 1 runs one section behind
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      // ---- L section: next tile's DMA, this tile's fragments
+      if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+      const char* la = lds + cur * BUF + grp * SA;
+      const char* lb = lds + cur * BUF + 2 * SA + bh * SB;
+      bf16x8 fa[8][2], fb[4][2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j][s] = frag<BK_>(lb, bcol + 16 * j, s, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) fa[i][s] = frag<AK>(la, 16 * i, s, lane);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (grp == 1) wait_vmcnt<0>();  // group 0 reads this DMA in the next section
+      wg_barrier();
+      // ---- M section
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[i][j], 0,
+                                                                0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (grp == 0) wait_vmcnt<0>();
+      wg_barrier();
+    }
+    if (grp == 0) wg_barrier();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // acc[i][j] element e -> row 128 grp + 16 i + 4 (lane >> 4) + e, col 64 wn + 16 j + (lane & 15)
+  const int rbase0 = m0 + 128 * grp;
+  const int cbase = n0 + 64 * wn;
+  float* st = reinterpret_cast<float*>(lds) + wave * (32 * EP_PITCH);
+  const bool slab = g.P != nullptr;
+  if (slab || g.vec_c) {
+    const float* bias = g.bias ? g.bias + batch * g.sBias : nullptr;
+    float bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = cbase + 16 * j + (lane & 15);
+      bv[j] = (!slab && has_bias(EPI) && col < g.N) ? bias[col] : 0.f;
+    }
+    const float alpha = slab ? 1.f : g.alpha;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {  // 32-row passes
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rl = 16 * ii + 4 * (lane >> 4) + e;
+            float v = acc[2 * p + ii][j][e] * alpha + bv[j];
+            if (!slab && EPI == EPI_BIAS_GELU) v = gelu_f(v);
+            st[rl * EP_PITCH + 16 * j + (lane & 15)] = v;
+          }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const int rbase = rbase0 + 32 * p;
+      if (slab) {
+        float* P = g.P + ((int64_t)batch * gridDim.z + blockIdx.z) * g.M * g.N;
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int c = it * 64 + lane;
+          const int rl = c >> 4, c4 = (c & 15) * 4;
+          const int row = rbase + rl, col = cbase + c4;
+          if (row >= g.M || col >= g.N) continue;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(&st[rl * EP_PITCH + c4]);
+          if (col + 4 <= g.N && (g.N & 3) == 0) {
+            *reinterpret_cast<f32x4*>(P + (int64_t)row * g.N + col) = v;
+          } else {
+            for (int t = 0; t < 4 && col + t < g.N; ++t) P[(int64_t)row * g.N + col + t] = v[t];
+          }
+        }
+      } else if constexpr (sizeof(TO) == 2) {
+        const unsigned short* R = reinterpret_cast<const unsigned short*>(g.R) + batch * g.sR;
+        unsigned short* C = reinterpret_cast<unsigned short*>(g.C) + batch * g.sC;
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int c = it * 64 + lane;
+          const int rl = c >> 3, c8 = (c & 7) * 8;
+          const int row = rbase + rl, col = cbase + c8;
+          if (row >= g.M || col >= g.N) continue;
+          const f32x4 v0 = *reinterpret_cast<const f32x4*>(&st[rl * EP_PITCH + c8]);
+          const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * EP_PITCH + c8 + 4]);
+          float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
+            const u16x8 rr = *reinterpret_cast<const u16x8*>(R + (int64_t)row * g.ldr + col);
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+              v[t] = EPI == EPI_DGELU ? v[t] * gelu_grad_f(bf16_to_f32(rr[t]))
+                                      : v[t] + bf16_to_f32(rr[t]);
+          }
+          if (EPI == EPI_BIAS_GELU_SAVE) {
+            u16x8 pre;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              pre[t] = f32_to_bf16(v[t]);
+              v[t] = gelu_f(v[t]);
+            }
+            *reinterpret_cast<u16x8*>(const_cast<unsigned short*>(R) + (int64_t)row * g.ldr + col) =
+                pre;
+          }
+          u16x8 o;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) o[t] = f32_to_bf16(v[t]);
+          *reinterpret_cast<u16x8*>(C + (int64_t)row * g.ldc + col) = o;
+        }
+      } else {
+        const float* R = reinterpret_cast<const float*>(g.R) + batch * g.sR;
+        float* C = reinterpret_cast<float*>(g.C) + batch * g.sC;
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int c = it * 64 + lane;
+          const int rl = c >> 4, c4 = (c & 15) * 4;
+          const int row = rbase + rl, col = cbase + c4;
+          if (row >= g.M || col >= g.N) continue;
+          f32x4 v = *reinterpret_cast<const f32x4*>(&st[rl * EP_PITCH + c4]);
+          if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
+            const f32x4 r = *reinterpret_cast<const f32x4*>(R + (int64_t)row * g.ldr + col);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] = EPI == EPI_DGELU ? v[t] * gelu_grad_f(r[t]) : v[t] + r[t];
+          }
+          if (EPI == EPI_BIAS_GELU_SAVE) {
+            *reinterpret_cast<f32x4*>(const_cast<float*>(R) + (int64_t)row * g.ldr + col) = v;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) v[t] = gelu_f(v[t]);
+          }
+          float* dst = C + (int64_t)row * g.ldc + col;
+          if (g.accumulate) v += *reinterpret_cast<const f32x4*>(dst);
+          *reinterpret_cast<f32x4*>(dst) = v;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    return;
+  }
+  // scalar epilogue (unaligned C / R)
+  const float* bias = g.bias ? g.bias + batch * g.sBias : nullptr;
+  const TO* R = reinterpret_cast<const TO*>(g.R) + (g.R ? batch * g.sR : 0);
+  TO* C = reinterpret_cast<TO*>(g.C) + batch * g.sC;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = cbase + 16 * j + (lane & 15);
+    if (col >= g.N) continue;
+    const float bvv = has_bias(EPI) ? bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = rbase0 + 16 * i + 4 * (lane >> 4) + e;
+        if (row >= g.M) continue;
+        float v = acc[i][j][e] * g.alpha + bvv;
+        if (EPI == EPI_BIAS_GELU) v = gelu_f(v);
+        if (EPI == EPI_BIAS_GELU_SAVE) {
+          TO* pre = const_cast<TO*>(R) + (int64_t)row * g.ldr + col;
+          if constexpr (sizeof(TO) == 2)
+            *reinterpret_cast<unsigned short*>(pre) = f32_to_bf16(v);
+          else
+            *reinterpret_cast<float*>(pre) = v;
+          v = gelu_f(v);
+        }
+        if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
+          float r;
+          if constexpr (sizeof(TO) == 2)
+            r = bf16_to_f32(reinterpret_cast<const unsigned short*>(R)[(int64_t)row * g.ldr + col]);
+          else
+            r = reinterpret_cast<const float*>(R)[(int64_t)row * g.ldr + col];
+          v = EPI == EPI_DGELU ? v * gelu_grad_f(r) : v + r;
+        }
+        TO* dst = C + (int64_t)row * g.ldc + col;
+        if constexpr (sizeof(TO) == 2) {
+          *reinterpret_cast<unsigned short*>(dst) = f32_to_bf16(v);
+        } else {
+          if (g.accumulate)
+            *reinterpret_cast<float*>(dst) += v;
+          else
+            *reinterpret_cast<float*>(dst) = v;
+        }
+      }
+  }
+}
+
+}  // namespace gpp
+
+// ------------------------------------------------------------------ host side
+// Called from irc_gemm (gemm.hip) for bf16 inputs.  Returns -1 when the shape /
+// alignment does not qualify (the caller then uses the general 128x128 kernel).
+// la/lb: 0 = K-major (A [M][K] / B [N][K]), 1 = K-outer (A [K][M] / B [K][N]).
+namespace gpp {
+
+template <bool AK, bool BKM, typename TO>
+static void launch_epi(int epi, const PArgs& a, dim3 grid, hipStream_t st) {
+  switch (epi) {
+#define IRC_PP(E)                                                                           \
+  case E:                                                                                   \
+    hipLaunchKernelGGL((gemm_pp_kernel<AK, BKM, TO, E>), grid, dim3(NT), 0, st, a); \
+    break;
+    IRC_PP(0) IRC_PP(1) IRC_PP(2) IRC_PP(3) IRC_PP(4) IRC_PP(5) IRC_PP(6)
+#undef IRC_PP
+  }
+}
+
+template <typename TO>
+static void launch_layout(int la, int lb, int epi, const PArgs& a, dim3 grid, hipStream_t st) {
+  if (la == 0 && lb == 0) launch_epi<true, true, TO>(epi, a, grid, st);
+  else if (la == 0) launch_epi<true, false, TO>(epi, a, grid, st);
+  else if (lb == 0) launch_epi<false, true, TO>(epi, a, grid, st);
+  else launch_epi<false, false, TO>(epi, a, grid, st);
+}
+
+}  // namespace gpp
+}  // namespace irc
+
+namespace irc {
+namespace gpp {
+
+// Split count: fill (at most) one wave of 256 blocks when the output tile grid
+// alone cannot (fp32 C, no fused epilogue), each K slice >= 1024 deep.
+int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t batch) {
+  if (!out_f32 || epi != 0) return 1;
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * batch;
+  if (tiles >= 160) return 1;
+  int64_t s = 256 / tiles;           // one wave of blocks on 256 CUs
+  const int64_t smax = K / 1024;     // >= 16 K-tiles per slice
+  if (s > smax) s = smax;
+  if (s > 32) s = 32;
+  if (s < 2) return 1;
+  const int64_t chunk = ((K + s - 1) / s + 63) / 64 * 64;
+  return (int)((K + chunk - 1) / chunk);
+}
+
+// Does the ping-pong kernel take this bf16 GEMM?  la/lb: 0 = K-major, 1 = K-outer.
+bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+               int64_t sA, const void* B, int64_t ldb, int64_t sB, int64_t batch, int splits) {
+  if (K % 64 != 0 || K == 0) return false;
+  // both operands K-outer with a small output (split-K slab traffic dominates):
+  // the 128x128 kernel's smaller slabs are faster
+  if (la == 1 && lb == 1 && ((M + 255) / 256) * ((N + 255) / 256) * batch < 16) return false;
+  // Wave quantisation on 256 CUs: where the 256x384 big-tile kernel fills whole
+  // waves and 256x256 tiles do not (N = 768 / 2304 at M = 32768), it wins.
+  if (la == 0 && lb == 0 && N % 384 == 0) {
+    const int64_t t384 = ((M + 255) / 256) * (N / 384) * batch;
+    const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
+    if (t384 % 256 == 0 && t256 % 256 != 0) return false;
+  }
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16) return false;
+  if (lda % 8 || ldb % 8 || sA % 8 || sB % 8) return false;
+  if (la == 1 && M % 8) return false;
+  if (lb == 1 && N % 8) return false;
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  return tiles * batch * splits >= 32;
+}
+
+void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, int splits,
+         hipStream_t st) {
+  const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
+  const dim3 grid((unsigned)tiles, (unsigned)batch, (unsigned)splits);
+  if (splits > 1)  // raw fp32 slabs, no epilogue (reduced afterwards)
+    launch_layout<float>(la, lb, 0, a, grid, st);
+  else if (out_f32)
+    launch_layout<float>(la, lb, epi, a, grid, st);
+  else
+    launch_layout<unsigned short>(la, lb, epi, a, grid, st);
+}
+
+}  // namespace gpp
+}  // namespace irc

@@ -294,6 +294,81 @@ __global__ void colsum_partial_vec_kernel(const unsigned short* __restrict__ x,
   for (int t = 0; t < 8; ++t) p[t] = s[t];
 }
 
+// Batched column sums x[b][r][c] -> out[b * so + c] (the per-layer bias gradients of
+// the trainable encoder's deferred weight-gradient pass), deterministic:
+// stage 1: block (column group of 512 [bf16] / 256 [fp32], row chunk, batch), 4 waves
+// striding the chunk's rows, lanes owning 8 (bf16) or 4 (fp32) adjacent columns,
+// folded across waves in fixed order -> partial[b][chunk][c];
+// stage 2: out (+)= sum over chunks in order.
+constexpr int CSB_ROWS = 256;
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_b_stage1(const T* __restrict__ x, int64_t R, int C,
+                                                       int64_t ldx, int64_t sx,
+                                                       float* __restrict__ partial, int nch) {
+  constexpr int V = sizeof(T) == 2 ? 8 : 4;  // columns per lane (16 bytes)
+  __shared__ float red[4][64 * V];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.z, ch = blockIdx.y;
+  const int c0 = (blockIdx.x * 64 + lane) * V;
+  const bool ok = c0 < C;
+  const T* xb = x + (int64_t)b * sx;
+  const int64_t r0 = (int64_t)ch * CSB_ROWS;
+  const int64_t r1 = r0 + CSB_ROWS < R ? r0 + CSB_ROWS : R;
+  float acc[V];
+#pragma unroll
+  for (int t = 0; t < V; ++t) acc[t] = 0.f;
+  if (ok) {
+    int64_t r = r0 + wv;
+    for (; r + 12 < r1; r += 16) {  // 4 independent 16-byte loads in flight
+      if constexpr (sizeof(T) == 2) {
+        u16x8 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[q] = *reinterpret_cast<const u16x8*>(reinterpret_cast<const unsigned short*>(xb) +
+                                                 (r + 4 * q) * ldx + c0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc[t] += bf16_to_f32(v[q][t]);
+      } else {
+        f32x4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[q] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(xb) +
+                                                 (r + 4 * q) * ldx + c0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[t] += v[q][t];
+      }
+    }
+    for (; r < r1; r += 4) {
+#pragma unroll
+      for (int t = 0; t < V; ++t) acc[t] += ldf(xb, r * ldx + c0 + t);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < V; ++t) red[wv][lane * V + t] = acc[t];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * V; e += 256) {
+    const int c = blockIdx.x * 64 * V + e;
+    if (c < C)
+      partial[((int64_t)b * nch + ch) * C + c] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+  }
+}
+
+__global__ void colsum_b_stage2(const float* __restrict__ partial, int nch, int C,
+                                float* __restrict__ out, int64_t so, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (c >= C) return;
+  const float* p = partial + (int64_t)b * nch * C + c;
+  float s = 0.f;
+  for (int k = 0; k < nch; ++k) s += p[(int64_t)k * C];
+  float* o = out + b * so + c;
+  *o = accumulate ? *o + s : s;
+}
+
 // W [R][C] fp32 -> W^T [C][R] bf16 through 32x33 LDS tiles (the nn.Linear-layout
 // operand of GEMMs that consume W as [K][N]).
 __global__ void cast_bf16_t_kernel(const float* __restrict__ x, unsigned short* __restrict__ y,
@@ -523,4 +598,34 @@ extern "C" int irc_axpby(float* out, const float* x, const float* y, float a, fl
   hipLaunchKernelGGL(axpby_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), out, x, y, a, b,
                      n);
   return check_launch("axpby");
+}
+
+extern "C" int64_t irc_colsum_batched_workspace(int64_t batch, int64_t R, int64_t C) {
+  return batch * ((R + CSB_ROWS - 1) / CSB_ROWS) * C;
+}
+
+// out[b * so + c] (+)= sum_r x[b * sx + r * ldx + c]; partial: the workspace above (floats).
+extern "C" int irc_colsum_batched(int dtype, const void* x, int64_t batch, int64_t R, int64_t C,
+                                  int64_t ldx, int64_t sx, float* out, int64_t so, int accumulate,
+                                  float* partial, int64_t partial_floats, irc_stream_t stream) {
+  IRC_REQUIRE(dtype == 0 || dtype == 1, "colsum_batched: dtype");
+  if (C == 0 || batch == 0) return IRC_OK;
+  const int64_t nch = R > 0 ? (R + CSB_ROWS - 1) / CSB_ROWS : 0;
+  IRC_REQUIRE(partial_floats >= batch * (nch > 0 ? nch : 1) * C, "colsum_batched: workspace");
+  const int V = dtype == 0 ? 8 : 4;
+  IRC_REQUIRE(C % V == 0 && ldx % V == 0 && sx % V == 0 && ((uintptr_t)x % 16) == 0,
+              "colsum_batched: needs 16-byte aligned rows (C %% %d == 0)", V);
+  hipStream_t st = as_stream(stream);
+  if (nch > 0) {
+    const dim3 g1((unsigned)((C + 64 * V - 1) / (64 * V)), (unsigned)nch, (unsigned)batch);
+    if (dtype == 0)
+      hipLaunchKernelGGL(colsum_b_stage1<unsigned short>, g1, dim3(256), 0, st,
+                         (const unsigned short*)x, R, (int)C, ldx, sx, partial, (int)nch);
+    else
+      hipLaunchKernelGGL(colsum_b_stage1<float>, g1, dim3(256), 0, st, (const float*)x, R, (int)C,
+                         ldx, sx, partial, (int)nch);
+  }
+  hipLaunchKernelGGL(colsum_b_stage2, dim3(nblk(C, 256), (unsigned)batch), dim3(256), 0, st,
+                     partial, (int)nch, (int)C, out, so, accumulate);
+  return check_launch("colsum_batched");
 }

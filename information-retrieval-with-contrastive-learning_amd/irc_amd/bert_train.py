@@ -22,9 +22,11 @@ Per layer, forward (saved for backward in brackets):
   qkv = x Wqkv^T + b [qkv] -> ctx = attention(qkv) [ctx] -> s1 = ctx Wo^T + bo + x
   [s1] -> a = LN1(s1) [a] -> g = gelu(u), u = a W1^T + b1 [u, g] -> s2 = g W2^T + b2
   + a [s2] -> y = LN2(s2) (next layer's x [x]).
-Backward mirrors it: LN bwd (recomputed statistics) -> dW / db (side stream) and
-dX GEMMs with fused residual / GELU' epilogues -> attention bwd -> ... -> the
-embedding LN bwd and the word / position / token-type scatter.
+Backward mirrors it: LN bwd (recomputed statistics) -> dX GEMMs with fused
+residual / GELU' epilogues -> attention bwd -> ... -> the embedding LN bwd and the
+word / position / token-type scatter; the weight / bias gradients are deferred and
+formed per kind for all layers at once (one batched GEMM + one batched column
+sum each) from [layers, B*L, dim] buffers.
 """
 from __future__ import annotations
 
@@ -35,7 +37,6 @@ import torch
 import torch.nn as nn
 
 from . import ops
-from ._torch import side_stream
 from .bert import BERT_BASE, PRESETS, BertConfig, BertModel
 from .precision import compute_dtype
 
@@ -104,7 +105,6 @@ class BertEncoder(nn.Module):
         self._shadow_t = None    # {name: bf16 transposed weight} (dX GEMM operands)
         self._shadow_ok = False
         self._shadow_t_ok = False
-        self._wgrad_pending = None
         if init_from is not None:
             self.load_from_bert(init_from)
         else:
@@ -273,69 +273,108 @@ class BertEncoder(nn.Module):
         return ops.gemm(dY, w, b_is_nk=False, **kw)
 
     def forward_compute(self, input_ids: torch.Tensor, attention_mask: torch.Tensor, save: bool):
-        """ids/mask [B, L] -> (emb [B, H] fp32 unit-norm, saved state or None)."""
+        """ids/mask [B, L] -> (emb [B, H] fp32 unit-norm, saved state or None).
+
+        With save, the four weight-gradient operands (layer input x, ctx, a, gelu
+        output g) are written into per-type [layers, B*L, dim] buffers so the
+        backward can form every layer's dW of one kind as ONE batched GEMM."""
         c = self.config
         ids = input_ids.to(torch.int64).contiguous()
         mask = attention_mask.to(torch.int64).contiguous()
         B, L = ids.shape
         if L > c.max_position_embeddings:
             raise ValueError(f"sequence length {L} > max_position_embeddings")
-        H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
+        H, I, heads, eps = c.hidden_size, c.intermediate_size, c.num_attention_heads, \
+            c.layer_norm_eps
+        nl = c.num_hidden_layers
         dt = compute_dtype()
         w = self._weights(dt, with_t=save)
-        x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
+        dev = self.flat.device
+        BL = B * L
+        if save:
+            xs = torch.empty((nl, BL, H), dtype=dt, device=dev)
+            ctxs = torch.empty((nl, BL, H), dtype=dt, device=dev)
+            as_ = torch.empty((nl, BL, H), dtype=dt, device=dev)
+            gs = torch.empty((nl, BL, I), dtype=dt, device=dev)
+        x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps,
+                         out=xs[0] if save else None)
         layers = []
-        for lw in w["layers"]:
+        for l, lw in enumerate(w["layers"]):
             qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
-            ctx = ops.attention(qkv, mask, B, L, H, heads)
+            ctx = ops.attention(qkv, mask, B, L, H, heads, out=ctxs[l] if save else None)
             s1 = ops.gemm(ctx, lw["wo"], bias=lw["bo"], residual=x, epilogue=ops.EPI_BIAS_RESID)
-            a = ops.layernorm(s1, lw["ln1_g"], lw["ln1_b"], eps, out=None if save else s1)
+            a = ops.layernorm(s1, lw["ln1_g"], lw["ln1_b"], eps, out=as_[l] if save else s1)
             if save:
-                g, u = ops.gemm_gelu_save(a, lw["w1"], lw["b1"])
+                g, u = ops.gemm_gelu_save(a, lw["w1"], lw["b1"], out=gs[l])
             else:
                 g, u = ops.gemm(a, lw["w1"], bias=lw["b1"], epilogue=ops.EPI_BIAS_GELU), None
             s2 = ops.gemm(g, lw["w2"], bias=lw["b2"], residual=a, epilogue=ops.EPI_BIAS_RESID)
-            y = ops.layernorm(s2, lw["ln2_g"], lw["ln2_b"], eps, out=None if save else s2)
+            last = l == nl - 1
             if save:
-                layers.append((x, qkv, ctx, s1, a, u, g, s2))
+                y = ops.layernorm(s2, lw["ln2_g"], lw["ln2_b"], eps,
+                                  out=None if last else xs[l + 1])
+                layers.append((qkv, s1, u, s2))
+            else:
+                y = ops.layernorm(s2, lw["ln2_g"], lw["ln2_b"], eps, out=s2)
             x = y
         m = ops.mean_rows(x, B, L, H)  # [B, H] fp32, PAD positions included
         emb, nrm = ops.l2norm_fwd(m)
-        saved = (ids, mask, B, L, w, layers, emb, nrm) if save else None
+        saved = (ids, mask, B, L, w, layers, (xs, ctxs, as_, gs), emb, nrm) if save else None
         return emb, saved
 
     def backward_compute(self, saved, demb: torch.Tensor):
-        """Accumulate d(loss)/d(params) into self.flat_grad."""
-        ids, mask, B, L, w, layers, emb, nrm = saved
+        """Accumulate d(loss)/d(params) into self.flat_grad.
+
+        The dX chain runs layer by layer; each layer's four output gradients (dqkv,
+        ds1, du, ds2) land in per-type [layers, B*L, dim] buffers, and after the
+        chain every layer's dW / db of one kind is ONE batched GEMM (K = B*L, both
+        operands K-outer) / one batched column sum, strided over the layers'
+        identically laid-out flat-buffer slices."""
+        ids, mask, B, L, w, layers, acts, emb, nrm = saved
+        xs, ctxs, as_, gs = acts
         c = self.config
-        H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
+        H, I, heads, eps = c.hidden_size, c.intermediate_size, c.num_attention_heads, \
+            c.layer_norm_eps
+        nl = c.num_hidden_layers
         g = self.flat_grad
         dev = g.device
+        BL = B * L
+        dt = xs.dtype
+        dqkvs = torch.empty((nl, BL, 3 * H), dtype=dt, device=dev)
+        ds1s = torch.empty((nl, BL, H), dtype=dt, device=dev)
+        dus = torch.empty((nl, BL, I), dtype=dt, device=dev)
+        ds2s = torch.empty((nl, BL, H), dtype=dt, device=dev)
         dm = ops.l2norm_bwd(demb.float().contiguous(), emb, nrm)  # [B, H] fp32
-        cur = torch.cuda.current_stream(dev)
-        side = side_stream(dev, "bert_wgrad")
         dy, bcast = dm, L  # top layer: the mean-pool backward folded into LN2's
-        for l in range(c.num_hidden_layers - 1, -1, -1):
-            x, qkv, ctx, s1, a, u, gg, s2 = layers[l]
+        for l in range(nl - 1, -1, -1):
+            qkv, s1, u, s2 = layers[l]
             lw = w["layers"][l]
             p = f"encoder.layer.{l}."
             ds2 = ops.layernorm_bwd(dy, s2, lw["ln2_g"], self.view(p + "output.LayerNorm.weight", g),
                                     self.view(p + "output.LayerNorm.bias", g), eps,
-                                    bcast_L=bcast, dy_scale=1.0 / L if bcast else 1.0)
+                                    bcast_L=bcast, dy_scale=1.0 / L if bcast else 1.0,
+                                    out=ds2s[l])
             bcast = 0
-            du = self._dx_gemm(ds2, lw["w2"], lw.get("w2T"), epilogue=ops.EPI_DGELU, residual=u)
-            self._wgrad(side, cur, ds2, gg, p + "output.dense")
+            du = self._dx_gemm(ds2, lw["w2"], lw.get("w2T"), epilogue=ops.EPI_DGELU, residual=u,
+                               out=dus[l])
             da = self._dx_gemm(du, lw["w1"], lw.get("w1T"), epilogue=ops.EPI_RESID, residual=ds2)
-            self._wgrad(side, cur, du, a, p + "intermediate.dense")
             ds1 = ops.layernorm_bwd(da, s1, lw["ln1_g"],
                                     self.view(p + "attention.output.LayerNorm.weight", g),
-                                    self.view(p + "attention.output.LayerNorm.bias", g), eps)
+                                    self.view(p + "attention.output.LayerNorm.bias", g), eps,
+                                    out=ds1s[l])
             dctx = self._dx_gemm(ds1, lw["wo"], lw.get("woT"))
-            self._wgrad(side, cur, ds1, ctx, p + "attention.output.dense")
-            dqkv = ops.attention_bwd(qkv, mask, ctx, dctx, B, L, H, heads)
-            self._wgrad(side, cur, dqkv, x, p + "attention.self.query")  # fused [3H, H]
+            dqkv = ops.attention_bwd(qkv, mask, ctxs[l], dctx, B, L, H, heads, out=dqkvs[l])
             dy = self._dx_gemm(dqkv, lw["wqkv"], lw.get("wqkvT"), epilogue=ops.EPI_RESID,
                                residual=ds1)
+        # layer-batched weight / bias gradients
+        for dY, X, wname, bname in ((dqkvs, xs, "attention.self.query.weight",
+                                     "attention.self.query.bias"),
+                                    (ds1s, ctxs, "attention.output.dense.weight",
+                                     "attention.output.dense.bias"),
+                                    (dus, as_, "intermediate.dense.weight",
+                                     "intermediate.dense.bias"),
+                                    (ds2s, gs, "output.dense.weight", "output.dense.bias")):
+            self._wgrad_batched(dY, X, wname, bname)
         # embeddings: LN backward on the rebuilt fp32 sum, then the table scatter
         e = ops.embed_sum(ids, w["word"], w["pos"], w["type0"])
         de = ops.layernorm_bwd(dy, e, w["ln_g"], self.view("embeddings.LayerNorm.weight", g),
@@ -344,23 +383,29 @@ class BertEncoder(nn.Module):
                       self.view("embeddings.position_embeddings.weight", g),
                       self.view("embeddings.token_type_embeddings.weight", g)[0],
                       c.pad_token_id)
-        cur.wait_stream(side)
 
-    def _wgrad(self, side, cur, dY, X, prefix):
-        """dW += dY^T X and db += colsum(dY) on the side stream (overlaps the dX
-        chain, which is the critical path)."""
-        g = self.flat_grad
-        wname, bname = prefix + ".weight", prefix + ".bias"
-        out_n, in_n = dY.shape[1], X.shape[1]
-        ow, ob = self.offsets[wname], self.offsets[bname]
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            ops.gemm(dY, X, trans_a=True, b_is_nk=False, accumulate=True,
-                     out=g.detach()[ow:ow + out_n * in_n].view(out_n, in_n),
-                     out_dtype=torch.float32)
-            ops.colsum(dY, out=g.detach()[ob:ob + out_n], accumulate=True)
-        dY.record_stream(side)
-        X.record_stream(side)
+    def _layer_stride(self, name):
+        c = self.config
+        if c.num_hidden_layers < 2:
+            return 0
+        st = self.offsets[f"encoder.layer.1.{name}"] - self.offsets[f"encoder.layer.0.{name}"]
+        for l in range(2, c.num_hidden_layers):  # identical per-layer layout
+            assert self.offsets[f"encoder.layer.{l}.{name}"] - \
+                self.offsets[f"encoder.layer.{l - 1}.{name}"] == st
+        return st
+
+    def _wgrad_batched(self, dY, X, wname, bname):
+        """dW[l] += dY[l]^T X[l] and db[l] += colsum(dY[l]) for every layer l."""
+        g = self.flat_grad.detach()
+        nl, BL, out_n = dY.shape
+        in_n = X.shape[2]
+        ow = self.offsets[f"encoder.layer.0.{wname}"]
+        ob = self.offsets[f"encoder.layer.0.{bname}"]
+        sw, sb = self._layer_stride(wname), self._layer_stride(bname)
+        ops.gemm_strided(dY, X, g[ow:], M=out_n, N=in_n, K=BL, batch=nl, lda=out_n,
+                         sA=BL * out_n, ldb=in_n, sB=BL * in_n, ldc=in_n, sC=sw, trans_a=True,
+                         b_is_nk=False, accumulate=True)
+        ops.colsum_batched(dY, g[ob:], sb, accumulate=True)
 
     def encode(self, input_ids, attention_mask):
         """last_hidden_state-free embedding path (no grad): [B, H] unit-norm."""

@@ -82,11 +82,11 @@ def gemm_strided(a, b, out, *, M, N, K, batch, lda, sA, ldb, sB, ldc, sC, trans_
     return out
 
 
-def embed_ln(ids, word, pos, type0, gamma, beta, eps=1e-12):
-    require_hip(ids, word, pos, type0, gamma, beta)
+def embed_ln(ids, word, pos, type0, gamma, beta, eps=1e-12, out=None):
+    require_hip(ids, word, pos, type0, gamma, beta, out)
     B, L = ids.shape
     H = word.shape[1]
-    y = torch.empty((B * L, H), dtype=word.dtype, device=word.device)
+    y = torch.empty((B * L, H), dtype=word.dtype, device=word.device) if out is None else out
     _lib.call("irc_embed_ln", _code(word), ptr(ids), ptr(word), ptr(pos), ptr(type0), ptr(gamma),
               ptr(beta), ptr(y), B * L, L, H, float(eps), stream_ptr(word.device))
     return y
@@ -101,9 +101,9 @@ def layernorm(x, gamma, beta, eps=1e-12, out=None):
     return out
 
 
-def attention(qkv, mask, B, L, H, heads):
-    require_hip(qkv, mask)
-    ctx = torch.empty((B * L, H), dtype=qkv.dtype, device=qkv.device)
+def attention(qkv, mask, B, L, H, heads, out=None):
+    require_hip(qkv, mask, out)
+    ctx = torch.empty((B * L, H), dtype=qkv.dtype, device=qkv.device) if out is None else out
     _lib.call("irc_attention", _code(qkv), ptr(qkv), ptr(mask), ptr(ctx), B, L, H, heads,
               stream_ptr(qkv.device))
     return ctx
@@ -370,14 +370,15 @@ def gemm_gelu_save(a, b, bias, out=None, pre=None):
 
 
 def layernorm_bwd(dy, x, gamma, dgamma, dbeta, eps=1e-12, bcast_L=0, dy_scale=1.0,
-                  accumulate=True, out_dtype=None):
+                  accumulate=True, out_dtype=None, out=None):
     """dL/dx of y = LN(x) * gamma + beta (statistics recomputed from x); dgamma /
     dbeta (+)= their deterministic column sums.  With bcast_L > 0, dy is [rows /
     bcast_L, H] and row r of the gradient is dy[r // bcast_L] * dy_scale."""
     require_hip(dy, x, gamma, dgamma, dbeta)
     H = x.shape[-1]
     rows = x.numel() // H
-    dx = torch.empty((rows, H), dtype=out_dtype or x.dtype, device=x.device)
+    dx = torch.empty((rows, H), dtype=out_dtype or x.dtype, device=x.device) if out is None \
+        else out
     if dx.dtype != x.dtype:
         raise TypeError("layernorm_bwd: dx dtype must match x")
     nws = int(_lib.load().irc_layernorm_bwd_workspace(rows, H))
@@ -388,10 +389,10 @@ def layernorm_bwd(dy, x, gamma, dgamma, dbeta, eps=1e-12, bcast_L=0, dy_scale=1.
     return dx
 
 
-def attention_bwd(qkv, mask, ctx, dctx, B, L, H, heads):
+def attention_bwd(qkv, mask, ctx, dctx, B, L, H, heads, out=None):
     """dqkv [B*L, 3H] of the fused-QKV masked self-attention (P recomputed)."""
-    require_hip(qkv, mask, ctx, dctx)
-    dqkv = torch.empty_like(qkv)
+    require_hip(qkv, mask, ctx, dctx, out)
+    dqkv = torch.empty_like(qkv) if out is None else out
     _lib.call("irc_attention_bwd", _code(qkv), ptr(qkv), ptr(mask), ptr(ctx), ptr(dctx),
               ptr(dqkv), B, L, H, heads, stream_ptr(qkv.device))
     return dqkv
@@ -443,3 +444,14 @@ def cast_bf16_into(x, y):
     require_hip(x, y)
     _lib.call("irc_cast_bf16", ptr(x), ptr(y), x.numel(), stream_ptr(x.device))
     return y
+
+
+def colsum_batched(x, out, out_stride, accumulate=True):
+    """x [batch, R, C] (bf16 / fp32, contiguous rows) -> out[b * out_stride + c] (+)=
+    column sums of x[b] (deterministic)."""
+    require_hip(x, out)
+    nb, R, C = x.shape
+    nws = int(_lib.load().irc_colsum_batched_workspace(nb, R, C))
+    ws = torch.empty((max(nws, 1),), dtype=F32, device=x.device)
+    _lib.call("irc_colsum_batched", _code(x), ptr(x), nb, R, C, x.stride(1), x.stride(0), ptr(out),
+              int(out_stride), 1 if accumulate else 0, ptr(ws), nws, stream_ptr(x.device))

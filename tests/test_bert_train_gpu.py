@@ -357,3 +357,20 @@ def test_bert_mode_bf16_steps_finite_and_shadow_current(gpu):
     sT = model.encoder_q.shadow_t()
     n = "encoder.layer.1.intermediate.dense.weight"
     assert torch.equal(sT[n], model.encoder_q.view(n).to(torch.bfloat16).T.contiguous())
+
+
+@pytest.mark.parametrize("dtype,R,C", [(torch.bfloat16, 16384, 768), (torch.bfloat16, 1000, 3072),
+                                       (torch.float32, 700, 136)])
+def test_colsum_batched(gpu, dtype, R, C):
+    from irc_amd import ops
+
+    nb = 3
+    g = torch.Generator().manual_seed(R + C)
+    x = torch.randn((nb, R, C), generator=g).to(dtype)
+    stride = C + 40
+    out = torch.ones((nb * stride,), device=gpu)
+    ops.colsum_batched(x.to(gpu), out, stride, accumulate=True)
+    ref = x.float().sum(1)
+    got = out.view(nb, stride)[:, :C].cpu() - 1
+    assert _rel(got, ref) <= 1e-5
+    assert torch.all(out.view(nb, stride)[:, C:] == 1)

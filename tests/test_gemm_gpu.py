@@ -160,3 +160,92 @@ def test_big_tile_accumulate_fp32(gpu):
     ops.gemm(a.to(gpu), b.to(gpu), out=out, accumulate=True)
     ref = c0 + a.float() @ b.float().t()
     assert (out.cpu() - ref).abs().max().item() <= 2e-3 * K ** 0.5
+
+
+# ---- the 256x256 ping-pong path (gemm_pp.hip): shapes with >= 32 output tiles
+@pytest.mark.parametrize("trans_a,b_is_nk", [(False, True), (False, False), (True, True),
+                                             (True, False)])
+@pytest.mark.parametrize("M,N,K", [(2048, 1024, 256), (1800, 1208, 320)])
+def test_pp_layouts(gpu, trans_a, b_is_nk, M, N, K):
+    """All four operand layouts, ragged M/N (not multiples of 256), bf16 in, fp32 out.
+    Tolerance: bf16 operands, fp32 accumulation -> 1e-3 relative to max |ref|."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(M + N + K + 7 * trans_a + 3 * b_is_nk)
+    a = torch.randn((K, M) if trans_a else (M, K), generator=g).bfloat16()
+    b = torch.randn((N, K) if b_is_nk else (K, N), generator=g).bfloat16()
+    out = ops.gemm(a.to(gpu), b.to(gpu), trans_a=trans_a, b_is_nk=b_is_nk,
+                   out_dtype=torch.float32)
+    ref = _ref(a, b, trans_a, b_is_nk, None, 0, None, 1.0)
+    assert (out.cpu() - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
+def test_pp_epilogues(gpu, epi, odt):
+    from irc_amd import ops
+
+    M, N, K = 2304, 1040, 192
+    g = torch.Generator().manual_seed(100 + epi)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    b = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g) if epi in (1, 2, 3, 6) else None
+    res = torch.randn(M, N, generator=g).to(odt) if epi in (3, 4, 5, 6) else None
+    out = ops.gemm(a.to(gpu), b.to(gpu), bias=None if bias is None else bias.to(gpu),
+                   epilogue=epi, residual=None if res is None else res.to(gpu), out_dtype=odt,
+                   alpha=0.5)
+    y = 0.5 * (a.float() @ b.float().T)
+    if bias is not None:
+        y = y + bias
+    if epi == 2:
+        ref = torch.nn.functional.gelu(y)
+    elif epi in (3, 4):
+        ref = y + res.float()
+    elif epi == 5:
+        ur = res.float().requires_grad_(True)
+        torch.nn.functional.gelu(ur).backward(y)
+        ref = ur.grad
+    elif epi == 6:
+        ref = torch.nn.functional.gelu(y)
+    else:
+        ref = y
+    tol = 1e-2 if odt == torch.bfloat16 else 1e-3
+    assert (out.float().cpu() - ref).abs().max().item() <= tol * ref.abs().max().item()
+
+
+def test_pp_gelu_save_writes_preactivation(gpu):
+    from irc_amd import ops
+
+    M, N, K = 2048, 1024, 128
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn(M, K, generator=g).bfloat16().to(gpu)
+    b = torch.randn(N, K, generator=g).bfloat16().to(gpu)
+    bias = torch.randn(N, generator=g).to(gpu)
+    out, pre = ops.gemm_gelu_save(a, b, bias)
+    y = a.float().cpu() @ b.float().cpu().T + bias.cpu()
+    assert (pre.float().cpu() - y).abs().max().item() <= 1e-2 * y.abs().max().item()
+    assert (out.float().cpu() - torch.nn.functional.gelu(y)).abs().max().item() <= \
+        1e-2 * y.abs().max().item()
+
+
+@pytest.mark.parametrize("M,N,K,batch", [(768, 768, 16384, 1), (1024, 256, 8192, 2),
+                                         (3072, 768, 4096, 1)])
+def test_pp_splitk_accumulate(gpu, M, N, K, batch):
+    """Weight-gradient shapes: both operands K-outer, few output tiles -> deterministic
+    split-K slabs, fp32 accumulate into an existing gradient.  Bitwise repeatable."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(M + K)
+    a = torch.randn((batch, K, M), generator=g).bfloat16().to(gpu)
+    b = torch.randn((batch, K, N), generator=g).bfloat16().to(gpu)
+    base = torch.randn((batch, M, N), generator=g).to(gpu)
+    outs = []
+    for _ in range(2):
+        out = base.clone()
+        ops.gemm_strided(a, b, out, M=M, N=N, K=K, batch=batch, lda=M, sA=K * M, ldb=N, sB=K * N,
+                         ldc=N, sC=M * N, trans_a=True, b_is_nk=False, accumulate=True)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+    ref = base.cpu() + torch.einsum("bkm,bkn->bmn", a.float().cpu(), b.float().cpu())
+    err = (outs[0].cpu() - ref).abs().max().item()
+    assert err <= 1e-3 * ref.abs().max().item()

@@ -25,16 +25,45 @@ SHAPES = [  # (name, M, N, K, epilogue)
     ("square4k", 4096, 4096, 4096, 0),
     ("dW_ih^T", 1024, 768, 16384, -1),   # dg^T x: both operands K-outer, split-K
     ("dW_hh^T", 1024, 256, 16384, -1),
+    # trainable BERT-base backward (256 anchors x L=64 -> 16384 rows)
+    ("bert_dx_ffn2", 16384, 3072, 768, 5),   # dU = (dS2 W2) * gelu'(u)
+    ("bert_dx_ffn1", 16384, 768, 3072, 4),   # dA = dU W1 + dS2
+    ("bert_dx_qkv", 16384, 768, 2304, 4),
+    ("bert_dW_ffn1", 3072, 768, 16384, -1),
+    ("bert_dW_qkv", 2304, 768, 16384, -1),
+    ("bert_dW_o", 768, 768, 16384, -1),
 ]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--layouts", action="store_true")
     args = ap.parse_args()
     from irc_amd import ops
 
     dev = torch.device("cuda:0")
+    if args.layouts:  # 4096^3 mainloop efficiency of every operand layout (bf16 out)
+        for ta, nk in ((False, True), (False, False), (True, True), (True, False)):
+            M = N = K = 4096
+            a = torch.randn((K, M) if ta else (M, K), device=dev).to(torch.bfloat16)
+            b = torch.randn((N, K) if nk else (K, N), device=dev).to(torch.bfloat16)
+            out = torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+            run = lambda: ops.gemm(a, b, trans_a=ta, b_is_nk=nk, out=out)
+            for _ in range(3):
+                run()
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(args.iters):
+                run()
+            e1.record(st)
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.iters
+            tf = 2.0 * M * N * K / us / 1e6
+            lay = ("COL" if ta else "ROW") + ("NK" if nk else "KN")
+            print(f"square4k {lay:6s} {us:9.1f} us  {tf:7.1f} TF/s  {tf / 2500:.1%}", flush=True)
+        return
     for name, M, N, K, epi in SHAPES:
         if epi < 0:  # K-outer operands: C[M,N] = A[K,M]^T B[K,N], fp32 accumulate
             a = torch.randn((K, M), device=dev).to(torch.bfloat16)
@@ -58,7 +87,7 @@ def main():
         a = torch.randn((M, K), device=dev).to(torch.bfloat16)
         b = torch.randn((N, K), device=dev).to(torch.bfloat16)
         bias = torch.randn((N,), device=dev) if epi in (1, 2, 3) else None
-        res = torch.randn((M, N), device=dev).to(torch.bfloat16) if epi in (3, 4) else None
+        res = torch.randn((M, N), device=dev).to(torch.bfloat16) if epi in (3, 4, 5) else None
         od = torch.float32 if name in ("lstm_dx",) or name.startswith("lstm_xp") else torch.bfloat16
         if res is not None:
             res = res.to(od)
