@@ -18,13 +18,27 @@ struct PArgs {
   float alpha;
   int accumulate;
   int vec_c;
+  // scan-filter epilogue (EPI_SCAN): survivors key >= thr[q] of C[q][doc] go to
+  // keys[(tn * qpad + q) * cap + slot] (cap >= 256: a doc tile never overflows),
+  // their count to counts[tn * qpad + q]; doc global index = idx_base + doc * stride
+  const uint64_t* thr;
+  uint64_t* keys;
+  uint32_t* counts;
+  int64_t cap;
+  int qpad;
+  int stride;
+  uint32_t idx_base;
 };
+
+constexpr int EPI_SCAN = 7;
 
 int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t batch);
 bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                int64_t sA, const void* B, int64_t ldb, int64_t sB, int64_t batch, int splits);
 void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, int splits,
          hipStream_t st);
+// scan filter: A = queries [M=Q][K=D], B = docs [N][D] (row stride ldb), EPI_SCAN
+void run_scan(const PArgs& a, hipStream_t st);
 
 }  // namespace gpp
 }  // namespace irc

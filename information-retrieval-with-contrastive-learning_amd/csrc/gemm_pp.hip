@@ -231,6 +231,89 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   // acc[i][j] element e -> row 128 grp + 16 i + 4 (lane >> 4) + e, col 64 wn + 16 j + (lane & 15)
   const int rbase0 = m0 + 128 * grp;
   const int cbase = n0 + 64 * wn;
+  if constexpr (EPI == EPI_SCAN) {
+    // rows = queries, cols = docs.  LDS is free (every wave is past its last
+    // fragment read): per-query survivor counters + thresholds (key and its float
+    // prefilter: key >= thr implies score >= float(thr >> 32) for non-NaN scores).
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
+    uint64_t* thk = reinterpret_cast<uint64_t*>(lds + 1024);
+    float* thf = reinterpret_cast<float*>(lds + 3072);
+    if (threadIdx.x < 256) {
+      const int q = m0 + threadIdx.x;
+      const uint64_t t = (g.thr != nullptr && q < g.M) ? g.thr[q] : 0ull;
+      cnt[threadIdx.x] = 0;
+      thk[threadIdx.x] = t;
+      const uint32_t hi = (uint32_t)(t >> 32);
+      // padded query rows never pass; no threshold (hi == 0) admits everything
+#ifdef IRC_PP_SCAN_NOPASS  // diagnostic build: nothing passes
+      thf[threadIdx.x] = __builtin_huge_valf();
+      if (true) {} else
+#endif
+      thf[threadIdx.x] = q >= g.M ? __builtin_huge_valf()
+                                  : (hi == 0 ? -__builtin_huge_valf() : unorderable_f32(hi));
+    }
+    __syncthreads();
+#ifdef IRC_PP_SCAN_NOEPI  // diagnostic build: main loop + counters only
+    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
+      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = acc[0][0][0] == 12345.f ? 1u : 0u;
+    return;
+#endif
+    // Pass test of the lane's 128 scores (bit 16 i + 4 j + e) as a branch-free
+    // mask; then per half (i < 4, i >= 4) the lane's 64 accumulators are staged in
+    // its private LDS slot (16 x 16-byte writes, unconditional) and only the set
+    // bits (a few per lane: the threshold admits ~16k of N per query) read their
+    // score back by a dynamic LDS index for the exact-key / slot / store path.
+    float* slotv = reinterpret_cast<float*>(lds + 4096) + threadIdx.x * 64;
+    uint64_t pm[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 tf = *reinterpret_cast<const f32x4*>(&thf[128 * grp + 16 * i + 4 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int bit = 16 * i + 4 * j + e;
+          pm[bit >> 6] |= (uint64_t)(!(acc[i][j][e] < tf[e])) << (bit & 63);
+        }
+    }
+#ifdef IRC_PP_SCAN_MASKONLY  // diagnostic build: mask, no exact path
+    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
+      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = __popcll(pm[0] | pm[1]) == 999 ? 1u : 0u;
+    return;
+#endif
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      if (__ballot(pm[hh] != 0) == 0) continue;  // wave-uniform
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4*>(slotv + 16 * i + 4 * j) = acc[4 * hh + i][j];
+      uint64_t bits = pm[hh];
+      while (__ballot(bits != 0) != 0) {
+        if (bits != 0) {
+          const int b = __builtin_ctzll(bits);
+          bits &= bits - 1;
+          const float v = slotv[b];
+          const int bit = 64 * hh + b;
+          const int ql = 128 * grp + 16 * (bit >> 4) + 4 * (lane >> 4) + (bit & 3);
+          const int q = m0 + ql;
+          const int d = cbase + 16 * ((bit >> 2) & 3) + (lane & 15);
+          if (q < g.M && d < g.N) {
+            const uint64_t key = make_key(v, g.idx_base + (uint32_t)d * (uint32_t)g.stride);
+            if (key >= thk[ql]) {
+              const uint32_t slot = atomicAdd(&cnt[ql], 1u);
+              g.keys[((int64_t)tn * g.qpad + q) * g.cap + slot] = key;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
+      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = cnt[threadIdx.x];
+    return;
+  }
   float* st = reinterpret_cast<float*>(lds) + wave * (32 * EP_PITCH);
   const bool slab = g.P != nullptr;
   if (slab || g.vec_c) {
@@ -401,6 +484,15 @@ static void launch_epi(int epi, const PArgs& a, dim3 grid, hipStream_t st) {
     IRC_PP(0) IRC_PP(1) IRC_PP(2) IRC_PP(3) IRC_PP(4) IRC_PP(5) IRC_PP(6)
 #undef IRC_PP
   }
+}
+
+template <typename TO>
+static void launch_layout(int la, int lb, int epi, const PArgs& a, dim3 grid, hipStream_t st);
+
+void run_scan(const PArgs& a, hipStream_t st) {
+  const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_pp_kernel<true, true, float, EPI_SCAN>), dim3((unsigned)tiles),
+                     dim3(NT), 0, st, a);
 }
 
 template <typename TO>

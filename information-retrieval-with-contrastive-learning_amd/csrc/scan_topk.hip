@@ -20,7 +20,7 @@
 //    digits) of the k-th key, then a bitonic sort of the k winners.
 #include <stdio.h>
 
-#include "irc_common.h"
+#include "gemm_pp.h"
 
 #ifndef IRC_SCAN_AUX
 #define IRC_SCAN_AUX 0  // cache policy of the corpus stream (0: default)
@@ -629,8 +629,23 @@ struct Plan {
   int64_t cap_s;
   int g_f, tpw_f;
   int64_t cap_f;
+  // filter pass on the ping-pong GEMM (Q >= pp_min_q): regions = 256-doc tiles
+  bool pp;
+  int pp_G, pp_qpad;
+  int64_t pp_cap;
   size_t off_thr, off_cnt, off_keys, bytes;
 };
+
+// IRC_SCAN_PP=0 disables the GEMM-kernel filter; IRC_SCAN_PP_MINQ sets its Q floor.
+static int pp_min_q() {
+  static const int v = [] {
+    const char* e = getenv("IRC_SCAN_PP");
+    if (e && e[0] == '0') return 1 << 30;
+    const char* m = getenv("IRC_SCAN_PP_MINQ");
+    return m ? atoi(m) : 192;
+  }();
+  return v;
+}
 
 static int pick_ks(int64_t D) { return D > 512 ? 2 : 1; }  // <= 128 fragment VGPRs/wave
 
@@ -700,11 +715,24 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k) {
   const int gmax = p.g_s > p.g_f ? p.g_s : p.g_f;
   int64_t kmax = (int64_t)p.g_f * p.cap_f;
   if (p.two_phase && (int64_t)p.g_s * p.cap_s > kmax) kmax = (int64_t)p.g_s * p.cap_s;
+  size_t cnt_bytes = (size_t)gmax * p.qpad * 2 * p.ks * 4;
+  size_t key_bytes = (size_t)kmax * p.qpad * 8;
+  p.pp_G = (int)((N + 255) / 256);
+  p.pp_qpad = (int)((Q + 255) / 256 * 256);
+  p.pp_cap = 256;  // a 256-doc tile can never overflow its region
+  const size_t pp_keys = (size_t)p.pp_G * p.pp_qpad * p.pp_cap * 8;
+  p.pp = Q >= pp_min_q() && N >= 256 && pp_keys <= ((size_t)2 << 30);
+  if (p.pp) {
+    const size_t pc = (size_t)p.pp_G * p.pp_qpad * 4;
+    if (pc > cnt_bytes) cnt_bytes = pc;
+    if (pp_keys > key_bytes) key_bytes = pp_keys;
+  }
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const int qthr = p.pp && p.pp_qpad > p.qpad ? p.pp_qpad : p.qpad;
   p.off_thr = 0;
-  p.off_cnt = al(p.off_thr + (size_t)p.qpad * 8);
-  p.off_keys = al(p.off_cnt + (size_t)gmax * p.qpad * 2 * p.ks * 4);
-  p.bytes = al(p.off_keys + (size_t)kmax * p.qpad * 8);
+  p.off_cnt = al(p.off_thr + (size_t)qthr * 8);
+  p.off_keys = al(p.off_cnt + cnt_bytes);
+  p.bytes = al(p.off_keys + key_bytes);
   return p;
 }
 
@@ -810,6 +838,35 @@ extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, i
                        (int)SEL_THRESHOLD, thr, nullptr, nullptr);
     if ((rc = check_launch("select_kernel(threshold)"))) return rc;
   }
+  if (p.pp && ((uintptr_t)qs % 16) == 0 && ((uintptr_t)ds % 16) == 0) {
+    // filter = NT GEMM C[q][doc] = Q . Docs^T on the ping-pong kernel with a
+    // threshold epilogue; regions are (256-doc tile, query) with cap 256.
+    gpp::PArgs a{};
+    a.A = qs;
+    a.B = ds;
+    a.M = (int)Q;
+    a.N = (int)N;
+    a.K = (int)D;
+    a.kchunk = (int)D;
+    a.lda = D;
+    a.ldb = D;
+    a.alpha = 1.f;
+    a.thr = p.two_phase ? thr : nullptr;
+    a.keys = keys;
+    a.counts = cnt;
+    a.cap = p.pp_cap;
+    a.qpad = p.pp_qpad;
+    a.stride = 1;
+    a.idx_base = base;
+    prof_begin(st);
+    gpp::run_scan(a, st);
+    prof_end("scan_filter", st, (double)N * D * 2 + (double)Q * D * 2);
+    if ((rc = check_launch("gemm_pp_kernel(scan)"))) return rc;
+    RegionSource s2{keys, cnt, p.pp_G, p.pp_qpad, p.pp_cap, 1};
+    hipLaunchKernelGGL((select_kernel<RegionSource>), dim3(Q), dim3(SEL_NT), 0, st, s2, (int)k,
+                       (int)SEL_FINAL, nullptr, out_score, out_idx);
+    return check_launch("select_kernel(final)");
+  }
   prof_begin(st);
   rc = dispatch_tile<KEYS>(D, p, p.g_f, qs, ds, (int)Q, N, 1, p.tpw_f, base,
                            p.two_phase ? thr : nullptr, keys, cnt, p.cap_f, nullptr, st);
@@ -839,6 +896,24 @@ extern "C" int irc_scan_scores(const void* queries, const void* docs, int64_t Q,
   IRC_REQUIRE(supported_d(D), "scan_scores: unsupported D=%lld", (long long)D);
   if (Q == 0 || N == 0) return IRC_OK;
   Plan p = make_plan(Q, N, D, 1);
+  if (p.pp && ((uintptr_t)queries % 16) == 0 && ((uintptr_t)docs % 16) == 0) {
+    // same MFMA arithmetic as irc_scan_topk's filter on this path
+    gpp::PArgs a{};
+    a.A = static_cast<const unsigned short*>(queries);
+    a.B = static_cast<const unsigned short*>(docs);
+    a.C = out;
+    a.M = (int)Q;
+    a.N = (int)N;
+    a.K = (int)D;
+    a.kchunk = (int)D;
+    a.lda = D;
+    a.ldb = D;
+    a.ldc = N;
+    a.alpha = 1.f;
+    a.vec_c = (N % 8 == 0) && ((uintptr_t)out % 16) == 0;
+    gpp::run(1, 0, 0, 0, a, 1, 1, as_stream(stream));
+    return check_launch("gemm_pp_kernel(scores)");
+  }
   return dispatch_tile<SCORES>(D, p, p.g_f, static_cast<const unsigned short*>(queries),
                                static_cast<const unsigned short*>(docs), (int)Q, N, 1, p.tpw_f, 0,
                                nullptr, nullptr, nullptr, 0, out, as_stream(stream));

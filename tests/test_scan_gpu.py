@@ -65,6 +65,10 @@ def test_golden_ties(gpu):
     (16, 60000, 128, 100, 0),   # two-phase (sampled threshold) path
     (64, 40000, 768, 1024, 3),  # maximum k
     (8, 20000, 128, 1, 0),      # k = 1
+    # Q >= 128: filter on the ping-pong GEMM kernel (regions = 256-doc tiles)
+    (128, 60000, 768, 100, 0),  # two-phase, C2 dims
+    (200, 30000, 256, 1024, 7),  # maximum k, ragged Q
+    (384, 9000, 64, 50, 0),     # two query tiles, D = 64 (one K-tile)
 ])
 def test_topk_exact_vs_oracle(gpu, Q, N, D, k, off):
     from irc_amd import retrieval
@@ -81,11 +85,24 @@ def test_topk_exact_vs_oracle(gpu, Q, N, D, k, off):
 def test_adversarial_sorted_corpus(gpu):
     """Later docs strictly better than the sample: nearly every doc survives the
     threshold, the selection must still be exact."""
-    from irc_amd import retrieval
-
     N, D, k = 50000, 128, 100
     q = np.zeros((4, D), np.float32)
     q[:, 0] = 1.0
+    _check_sorted_corpus(gpu, q, N, D, k)
+
+
+def test_adversarial_sorted_corpus_gemm_filter(gpu):
+    """Same with Q = 160 (the GEMM-kernel filter): whole 256-doc regions survive."""
+    N, D, k = 50000, 128, 100
+    q = np.zeros((160, D), np.float32)
+    q[:, 0] = 1.0
+    q[::2, 1] = 0.5
+    _check_sorted_corpus(gpu, q, N, D, k)
+
+
+def _check_sorted_corpus(gpu, q, N, D, k):
+    from irc_amd import retrieval
+
     d = np.zeros((N, D), np.float32)
     d[:, 0] = (np.arange(N) % 256) / 128.0 - 1.0  # ramp, repeated -> huge tie groups
     s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), k)
@@ -94,11 +111,12 @@ def test_adversarial_sorted_corpus(gpu):
     np.testing.assert_array_equal(s.cpu().numpy(), rs)
 
 
-def test_gaussian_margin_aware(gpu):
+@pytest.mark.parametrize("Q", [64, 256])
+def test_gaussian_margin_aware(gpu, Q):
     from irc_amd import retrieval
 
     torch.manual_seed(2024)
-    Q, N, D, k = 64, 30000, 768, 100
+    N, D, k = 30000, 768, 100
     q = torch.nn.functional.normalize(torch.randn(Q, D)).bfloat16()
     d = torch.nn.functional.normalize(torch.randn(N, D)).bfloat16()
     s, i = retrieval.scan_topk(q.to(gpu), d.to(gpu), k)

@@ -32,6 +32,10 @@ SHAPES = [  # (name, M, N, K, epilogue)
     ("bert_dW_ffn1", 3072, 768, 16384, -1),
     ("bert_dW_qkv", 2304, 768, 16384, -1),
     ("bert_dW_o", 768, 768, 16384, -1),
+    # scan-shaped (C = Q . Docs^T): one shared 256-row operand vs the roles swapped
+    ("scan_q256", 256, 100352, 768, 0),
+    ("scan_swap", 100352, 256, 768, 0),
+    ("scan_q1024", 1024, 100352, 768, 0),
 ]
 
 
@@ -89,6 +93,8 @@ def main():
         bias = torch.randn((N,), device=dev) if epi in (1, 2, 3) else None
         res = torch.randn((M, N), device=dev).to(torch.bfloat16) if epi in (3, 4, 5) else None
         od = torch.float32 if name in ("lstm_dx",) or name.startswith("lstm_xp") else torch.bfloat16
+        if name.startswith("scan"):
+            od = torch.bfloat16
         if res is not None:
             res = res.to(od)
         out = torch.empty((M, N), device=dev, dtype=od)
