@@ -615,6 +615,239 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
   }
 }
 
+// Wave-per-query select for region sources (the scan's two selects): the same
+// exact radix select (8-bit digits, MSB first, early exit when the chosen bucket
+// holds exactly the remaining rank) and the same outputs as select_kernel, but
+// one wave per query (SWQ per workgroup), so every step is
+// wave-synchronous (no workgroup barriers).  Candidates are staged in the wave's
+// LDS slice (up to SW keys); a query with more candidates visits its regions in
+// global memory on every pass instead, lanes striding over regions (slower, same
+// result).  k <= SW.
+constexpr int SW = 8192;  // 64 KB of staged keys per query
+constexpr int SWQ = 1;   // queries (waves) per workgroup
+
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64 * SWQ) void select_wave_kernel(RegionSource src, int Q, int k,
+                                                               int mode,
+                                                               uint64_t* __restrict__ thr_out,
+                                                               float* __restrict__ out_score,
+                                                               int64_t* __restrict__ out_idx) {
+  __shared__ uint64_t stage_all[SWQ][SW];
+  __shared__ uint32_t hist_all[SWQ][256];
+  __shared__ uint16_t rid_all[SWQ][SW];
+  __shared__ uint32_t roff_all[SWQ][SEL_MAXR + 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int q = blockIdx.x * SWQ + wv;
+  if (q >= Q) return;  // whole wave; nothing below synchronises across waves
+  uint64_t* stage = stage_all[wv];
+  uint32_t* hist = hist_all[wv];
+  const int R = src.nregions();
+  // total candidates
+  uint32_t M = 0;
+  for (int r = lane; r < R; r += 64) M += src.count(q, r);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) M += __shfl_xor(M, o, 64);
+  const bool staged = M <= (uint32_t)SW && R <= SEL_MAXR;
+  if (staged) {
+    // region offsets (running wave scan) + a region-id map in LDS, then a flat
+    // copy with 8 independent loads in flight per lane
+    uint16_t* rid = rid_all[wv];
+    uint32_t* roff = roff_all[wv];
+    uint32_t base = 0;
+    for (int r0 = 0; r0 < R; r0 += 64) {
+      const int r = r0 + lane;
+      const uint32_t c = r < R ? src.count(q, r) : 0u;
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      const uint32_t off = base + incl - c;
+      if (r < R) roff[r] = off;
+      for (uint32_t j = 0; j < c; ++j) rid[off + j] = (uint16_t)r;
+      base += __shfl(incl, 63, 64);
+    }
+    wsync();
+    constexpr int U = 8;
+    for (uint32_t i0 = lane; i0 < M; i0 += 64 * U) {
+      uint64_t v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = i0 + 64 * u;
+        if (i < M) {
+          const int r = rid[i];
+          v[u] = src.region(q, r)[i - roff[r]];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = i0 + 64 * u;
+        if (i < M) stage[i] = v[u];
+      }
+    }
+    wsync();
+  }
+  auto visit = [&](auto&& f) {  // f must not use cross-lane operations
+    if (staged) {
+      for (uint32_t i = lane; i < M; i += 64) f(stage[i]);
+    } else {
+      for (int r = lane; r < R; r += 64) {
+        const uint32_t n = src.count(q, r);
+        const uint64_t* rp = src.region(q, r);
+        for (uint32_t j = 0; j < n; ++j) f(rp[j]);
+      }
+    }
+  };
+  uint64_t kth = 0;
+  if (M > (uint32_t)k) {
+    uint64_t mn = ~0ull, mx = 0;
+    visit([&](uint64_t key) {
+      mn = key < mn ? key : mn;
+      mx = key > mx ? key : mx;
+    });
+    mn = wave_min_u64(mn);
+    mx = wave_max_u64(mx);
+    const int top = 63 - __builtin_clzll((mn ^ mx) | 1ull);
+    const int first_shift = (top / 8) * 8;
+    const int last_shift = (mode == SEL_THRESHOLD) ? 48 : 0;
+    uint64_t pmask = first_shift >= 56 ? 0ull : (~0ull << (first_shift + 8));
+    uint64_t prefix = mn & pmask;
+    uint32_t kr = (uint32_t)k;
+    for (int shift = first_shift; shift >= last_shift; shift -= 8) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) hist[4 * lane + t] = 0;
+      wsync();
+      visit([&](uint64_t key) {
+        if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+      });
+      wsync();
+      uint32_t bb[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bb[t] = hist[4 * lane + t];
+      const uint32_t mine = bb[0] + bb[1] + bb[2] + bb[3];
+      uint32_t suf = mine;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_down(suf, o, 64);
+        if (lane + o < 64) suf += t;
+      }
+      const uint32_t above = suf - mine;
+      // the lane whose 4 digits contain the kr-th largest
+      const bool hit = suf >= kr && above < kr;
+      uint32_t sel = 0, rem = 0, selc = 0;
+      if (hit) {
+        uint32_t acc = above;
+        for (int t = 3; t >= 0; --t) {
+          if (acc + bb[t] >= kr) {
+            sel = 4 * lane + t;
+            selc = bb[t];
+            break;
+          }
+          acc += bb[t];
+        }
+        rem = kr - acc;
+      }
+      const int src_lane = __builtin_ctzll(__ballot(hit));
+      sel = __shfl(sel, src_lane, 64);
+      rem = __shfl(rem, src_lane, 64);
+      selc = __shfl(selc, src_lane, 64);
+      prefix |= (uint64_t)sel << shift;
+      pmask |= (uint64_t)0xff << shift;
+      kr = rem;
+      if (selc == rem) break;  // the bucket holds exactly the remaining rank
+    }
+    kth = (mode == SEL_THRESHOLD) ? (prefix & (~0ull << 48)) : prefix;
+  }
+  if (mode == SEL_THRESHOLD) {
+    if (lane == 0) thr_out[q] = kth;
+    return;
+  }
+  // collect the min(M, k) keys >= kth (wave prefix-sum compaction), then sort
+  const int cnt = (int)(M < (uint32_t)k ? M : (uint32_t)k);
+  int npow = 1;
+  while (npow < cnt) npow <<= 1;
+  // In-place compaction: chunk i0 is read by every lane before any of its slots
+  // is written, and the write position never passes the read position.
+  uint64_t* cand = stage;
+  uint32_t wpos = 0;
+  if (staged) {
+    for (uint32_t i0 = 0; i0 < M; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const uint64_t key = i < M ? stage[i] : 0ull;
+      const bool take = i < M && key >= kth;
+      const uint64_t bal = __ballot(take);
+      wsync();  // every lane has read its key before any slot of this chunk is written
+      if (take) cand[wpos + __popcll(bal & ((1ull << lane) - 1))] = key;
+      wpos += (uint32_t)__popcll(bal);
+      wsync();
+    }
+  } else {  // order is irrelevant (sorted below): an LDS slot counter
+    if (lane == 0) hist[0] = 0;
+    wsync();
+    visit([&](uint64_t key) {
+      if (key >= kth) cand[atomicAdd(&hist[0], 1u)] = key;
+    });
+    wsync();
+  }
+  for (int i = cnt + lane; i < npow; i += 64) cand[i] = 0ull;
+  wsync();
+  for (int size = 2; size <= npow; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < npow; i += 64) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool desc = ((i & size) == 0);
+          const uint64_t x = cand[i], y = cand[j];
+          if (desc ? (x < y) : (x > y)) {
+            cand[i] = y;
+            cand[j] = x;
+          }
+        }
+      }
+      wsync();
+    }
+  }
+  for (int i = lane; i < k; i += 64) {
+    float sc = -__builtin_huge_valf();
+    int64_t id = -1;
+    if (i < cnt) {
+      const uint64_t key = cand[i];
+      sc = unorderable_f32((uint32_t)(key >> 32));
+      id = (int64_t)(uint32_t)(~(uint32_t)key);
+    }
+    out_score[(int64_t)q * k + i] = sc;
+    out_idx[(int64_t)q * k + i] = id;
+  }
+}
+
+// The 256-thread select_kernel is the default: measured on MI355X (100k x 768,
+// k=100) the wave-per-query variant made the whole call 40 us slower at Q=1 and
+// 35 us slower at Q=256 (one wave walks every region and every radix pass alone).
+// IRC_SCAN_WAVE_SELECT=1 selects it, for comparison.
+static bool wave_select() {
+  static const bool v = [] {
+    const char* e = getenv("IRC_SCAN_WAVE_SELECT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+static void launch_select(const RegionSource& src, int Q, int k, int mode, uint64_t* thr,
+                          float* out_score, int64_t* out_idx, hipStream_t st) {
+  if (wave_select())
+    hipLaunchKernelGGL(select_wave_kernel, dim3((unsigned)((Q + SWQ - 1) / SWQ)), dim3(64 * SWQ),
+                       0, st, src, Q, k, mode, thr, out_score, out_idx);
+  else
+    hipLaunchKernelGGL((select_kernel<RegionSource>), dim3((unsigned)Q), dim3(SEL_NT), 0, st, src,
+                       k, mode, thr, out_score, out_idx);
+}
+
 // ------------------------------------------------------------------ planning
 struct Plan {
   int nw;  // waves = nq * ks
@@ -834,8 +1067,7 @@ extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, i
                              base, nullptr, keys, cnt, p.cap_s, nullptr, st);
     if (rc) return rc;
     RegionSource s1{keys, cnt, p.g_s, p.qpad, p.cap_s, 2 * p.ks};
-    hipLaunchKernelGGL((select_kernel<RegionSource>), dim3(Q), dim3(SEL_NT), 0, st, s1, (int)k,
-                       (int)SEL_THRESHOLD, thr, nullptr, nullptr);
+    launch_select(s1, (int)Q, (int)k, SEL_THRESHOLD, thr, nullptr, nullptr, st);
     if ((rc = check_launch("select_kernel(threshold)"))) return rc;
   }
   if (p.pp && ((uintptr_t)qs % 16) == 0 && ((uintptr_t)ds % 16) == 0) {
@@ -863,8 +1095,7 @@ extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, i
     prof_end("scan_filter", st, (double)N * D * 2 + (double)Q * D * 2);
     if ((rc = check_launch("gemm_pp_kernel(scan)"))) return rc;
     RegionSource s2{keys, cnt, p.pp_G, p.pp_qpad, p.pp_cap, 1};
-    hipLaunchKernelGGL((select_kernel<RegionSource>), dim3(Q), dim3(SEL_NT), 0, st, s2, (int)k,
-                       (int)SEL_FINAL, nullptr, out_score, out_idx);
+    launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, st);
     return check_launch("select_kernel(final)");
   }
   prof_begin(st);
@@ -873,8 +1104,7 @@ extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, i
   prof_end("scan_filter", st, (double)N * D * 2 + (double)Q * D * 2);  // algorithmic bytes
   if (rc) return rc;
   RegionSource s2{keys, cnt, p.g_f, p.qpad, p.cap_f, 2 * p.ks};
-  hipLaunchKernelGGL((select_kernel<RegionSource>), dim3(Q), dim3(SEL_NT), 0, st, s2, (int)k,
-                     (int)SEL_FINAL, nullptr, out_score, out_idx);
+  launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, st);
   return check_launch("select_kernel(final)");
 }
 
