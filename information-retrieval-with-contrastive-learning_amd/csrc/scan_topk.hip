@@ -31,6 +31,22 @@ namespace scan {
 
 constexpr int TD = 32;  // docs per tile (M of the 32x32x16 MFMA)
 
+#ifdef IRC_SCAN_STAMPS  // diagnostic build: phase timestamps of block 0 (s_memrealtime, 100 MHz)
+__device__ uint64_t dbg_stamps[4][32];
+#define STAMP(slot, i)                                                                   \
+  do {                                                                                   \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                                           \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                              \
+      volatile uint64_t* p_ = &dbg_stamps[slot][(i) + (int)(threadIdx.x & 0)];            \
+      *p_ = t_;                                                                          \
+    }                                                                                    \
+  } while (0)
+#else
+#define STAMP(slot, i) \
+  do {                 \
+  } while (0)
+#endif
+
 template <int D>
 struct Geo {
   static constexpr int CH = D / 8;                   // 16-byte chunks per row
@@ -43,7 +59,11 @@ struct Geo {
   static constexpr int KK = D / 16;                  // MFMA k-steps
 };
 
-enum Mode { KEYS = 0, SCORES = 1 };
+// KEYS: every key >= the threshold survives.  GMAX (the sample pass): each lane
+// keeps only the largest key of the JPW docs it finishes per tile -- the k-th
+// largest of these group maxima is still a lower bound of the true k-th key
+// (k distinct docs reach it), with 8-16x fewer keys to store and select.
+enum Mode { KEYS = 0, SCORES = 1, GMAX = 2 };
 
 // Opaque copy: stops LICM from hoisting per-lane address math out of the tile
 // loop (keeping 12+ 64-bit DMA addresses live costs more VGPRs than recomputing).
@@ -93,6 +113,7 @@ void scan_tile_kernel(
   const int worker = ((b >> 3) / GY) * 8 + (b & 7);
   const int q = qblock * (NQ * 32) + g * 32 + r32;
 
+  STAMP(thr == nullptr ? 2 : 3, 0);
   const int ntiles_total = (NS + TD - 1) / TD;
   const int t_begin = worker * tiles_per_worker;
   int t_end = t_begin + tiles_per_worker;
@@ -148,6 +169,9 @@ void scan_tile_kernel(
     }
   }
   const uint64_t qthr = (MODE == KEYS && thr != nullptr && q < Q) ? thr[q] : 0ull;
+  const uint32_t qthr_hi = (uint32_t)(qthr >> 32);
+  const float qtf = q >= Q ? __builtin_huge_valf()
+                           : (qthr_hi == 0 ? -__builtin_huge_valf() : unorderable_f32(qthr_hi));
   // LDS read offsets: chunk c = 2kk + h of row r32 lives at 16*(c ^ (r32 & SWZ));
   // the XOR only touches the low 4 bits, so 8 per-lane offsets + an immediate
   // 256*(kk>>3) cover all k-steps.
@@ -241,43 +265,74 @@ void scan_tile_kernel(
       for (int jj = 0; jj < 8; ++jj) fin[jj] = acc[jj + 8];
       joff = 8;
     }
+    // Survivors wait in a per-lane 4-key shift buffer and leave 4 at a time: a
+    // store is older than the DMAs issued after it and vmcnt retires in order,
+    // so every store episode delays a later tile's wait by its write-ack
+    // latency -- 4x fewer episodes.  Called by the whole wave (ballot).
+    auto push = [&](bool keep, uint64_t key) {
+      if (keep) {
+        sb3 = sb2;
+        sb2 = sb1;
+        sb1 = sb0;
+        sb0 = key;
+        ++sbn;
+      }
+      if (__ballot(sbn == 4)) {
+        nst += 4;
+        if (sbn == 4) {
+          myreg[nsurv] = sb0;
+          myreg[nsurv + 1] = sb1;
+          myreg[nsurv + 2] = sb2;
+          myreg[nsurv + 3] = sb3;
+          nsurv += 4;
+          sbn = 0;
+        }
+      }
+    };
+    if (MODE == SCORES) {
 #pragma unroll
-    for (int jj = 0; jj < JPW; ++jj) {
-      const int j = jj + joff;
-      const int s = s0row + (j & 3) + 8 * (j >> 2) + 4 * h;
-      const float v = fin[jj];
-      const bool ok = (q < Q) && (s < NS);
-      if (MODE == SCORES) {
-        if (ok) scores_out[(int64_t)q * NS + s] = v;
-      } else {
-        const uint32_t gidx = idx_base + (uint32_t)s * (uint32_t)stride;
-        const uint64_t key = make_key(v, gidx);
-        const bool keep = ok && key >= qthr;
+      for (int jj = 0; jj < JPW; ++jj) {
+        const int j = jj + joff;
+        const int s = s0row + (j & 3) + 8 * (j >> 2) + 4 * h;
+        if (q < Q && s < NS) scores_out[(int64_t)q * NS + s] = fin[jj];
+      }
+    } else if (MODE == GMAX) {
+      // the largest score of the lane's docs (first of equals) -> one real key
+      float bv = -__builtin_huge_valf();
+      int bs = -1;
+#pragma unroll
+      for (int jj = 0; jj < JPW; ++jj) {
+        const int j = jj + joff;
+        const int s = s0row + (j & 3) + 8 * (j >> 2) + 4 * h;
+        const bool better = (q < Q) && (s < NS) && fin[jj] > bv;
+        bv = better ? fin[jj] : bv;
+        bs = better ? s : bs;
+      }
+      push(bs >= 0, make_key(bv, idx_base + (uint32_t)bs * (uint32_t)stride));
+    } else {
+      // Float prefilter (key >= thr implies score >= qtf for non-NaN scores; NaN
+      // passes it and fails the exact test): a branch-free pass mask, and the
+      // exact key path only when some lane of the wave has a candidate.
+      uint32_t pm = 0;
+#pragma unroll
+      for (int jj = 0; jj < JPW; ++jj) pm |= (uint32_t)(!(fin[jj] < qtf)) << jj;
+      // set bits only: one candidate per lane per round (rounds = the wave's
+      // largest candidate count, usually 0 or 1)
+      while (__ballot(pm != 0)) {
+        const int b = pm != 0 ? __builtin_ctz(pm) : 0;
+        const bool cand = pm != 0;
+        pm &= pm - 1;
+        float v = fin[0];
+#pragma unroll
+        for (int jj = 1; jj < JPW; ++jj) v = b == jj ? fin[jj] : v;
+        const int j = b + joff;
+        const int s = s0row + (j & 3) + 8 * (j >> 2) + 4 * h;
+        const uint64_t key = make_key(v, idx_base + (uint32_t)s * (uint32_t)stride);
+        const bool keep = cand && (q < Q) && (s < NS) && key >= qthr;
 #ifdef IRC_SCAN_NO_STORE  // diagnostic build: survivors counted, never stored
         if (keep) ++nsurv;
 #else
-        // Survivors wait in a per-lane 4-key shift buffer and leave 4 at a time:
-        // a store is older than the DMAs issued after it and vmcnt retires in
-        // order, so every store episode delays a later tile's wait by its
-        // write-ack latency -- 4x fewer episodes.
-        if (keep) {
-          sb3 = sb2;
-          sb2 = sb1;
-          sb1 = sb0;
-          sb0 = key;
-          ++sbn;
-        }
-        if (__ballot(sbn == 4)) {
-          nst += 4;
-          if (sbn == 4) {
-            myreg[nsurv] = sb0;
-            myreg[nsurv + 1] = sb1;
-            myreg[nsurv + 2] = sb2;
-            myreg[nsurv + 3] = sb3;
-            nsurv += 4;
-            sbn = 0;
-          }
-        }
+        push(keep, key);
 #endif
       }
     }
@@ -286,14 +341,15 @@ void scan_tile_kernel(
     wg_barrier();  // all reads of this buffer (and of xbuf) done before reuse
   }
 
-  if (MODE == KEYS) {  // flush the shift buffer (newest first; order is irrelevant)
+  if (MODE != SCORES) {  // flush the shift buffer (newest first; order is irrelevant)
     if (sbn > 0) myreg[nsurv] = sb0;
     if (sbn > 1) myreg[nsurv + 1] = sb1;
     if (sbn > 2) myreg[nsurv + 2] = sb2;
     nsurv += (uint32_t)sbn;
   }
-  if (MODE == KEYS && q < Qpad)
+  if (MODE != SCORES && q < Qpad)
     counts[((int64_t)worker * Qpad + q) * (2 * KS) + slice] = nsurv;
+  STAMP(thr == nullptr ? 2 : 3, 1);
 }
 
 // ----------------------------------------------------------------- selection
@@ -354,17 +410,6 @@ constexpr int SEL_MAXR = 2048;   // region table size for the parallel staging p
 
 enum SelMode { SEL_THRESHOLD = 0, SEL_FINAL = 1 };
 
-// One workgroup per query.  Exact radix select (8-bit digits, MSB first) of the
-// k-th largest distinct key among the query's candidates, then collect + bitonic
-// sort of the winners.  SEL_THRESHOLD only needs a LOWER BOUND of the k-th key
-// (the filter keeps key >= bound), so it stops after the top 16 bits: bound =
-// (16-bit prefix of the k-th key) << 48 -- exact top-k is still guaranteed
-// because the FINAL pass selects exactly among everything >= bound.
-//
-// Fast path (region sources with <= SEL_STAGE candidates): counts of all
-// regions -> exclusive scan -> an LDS region-id map -> every candidate load is
-// independent (no dependent search per element) -> keys staged in LDS; the
-// radix passes start at the first bit where min and max key differ.
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -382,6 +427,91 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
   return v;
 }
 
+// Bitonic sort (descending) of the 64*E keys one wave holds in registers,
+// blocked: lane l owns indices l*E .. l*E+E-1.  Strides below E swap inside a
+// lane; wider ones exchange with lane ^ (stride / E) -- no LDS, no barrier.
+template <int E>
+__device__ __forceinline__ void wave_sort_desc(uint64_t (&v)[E], int lane) {
+  constexpr int n = 64 * E;
+#pragma unroll
+  for (int size = 2; size <= n; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride < E) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int ep = e ^ stride;
+          if (ep > e) {
+            const bool desc = ((lane * E + e) & size) == 0;
+            const uint64_t x = v[e], y = v[ep];
+            if (desc ? (x < y) : (x > y)) {
+              v[e] = y;
+              v[ep] = x;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = lane * E + e;
+          const uint64_t y = __shfl_xor(v[e], stride / E, 64);
+          // the lower index of a descending pair keeps the larger key
+          const bool keep_max = (((i & stride) == 0) == ((i & size) == 0));
+          const uint64_t hi = v[e] > y ? v[e] : y, lo = v[e] > y ? y : v[e];
+          v[e] = keep_max ? hi : lo;
+        }
+      }
+    }
+  }
+}
+
+// Wave 0 of the select: sort the npow (>= cnt) collected keys and write the k
+// outputs of query q (slots past cnt are empty: -inf / -1).
+template <int E>
+__device__ __forceinline__ void sort_and_emit(const uint64_t* cand, int cnt, int k, int q,
+                                              int lane, float* __restrict__ out_score,
+                                              int64_t* __restrict__ out_idx) {
+  uint64_t v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    v[e] = i < cnt ? cand[i] : 0ull;
+  }
+  wave_sort_desc<E>(v, lane);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane * E + e;
+    if (i < k) {
+      float sc = -__builtin_huge_valf();
+      int64_t id = -1;
+      if (i < cnt) {
+        sc = unorderable_f32((uint32_t)(v[e] >> 32));
+        id = (int64_t)(uint32_t)(~(uint32_t)v[e]);
+      }
+      out_score[(int64_t)q * k + i] = sc;
+      out_idx[(int64_t)q * k + i] = id;
+    }
+  }
+  for (int i = 64 * E + lane; i < k; i += 64) {
+    out_score[(int64_t)q * k + i] = -__builtin_huge_valf();
+    out_idx[(int64_t)q * k + i] = -1;
+  }
+}
+
+// One workgroup per query: the exact k-th largest distinct key among the
+// query's candidates by radix select, then the winners sorted.
+//  * Region sources: all region counts are loaded at once (each thread owns up
+//    to 8 consecutive regions), block-scanned, and turned into an LDS region-id
+//    map, so every candidate load is independent; the keys are staged in LDS
+//    (<= SEL_STAGE) and their min / max taken on the way.
+//  * Digits are 8 bits wide and start right below the candidates' common
+//    prefix (the highest bit where min and max differ), not at byte
+//    boundaries: the first pass already spreads the keys over the buckets.
+//    Early exit when the chosen bucket holds exactly the remaining rank.
+//  * SEL_THRESHOLD only needs a LOWER BOUND of the k-th key (the filter keeps
+//    key >= bound, so the FINAL pass still selects exactly): two passes, bound =
+//    the common prefix + 16 selected bits, lower bits zero.
+//  * The min(M, k) winners are sorted in registers by wave 0 (wave_sort_desc).
 template <class Src>
 __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode,
                                                          uint64_t* __restrict__ thr_out,
@@ -391,9 +521,11 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
   __shared__ uint64_t cand[SEL_MAXK];
   __shared__ uint64_t stage[SEL_STAGE];
   __shared__ uint16_t rid[SEL_STAGE];
-  __shared__ uint32_t roff[SEL_MAXR + 1];
+  __shared__ uint32_t roff[SEL_MAXR];
   __shared__ uint64_t s_mm[2][SEL_NW];
-  __shared__ uint32_t s_misc[4];  // 0: total count, 1: kr, 2: selected digit, 3: collect ctr
+  __shared__ uint32_t s_wsum[SEL_NW];
+  __shared__ uint32_t s_misc[4];  // 0: total count, 1: kr, 2: selected digit, 3: staging ctr
+  __shared__ uint32_t s_coll;     // collect counter
   __shared__ bool s_exact;
 
   const int q = blockIdx.x;
@@ -401,53 +533,67 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
   const int wave = tid >> 6;
   const int lane = tid & 63;
 
+  STAMP(mode, 0);
   if (tid == 0) {
     s_misc[0] = 0;
     s_misc[3] = 0;
+    s_coll = 0;
   }
-  __syncthreads();
   bool table = false;
+  uint32_t M = 0;
   if constexpr (Src::kRegions) {
     const int R = src.nregions();
     table = R <= SEL_MAXR;
     if (table) {
-      for (int r = tid; r < R; r += SEL_NT) roff[r + 1] = src.count(q, r);
-      __syncthreads();
-      if (wave == 0) {
-        uint32_t carry = 0;
-        for (int base = 0; base < R; base += 64) {
-          const int r = base + lane;
-          uint32_t v = r < R ? roff[r + 1] : 0;
+      const int rpt = (R + SEL_NT - 1) / SEL_NT;  // <= 8
+      uint32_t c[8];
+      uint32_t mine = 0;
 #pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = __shfl_up(v, o, 64);
-            if (lane >= o) v += t;
-          }
-          if (r < R) roff[r + 1] = carry + v;
-          carry += __shfl(v, 63, 64);
-        }
-        if (lane == 0) {
-          roff[0] = 0;
-          s_misc[0] = carry;
+      for (int u = 0; u < 8; ++u) {
+        const int r = tid * rpt + u;
+        c[u] = (u < rpt && r < R) ? src.count(q, r) : 0u;
+        mine += c[u];
+      }
+      uint32_t incl = mine;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      if (lane == 63) s_wsum[wave] = incl;
+      __syncthreads();
+      uint32_t off = incl - mine;
+#pragma unroll
+      for (int w = 0; w < SEL_NW; ++w) {
+        if (w < wave) off += s_wsum[w];
+        M += s_wsum[w];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = tid * rpt + u;
+        if (u < rpt && r < R) {
+          roff[r] = off;
+          if (M <= (uint32_t)SEL_STAGE)
+            for (uint32_t j = 0; j < c[u]; ++j) rid[off + j] = (uint16_t)r;
+          off += c[u];
         }
       }
-      __syncthreads();
     }
   }
   if (!table) {
+    __syncthreads();
     uint32_t c = 0;
     src.for_each(q, tid, SEL_NT, [&](uint64_t) { ++c; });
     atomicAdd(&s_misc[0], c);
     __syncthreads();
+    M = s_misc[0];
   }
-  const uint32_t M = s_misc[0];
   const bool staged = M <= (uint32_t)SEL_STAGE;
+  __syncthreads();
+  STAMP(mode, 1);
+  uint64_t mn = ~0ull, mx = 0;
   if (staged) {
     if (table) {
-      const int R = src.nregions();
-      for (int r = tid; r < R; r += SEL_NT)
-        for (uint32_t j = roff[r]; j < roff[r + 1]; ++j) rid[j] = (uint16_t)r;
-      __syncthreads();
       constexpr int U = 8;  // independent loads in flight per thread
       for (uint32_t i0 = tid; i0 < M; i0 += SEL_NT * U) {
         uint64_t v[U];
@@ -462,15 +608,20 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint32_t i = i0 + u * SEL_NT;
-          if (i < M) stage[i] = v[u];
+          if (i < M) {
+            stage[i] = v[u];
+            mn = v[u] < mn ? v[u] : mn;
+            mx = v[u] > mx ? v[u] : mx;
+          }
         }
       }
     } else {
-      src.for_each(q, tid, SEL_NT, [&](uint64_t key) { stage[atomicAdd(&s_misc[3], 1u)] = key; });
+      src.for_each(q, tid, SEL_NT, [&](uint64_t key) {
+        stage[atomicAdd(&s_misc[3], 1u)] = key;
+        mn = key < mn ? key : mn;
+        mx = key > mx ? key : mx;
+      });
     }
-    __syncthreads();
-    if (tid == 0) s_misc[3] = 0;
-    __syncthreads();
   }
   auto visit = [&](auto&& f) {
     if (staged) {
@@ -479,22 +630,25 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
       src.for_each(q, tid, SEL_NT, f);
     }
   };
-
-  uint64_t kth = 0;  // 0 = keep everything
-  if (M > (uint32_t)k) {
-    // common prefix of all candidates: start the digits at the first differing bit
-    uint64_t mn = ~0ull, mx = 0;
+  if (!staged && M > (uint32_t)k)
     visit([&](uint64_t key) {
       mn = key < mn ? key : mn;
       mx = key > mx ? key : mx;
     });
-    mn = wave_min_u64(mn);
-    mx = wave_max_u64(mx);
-    if (lane == 0) {
-      s_mm[0][wave] = mn;
-      s_mm[1][wave] = mx;
-    }
-    __syncthreads();
+  mn = wave_min_u64(mn);
+  mx = wave_max_u64(mx);
+  if (lane == 0) {
+    s_mm[0][wave] = mn;
+    s_mm[1][wave] = mx;
+  }
+  __syncthreads();
+  STAMP(mode, 2);
+#ifdef IRC_SCAN_STAMPS
+  if (blockIdx.x == 0 && tid == 0) *(volatile uint64_t*)&dbg_stamps[mode][21 + (tid & 0)] = M;
+#endif
+
+  uint64_t kth = 0;  // 0 = keep everything
+  if (M > (uint32_t)k) {
     mn = s_mm[0][0];
     mx = s_mm[1][0];
 #pragma unroll
@@ -503,20 +657,17 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
       mx = s_mm[1][w] > mx ? s_mm[1][w] : mx;
     }
     const int top = 63 - __builtin_clzll((mn ^ mx) | 1ull);  // highest differing bit
-    const int first_shift = (top / 8) * 8;
-    const int last_shift = (mode == SEL_THRESHOLD) ? 48 : 0;
-    uint64_t pmask = first_shift >= 56 ? 0ull : (~0ull << (first_shift + 8));
+    uint64_t pmask = top >= 63 ? 0ull : (~0ull << (top + 1));
     uint64_t prefix = mn & pmask;
-    if (tid == 0) {
-      s_misc[1] = (uint32_t)k;
-      s_exact = false;
-    }
-    __syncthreads();
-    for (int shift = first_shift; shift >= last_shift; shift -= 8) {
+    uint32_t kr = (uint32_t)k;
+    int hi = top;
+    for (int pass = 0;; ++pass) {
+      const int lo = hi >= 7 ? hi - 7 : 0;
+      const uint32_t dm = (2u << (hi - lo)) - 1u;  // digit = bits [lo, hi]
       for (int i = tid; i < SEL_NW * 256; i += SEL_NT) (&hist[0][0])[i] = 0;
       __syncthreads();
       visit([&](uint64_t key) {
-        if ((key & pmask) == prefix) atomicAdd(&hist[wave][(key >> shift) & 255], 1u);
+        if ((key & pmask) == prefix) atomicAdd(&hist[wave][(uint32_t)(key >> lo) & dm], 1u);
       });
       __syncthreads();
       if (wave == 0) {
@@ -529,15 +680,14 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
           for (int w = 0; w < SEL_NW; ++w) t += hist[w][4 * lane + j];
           bb[j] = t;
         }
-        const uint32_t mine = bb[0] + bb[1] + bb[2] + bb[3];
-        uint32_t suf = mine;
+        const uint32_t cnt4 = bb[0] + bb[1] + bb[2] + bb[3];
+        uint32_t suf = cnt4;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
           const uint32_t t = __shfl_down(suf, o, 64);
           if (lane + o < 64) suf += t;
         }
-        const uint32_t kr = s_misc[1];
-        const uint32_t above = suf - mine;  // count in digits of higher lanes
+        const uint32_t above = suf - cnt4;  // count in digits of higher lanes
         if (suf >= kr && above < kr) {
           uint32_t acc = above;
           int sel = 4 * lane, selc = 0;
@@ -555,16 +705,17 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
         }
       }
       __syncthreads();
-      prefix |= (uint64_t)s_misc[2] << shift;
-      pmask |= (uint64_t)0xff << shift;
-      // Early exit: when the chosen bucket holds exactly the remaining rank, every
-      // key with this prefix is selected, so prefix (lower bits zero) is a bound
-      // that admits exactly k keys -- the lower digits are not needed.
-      if (s_exact) break;
+      prefix |= (uint64_t)s_misc[2] << lo;
+      pmask |= (uint64_t)dm << lo;
+      kr = s_misc[1];
+      STAMP(mode, 4 + pass);
+      // Early exit: the chosen bucket holds exactly the remaining rank, so every
+      // key with this prefix is selected and prefix (lower bits zero) admits
+      // exactly k keys.  THRESHOLD stops after two digits (a lower bound).
+      if (s_exact || lo == 0 || (mode == SEL_THRESHOLD && pass == 1)) break;
+      hi = lo - 1;  // (wave 0 rewrites s_misc only two barriers later)
     }
-    // THRESHOLD: bits below 48 of `prefix` are zero unless the candidates share
-    // their top 16 bits; mask them so the bound is the 16-bit prefix << 48.
-    kth = (mode == SEL_THRESHOLD) ? (prefix & (~0ull << 48)) : prefix;
+    kth = prefix;
   }
 
   if (mode == SEL_THRESHOLD) {
@@ -572,47 +723,25 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
     return;
   }
 
+  STAMP(mode, 12);
   // collect the (exactly min(M, k)) keys >= kth
   const int cnt = (int)(M < (uint32_t)k ? M : (uint32_t)k);
-  int npow = 1;
-  while (npow < cnt) npow <<= 1;
-  for (int i = tid; i < npow; i += SEL_NT) cand[i] = 0;
-  __syncthreads();
   visit([&](uint64_t key) {
     if (key >= kth) {
-      const uint32_t slot = atomicAdd(&s_misc[3], 1u);
+      const uint32_t slot = atomicAdd(&s_coll, 1u);
       if (slot < (uint32_t)SEL_MAXK) cand[slot] = key;
     }
   });
   __syncthreads();
-  // bitonic sort, descending
-  for (int size = 2; size <= npow; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < npow; i += SEL_NT) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const bool desc = ((i & size) == 0);
-          const uint64_t x = cand[i], y = cand[j];
-          if (desc ? (x < y) : (x > y)) {
-            cand[i] = y;
-            cand[j] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
+  STAMP(mode, 13);
+  if (wave == 0) {
+    if (cnt <= 64) sort_and_emit<1>(cand, cnt, k, q, lane, out_score, out_idx);
+    else if (cnt <= 128) sort_and_emit<2>(cand, cnt, k, q, lane, out_score, out_idx);
+    else if (cnt <= 256) sort_and_emit<4>(cand, cnt, k, q, lane, out_score, out_idx);
+    else if (cnt <= 512) sort_and_emit<8>(cand, cnt, k, q, lane, out_score, out_idx);
+    else sort_and_emit<16>(cand, cnt, k, q, lane, out_score, out_idx);
   }
-  for (int i = tid; i < k; i += SEL_NT) {
-    float sc = -__builtin_huge_valf();
-    int64_t id = -1;
-    if (i < cnt) {
-      const uint64_t key = cand[i];
-      sc = unorderable_f32((uint32_t)(key >> 32));
-      id = (int64_t)(uint32_t)(~(uint32_t)key);
-    }
-    out_score[(int64_t)q * k + i] = sc;
-    out_idx[(int64_t)q * k + i] = id;
-  }
+  STAMP(mode, 14);
 }
 
 // Wave-per-query select for region sources (the scan's two selects): the same
@@ -935,8 +1064,13 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k) {
   p.gy = (int)((Q + qb - 1) / qb);
   if (p.gy < 1) p.gy = 1;
   p.qpad = p.gy * qb;
-  int64_t s_target = 16 * k;
-  if (N / 16 > s_target) s_target = N / 16;
+  // Sample of N/8 docs (>= 32k; GMAX leaves 2*KS keys per 32-doc tile, so >= 2k
+  // group maxima per query for the threshold select, capped at its LDS stage).
+  // The filter's survivors ~ k * N / S (~8k per query).
+  int64_t s_target = 32 * k;
+  if (N / 8 > s_target) s_target = N / 8;
+  const int64_t s_cap = (int64_t)SEL_STAGE * TD / (2 * p.ks);
+  if (s_target > s_cap) s_target = s_cap;
   p.stride = s_target > 0 ? N / s_target : 1;
   if (p.stride < 1) p.stride = 1;
   p.two_phase = p.stride > 1;
@@ -1023,6 +1157,17 @@ static bool supported_d(int64_t D) {
 using namespace irc;
 using namespace irc::scan;
 
+// Diagnostic builds only (-DIRC_SCAN_STAMPS): copy the phase stamps out.
+extern "C" int irc_scan_dbg_stamps(uint64_t* out /* [4][32] */) {
+#ifdef IRC_SCAN_STAMPS
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(dbg_stamps), sizeof(dbg_stamps)) == hipSuccess ? 0 : -1;
+#else
+  (void)out;
+  return -1;
+#endif
+}
+
 extern "C" int64_t irc_scan_topk_workspace(int64_t Q, int64_t N, int64_t D, int64_t k) {
   if (Q <= 0 || N <= 0 || k <= 0) return 256;
   return (int64_t)make_plan(Q, N, D, k).bytes;
@@ -1063,7 +1208,7 @@ extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, i
   const uint32_t base = (uint32_t)doc_offset;
   int rc;
   if (p.two_phase) {
-    rc = dispatch_tile<KEYS>(D, p, p.g_s, qs, ds, (int)Q, p.S, p.stride, p.tpw_s,
+    rc = dispatch_tile<GMAX>(D, p, p.g_s, qs, ds, (int)Q, p.S, p.stride, p.tpw_s,
                              base, nullptr, keys, cnt, p.cap_s, nullptr, st);
     if (rc) return rc;
     RegionSource s1{keys, cnt, p.g_s, p.qpad, p.cap_s, 2 * p.ks};

@@ -1,0 +1,56 @@
+"""Diagnostic: phase timestamps of the scan's kernels (block 0), from a library
+built with -DIRC_SCAN_STAMPS (make EXTRA=-DIRC_SCAN_STAMPS OUT=... OBJDIR=...),
+loaded through IRC_LIB_PATH.
+
+    IRC_LIB_PATH=.../libirc_hip_stamps.so python tools/scan_stamps.py --q 1 256 --k 100
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "information-retrieval-with-contrastive-learning_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+NAMES = {0: "select(threshold)", 1: "select(final)", 2: "tile kernel (sample)", 3: "tile kernel (filter)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=100_000)
+    ap.add_argument("--d", type=int, default=768)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--q", type=int, nargs="*", default=[1, 256])
+    args = ap.parse_args()
+    from irc_amd import _lib, retrieval
+
+    lib = _lib.load()
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(2024)
+    docs = torch.nn.functional.normalize(torch.randn(args.n, args.d, generator=g)).bfloat16().to(dev)
+    buf = np.zeros((4, 32), dtype=np.uint64)
+    for q in args.q:
+        qq = torch.nn.functional.normalize(torch.randn(q, args.d, generator=g)).bfloat16().to(dev)
+        for _ in range(5):
+            buf[:] = 0
+            lib.irc_scan_dbg_stamps(buf.ctypes.data_as(ctypes.c_void_p))  # clears nothing; read
+            retrieval.scan_topk(qq, docs, args.k)
+        torch.cuda.synchronize()
+        rc = lib.irc_scan_dbg_stamps(buf.ctypes.data_as(ctypes.c_void_p))
+        assert rc == 0, "library not built with -DIRC_SCAN_STAMPS"
+        print(f"--- Q={q} k={args.k}")
+        for slot in range(4):
+            row = buf[slot].astype(np.int64)
+            t0 = row[0]
+            if t0 == 0:
+                continue
+            pts = [(i, (row[i] - t0) / 100.0) for i in range(1, 20) if row[i] > 0 and row[i] >= t0]
+            extra = f"  M={row[21]}" if slot < 2 else ""
+            print(f"{NAMES[slot]:22s}" + " ".join(f"[{i}]{us:6.2f}" for i, us in pts) + extra)
+
+
+if __name__ == "__main__":
+    main()
