@@ -66,6 +66,28 @@ int irc_topk_merge(const float* in_score, const int64_t* in_idx, int64_t P, int6
 int irc_scan_scores(const void* queries, const void* docs, int64_t Q, int64_t N, int64_t D,
                     float* out, irc_stream_t stream);
 
+/* fp8 (e4m3fn) corpus scan: the same exact top-k as irc_scan_topk over e4m3
+ * queries [Q][D] and docs [N][D] (16-byte aligned rows), products exact, fp32
+ * accumulation; returned scores are the raw dot products times score_scale (a
+ * power of two, e.g. 1/(s_q*s_d) for quantisation scales s_q, s_d), so the
+ * ranking is that of the quantised embeddings.  The fp8 form of BASELINE
+ * config C5 ("fp8 ... 5M docs"); replaces the same dense scoring
+ * (src/evaluation.py:110-112, tfidf_doc_ranker.py:60-75 ranking) as
+ * irc_scan_topk. */
+int64_t irc_scan_topk_fp8_workspace(int64_t Q, int64_t N, int64_t D, int64_t k);
+int irc_scan_topk_fp8(const void* queries, const void* docs, int64_t Q, int64_t N, int64_t D,
+                      int64_t k, int64_t doc_offset, float score_scale, void* workspace,
+                      int64_t workspace_bytes, float* out_score, int64_t* out_idx,
+                      irc_stream_t stream);
+/* raw fp32 dot products of e4m3 queries and docs (the fp8 filter's arithmetic) */
+int irc_scan_scores_fp8(const void* queries, const void* docs, int64_t Q, int64_t N, int64_t D,
+                        float* out, irc_stream_t stream);
+/* out[i] = e4m3fn(round-to-nearest-even(x[i] * scale)), saturated to +-448;
+ * in_dtype 0 = bf16, 1 = fp32.  Used to store a corpus shard and its queries
+ * in fp8 (ShardedDenseIndex(dtype="fp8")). */
+int irc_quantize_fp8(int in_dtype, const void* x, int64_t n, float scale, void* out,
+                     irc_stream_t stream);
+
 /* ---------------------------------------------------------------- GEMM
  * C[M,N] (=|+=) alpha * op(A) . op(B) (+bias[N]) (->GELU) (+R[M,N]), batched.
  * Replaces the cuBLAS GEMMs behind nn.Linear / torch.matmul on the path: BERT

@@ -44,6 +44,20 @@ enum Epi {
 namespace gpp {
 using namespace irc::gemm;
 
+#ifdef IRC_SCAN_STAMPS  // diagnostic build: EPI_SCAN phase stamps of block 0 (s_memrealtime)
+__device__ uint64_t pp_stamps[16];
+#define PSTAMP(i)                                                              \
+  do {                                                                         \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                   \
+      *(volatile uint64_t*)&pp_stamps[(i) + (int)(threadIdx.x & 0)] =          \
+          __builtin_amdgcn_s_memrealtime();                                    \
+  } while (0)
+#else
+#define PSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
+
 constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
 // K-outer half-tile image: 16 blocks of 4 k-rows, each block = [16 column chunks]
 // [4 k-rows][16 B] (1 KB) + a 64-B pad (BPITCH).  One DMA wave-instruction fills
@@ -182,6 +196,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
       stage_half<false>(B, g.ldb, n0 + 128 * grp, g.N, k0, base + 2 * SA + grp * SB, wq, lane);
   };
 
+  if (EPI == EPI_SCAN) PSTAMP(0);
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -235,6 +250,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
     // rows = queries, cols = docs.  LDS is free (every wave is past its last
     // fragment read): per-query survivor counters + thresholds (key and its float
     // prefilter: key >= thr implies score >= float(thr >> 32) for non-NaN scores).
+    PSTAMP(1);
     uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
     uint64_t* thk = reinterpret_cast<uint64_t*>(lds + 1024);
     float* thf = reinterpret_cast<float*>(lds + 3072);
@@ -276,6 +292,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
           pm[bit >> 6] |= (uint64_t)(!(acc[i][j][e] < tf[e])) << (bit & 63);
         }
     }
+    PSTAMP(2);
 #ifdef IRC_PP_SCAN_MASKONLY  // diagnostic build: mask, no exact path
     if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
       g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = __popcll(pm[0] | pm[1]) == 999 ? 1u : 0u;
@@ -309,7 +326,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
         }
       }
     }
+    PSTAMP(3);
     __syncthreads();
+    PSTAMP(4);
     if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
       g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = cnt[threadIdx.x];
     return;
@@ -488,6 +507,16 @@ static void launch_epi(int epi, const PArgs& a, dim3 grid, hipStream_t st) {
 
 template <typename TO>
 static void launch_layout(int la, int lb, int epi, const PArgs& a, dim3 grid, hipStream_t st);
+
+extern "C" int irc_pp_dbg_stamps(uint64_t* out /* [16] */) {
+#ifdef IRC_SCAN_STAMPS
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(pp_stamps), sizeof(pp_stamps)) == hipSuccess ? 0 : -1;
+#else
+  (void)out;
+  return -1;
+#endif
+}
 
 void run_scan(const PArgs& a, hipStream_t st) {
   const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);

@@ -47,6 +47,29 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
+// vmcnt(n) for a wave-uniform run-time n (clamped to 63: waiting for more is safe).
+__device__ __forceinline__ void wait_vmcnt_n(int n) {
+#define IRC_VMN(E) \
+  case E:          \
+    wait_vmcnt<E>(); \
+    return;
+  switch (n < 63 ? n : 63) {
+    IRC_VMN(0) IRC_VMN(1) IRC_VMN(2) IRC_VMN(3) IRC_VMN(4) IRC_VMN(5) IRC_VMN(6) IRC_VMN(7)
+    IRC_VMN(8) IRC_VMN(9) IRC_VMN(10) IRC_VMN(11) IRC_VMN(12) IRC_VMN(13) IRC_VMN(14)
+    IRC_VMN(15) IRC_VMN(16) IRC_VMN(17) IRC_VMN(18) IRC_VMN(19) IRC_VMN(20) IRC_VMN(21)
+    IRC_VMN(22) IRC_VMN(23) IRC_VMN(24) IRC_VMN(25) IRC_VMN(26) IRC_VMN(27) IRC_VMN(28)
+    IRC_VMN(29) IRC_VMN(30) IRC_VMN(31) IRC_VMN(32) IRC_VMN(33) IRC_VMN(34) IRC_VMN(35)
+    IRC_VMN(36) IRC_VMN(37) IRC_VMN(38) IRC_VMN(39) IRC_VMN(40) IRC_VMN(41) IRC_VMN(42)
+    IRC_VMN(43) IRC_VMN(44) IRC_VMN(45) IRC_VMN(46) IRC_VMN(47) IRC_VMN(48) IRC_VMN(49)
+    IRC_VMN(50) IRC_VMN(51) IRC_VMN(52) IRC_VMN(53) IRC_VMN(54) IRC_VMN(55) IRC_VMN(56)
+    IRC_VMN(57) IRC_VMN(58) IRC_VMN(59) IRC_VMN(60) IRC_VMN(61) IRC_VMN(62)
+    default:
+      wait_vmcnt<63>();
+      return;
+  }
+#undef IRC_VMN
+}
+
 // vmcnt(ahead*PW + extra) with ahead in {0,1,2} and a run-time extra in [0, 32]:
 // s_waitcnt takes an immediate, so dispatch over the small range (counts above
 // 63 clamp, which only waits for more).

@@ -18,7 +18,10 @@
 //    the exact top-k and the result is exact for any input, ties included.
 //  * select_kernel: one workgroup per query, exact radix select (8 x 8-bit
 //    digits) of the k-th key, then a bitonic sort of the k winners.
+#include <math.h>
 #include <stdio.h>
+
+#include <cmath>
 
 #include "gemm_pp.h"
 
@@ -47,16 +50,24 @@ __device__ uint64_t dbg_stamps[4][32];
   } while (0)
 #endif
 
-template <int D>
+// Tile geometry for embeddings of D elements of EB bytes (2: bf16, 1: fp8 e4m3).
+// The chunk XOR is confined to the low bits that divide a k-slice's chunk count,
+// so the per-slice read offsets stay base + immediate.
+template <int D, int EB = 2>
 struct Geo {
-  static constexpr int CH = D / 8;                   // 16-byte chunks per row
-  static constexpr int LOWBIT = CH & (-CH);
+  static constexpr int KS = D > 512 ? 2 : 1;
+  static constexpr int CH = D * EB / 16;             // 16-byte chunks per row
+  static constexpr int LOWBIT = (CH / KS) & (-(CH / KS));
   static constexpr int SWZ = (LOWBIT < 16 ? LOWBIT : 16) - 1;
-  static constexpr int TILE_BYTES = TD * D * 2;
+  static constexpr int TILE_BYTES = TD * D * EB;
   static constexpr int GLDS_PER_TILE = TD * CH / 64;  // wave-instructions per tile
   static constexpr int XBUF_BYTES = (D > 512) ? 4 * 4096 : 0;  // KS=2 exchange (NQ <= 4)
-  static constexpr int NBUF = ((IRC_LDS_BYTES - XBUF_BYTES) / TILE_BYTES) >= 3 ? 3 : 2;
-  static constexpr int KK = D / 16;                  // MFMA k-steps
+  // ring depth: 3 x 48 KB for bf16 D=768; fp8 tiles are half as large, so the
+  // ring goes deeper (same bytes in flight)
+  static constexpr int NBMAX = EB == 1 ? 5 : 3;
+  static constexpr int NFIT = (IRC_LDS_BYTES - XBUF_BYTES) / TILE_BYTES;
+  static constexpr int NBUF = NFIT >= NBMAX ? NBMAX : (NFIT >= 3 ? 3 : 2);
+  static constexpr int KK = D / 16;                  // MFMA k-steps (K = 16 for both types)
 };
 
 // KEYS: every key >= the threshold survives.  GMAX (the sample pass): each lane
@@ -87,16 +98,21 @@ __device__ __forceinline__ int opaque(int x) {
 // for j in its half of [0, 16) of every tile, for query (g, r32).  It owns the
 // private slice (kh*2 + h) of the (worker, query) region and counts in a
 // register -- no atomics, nothing that could drain the LDS-DMA ring.
-template <int D, int NQ, int KS, int MODE>
+// EB = 1: e4m3 embeddings on v_mfma_f32_32x32x16_fp8_fp8.  A 16-byte chunk then
+// holds two k-steps (low 8 bytes: step 2c, high: step 2c+1); queries and docs use
+// the same k order, so the dot product is unchanged.
+template <int D, int NQ, int KS, int MODE, int EB = 2>
 __global__ __launch_bounds__(NQ * KS * 64) __attribute__((amdgpu_waves_per_eu(1, 4)))
 void scan_tile_kernel(
-    const unsigned short* __restrict__ queries, const unsigned short* __restrict__ docs, int Q,
+    const unsigned char* __restrict__ queries, const unsigned char* __restrict__ docs, int Q,
     int Qpad, int GY, int NS, int stride, int tiles_per_worker, uint32_t idx_base,
     const uint64_t* __restrict__ thr, uint64_t* __restrict__ keys, uint32_t* __restrict__ counts,
     int64_t cap, float* __restrict__ scores_out) {
-  using G = Geo<D>;
+  using G = Geo<D, EB>;
+  static_assert(G::KS == KS, "k-slices");
   constexpr int NW = NQ * KS;
   constexpr int KKW = G::KK / KS;  // k-steps per wave
+  constexpr int NCW = KKW * EB / 2;  // 16-byte fragment chunks per wave per tile
   constexpr int JPW = 16 / KS;     // accumulator registers each wave finishes
   constexpr int PW = (G::GLDS_PER_TILE + NW - 1) / NW;  // glds per wave per tile (upper bound)
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -123,7 +139,7 @@ void scan_tile_kernel(
   // Per-lane byte offsets (within a tile) of this wave's PW DMA pieces; a piece
   // i covers LDS bytes [1024 i, 1024 i + 1024) of the lane-linear image, lane l
   // the 16 bytes at 1024 i + 16 l, sourced from (row, chunk ^ (row & SWZ)).
-  const int64_t row_bytes = (int64_t)stride * D * 2;
+  const int64_t row_bytes = (int64_t)stride * D * EB;
   uint32_t goff[PW];
   int grow[PW];
 #pragma unroll
@@ -156,16 +172,18 @@ void scan_tile_kernel(
   for (int bb = 0; bb < G::NBUF - 1; ++bb)
     if (bb < my_tiles) issue_tile(t_begin + bb, bb);
 
-  // Stationary B fragments: lane holds Q[q][kk*16 + 8h .. +8] for its k-steps.
-  bf16x8 bq[KKW];
+  // Stationary B fragments: lane holds chunk 2c + h of its query row (of its
+  // k-slice) for every c -- the same chunks it reads of each doc row.
+  u16x8 bq[NCW];
   {
     const bool qv = q < Q;
-    const unsigned short* qrow = queries + (int64_t)(qv ? q : 0) * D + 8 * h + kh * (D / KS);
+    const unsigned char* qrow =
+        queries + (int64_t)(qv ? q : 0) * D * EB + 16 * h + kh * (D * EB / KS);
 #pragma unroll
-    for (int kk = 0; kk < KKW; ++kk) {
-      u16x8 v = *reinterpret_cast<const u16x8*>(qrow + kk * 16);
+    for (int c = 0; c < NCW; ++c) {
+      u16x8 v = *reinterpret_cast<const u16x8*>(qrow + c * 32);
       if (!qv) v = (u16x8)0;
-      bq[kk] = __builtin_bit_cast(bf16x8, v);
+      bq[c] = v;
     }
   }
   const uint64_t qthr = (MODE == KEYS && thr != nullptr && q < Q) ? thr[q] : 0ull;
@@ -184,10 +202,10 @@ void scan_tile_kernel(
   uint32_t nsurv = 0;
   uint64_t sb0 = 0, sb1 = 0, sb2 = 0, sb3 = 0;  // survivor shift buffer (KEYS mode)
   int sbn = 0;
-  // Survivor store instructions issued by this wave in the last two tiles
-  // (wave-uniform).  They sit between the ring's DMAs in vmcnt order, so the
-  // wait for tile `it` allows them as extra younger operations.
-  int nst1 = 0, nst2 = 0;
+  // Survivor store instructions issued by this wave in each of the last NBUF-1
+  // tiles, one byte per tile (wave-uniform).  They sit between the ring's DMAs in
+  // vmcnt order, so the wait for tile `it` allows them as extra younger operations.
+  uint64_t nst_hist = 0;
   const int slice = kh * 2 + h;  // private output slice (of 2*KS)
   uint64_t* myreg = keys + ((int64_t)worker * Qpad + q) * cap + slice * (cap / (2 * KS));
 
@@ -195,28 +213,40 @@ void scan_tile_kernel(
     const int tile = t_begin + it;
     if (it + G::NBUF - 1 < my_tiles) issue_tile(tile + G::NBUF - 1, (it + G::NBUF - 1) % G::NBUF);
     const int after = my_tiles - 1 - it;
-    const int ahead = (G::NBUF == 3 && after >= 2) ? 2 : (after >= 1 ? 1 : 0);
-    int extra = G::NBUF == 3 ? nst1 + nst2 : nst1;
-    extra = __builtin_amdgcn_readfirstlane(extra < 15 ? extra : 15);  // smaller = safe
-    wait_vmcnt_dyn<PW>(ahead, extra);
+    const int ahead = after < G::NBUF - 1 ? after : G::NBUF - 1;
+    int extra = 0;
+#pragma unroll
+    for (int t = 0; t < G::NBUF - 1; ++t) extra += (int)((nst_hist >> (8 * t)) & 0xff);
+    extra = extra < 15 ? extra : 15;  // smaller = safe
+    wait_vmcnt_n(__builtin_amdgcn_readfirstlane(ahead == 0 ? 0 : ahead * PW + extra));
     wg_barrier();  // every wave's share of the tile has landed
 
 #ifdef IRC_SCAN_DMA_ONLY  // diagnostic build: the corpus stream alone
     wg_barrier();
     continue;
 #endif
-    const char* tb = smem + (it % G::NBUF) * G::TILE_BYTES + kh * (D / KS) * 2;
+    const char* tb = smem + (it % G::NBUF) * G::TILE_BYTES + kh * (D * EB / KS);
     f32x16 acc = (f32x16)0.0f;
     {
-      // every A fragment of the tile first (one LDS latency, not KKW of them:
+      // every A fragment of the tile first (one LDS latency, not NCW of them:
       // with one wave per SIMD nothing else hides it), then the MFMA chain
-      bf16x8 af[KKW];
+      u16x8 af[NCW];
 #pragma unroll
-      for (int kk = 0; kk < KKW; ++kk)
-        af[kk] = *reinterpret_cast<const bf16x8*>(tb + lo[kk & 7] + 256 * (kk >> 3));
+      for (int c = 0; c < NCW; ++c)
+        af[c] = *reinterpret_cast<const u16x8*>(tb + lo[c & 7] + 256 * (c >> 3));
 #pragma unroll
-      for (int kk = 0; kk < KKW; ++kk)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk], bq[kk], acc, 0, 0, 0);
+      for (int c = 0; c < NCW; ++c) {
+        if constexpr (EB == 2) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[c]),
+                                                        __builtin_bit_cast(bf16x8, bq[c]), acc,
+                                                        0, 0, 0);
+        } else {
+          typedef long l2 __attribute__((ext_vector_type(2)));
+          const l2 a2 = __builtin_bit_cast(l2, af[c]), b2 = __builtin_bit_cast(l2, bq[c]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a2[0], b2[0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a2[1], b2[1], acc, 0, 0, 0);
+        }
+      }
     }
 #ifdef IRC_SCAN_MFMA_ONLY  // diagnostic build
     if (acc[0] == 12345.f) myreg[0] = 1;  // keep the MFMAs alive
@@ -336,8 +366,7 @@ void scan_tile_kernel(
 #endif
       }
     }
-    nst2 = nst1;
-    nst1 = nst;
+    nst_hist = (nst_hist << 8) | (uint64_t)(nst < 255 ? nst : 255);
     wg_barrier();  // all reads of this buffer (and of xbuf) done before reuse
   }
 
@@ -469,7 +498,7 @@ __device__ __forceinline__ void wave_sort_desc(uint64_t (&v)[E], int lane) {
 // outputs of query q (slots past cnt are empty: -inf / -1).
 template <int E>
 __device__ __forceinline__ void sort_and_emit(const uint64_t* cand, int cnt, int k, int q,
-                                              int lane, float* __restrict__ out_score,
+                                              int lane, float smul, float* __restrict__ out_score,
                                               int64_t* __restrict__ out_idx) {
   uint64_t v[E];
 #pragma unroll
@@ -485,7 +514,7 @@ __device__ __forceinline__ void sort_and_emit(const uint64_t* cand, int cnt, int
       float sc = -__builtin_huge_valf();
       int64_t id = -1;
       if (i < cnt) {
-        sc = unorderable_f32((uint32_t)(v[e] >> 32));
+        sc = unorderable_f32((uint32_t)(v[e] >> 32)) * smul;
         id = (int64_t)(uint32_t)(~(uint32_t)v[e]);
       }
       out_score[(int64_t)q * k + i] = sc;
@@ -512,11 +541,13 @@ __device__ __forceinline__ void sort_and_emit(const uint64_t* cand, int cnt, int
 //    key >= bound, so the FINAL pass still selects exactly): two passes, bound =
 //    the common prefix + 16 selected bits, lower bits zero.
 //  * The min(M, k) winners are sorted in registers by wave 0 (wave_sort_desc).
+// smul: power-of-two factor applied to the returned scores (fp8 descale).
 template <class Src>
 __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode,
                                                          uint64_t* __restrict__ thr_out,
                                                          float* __restrict__ out_score,
-                                                         int64_t* __restrict__ out_idx) {
+                                                         int64_t* __restrict__ out_idx,
+                                                         float smul) {
   __shared__ uint32_t hist[SEL_NW][256];
   __shared__ uint64_t cand[SEL_MAXK];
   __shared__ uint64_t stage[SEL_STAGE];
@@ -735,11 +766,11 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
   __syncthreads();
   STAMP(mode, 13);
   if (wave == 0) {
-    if (cnt <= 64) sort_and_emit<1>(cand, cnt, k, q, lane, out_score, out_idx);
-    else if (cnt <= 128) sort_and_emit<2>(cand, cnt, k, q, lane, out_score, out_idx);
-    else if (cnt <= 256) sort_and_emit<4>(cand, cnt, k, q, lane, out_score, out_idx);
-    else if (cnt <= 512) sort_and_emit<8>(cand, cnt, k, q, lane, out_score, out_idx);
-    else sort_and_emit<16>(cand, cnt, k, q, lane, out_score, out_idx);
+    if (cnt <= 64) sort_and_emit<1>(cand, cnt, k, q, lane, smul, out_score, out_idx);
+    else if (cnt <= 128) sort_and_emit<2>(cand, cnt, k, q, lane, smul, out_score, out_idx);
+    else if (cnt <= 256) sort_and_emit<4>(cand, cnt, k, q, lane, smul, out_score, out_idx);
+    else if (cnt <= 512) sort_and_emit<8>(cand, cnt, k, q, lane, smul, out_score, out_idx);
+    else sort_and_emit<16>(cand, cnt, k, q, lane, smul, out_score, out_idx);
   }
   STAMP(mode, 14);
 }
@@ -765,7 +796,8 @@ __global__ __launch_bounds__(64 * SWQ) void select_wave_kernel(RegionSource src,
                                                                int mode,
                                                                uint64_t* __restrict__ thr_out,
                                                                float* __restrict__ out_score,
-                                                               int64_t* __restrict__ out_idx) {
+                                                               int64_t* __restrict__ out_idx,
+                                                               float smul) {
   __shared__ uint64_t stage_all[SWQ][SW];
   __shared__ uint32_t hist_all[SWQ][256];
   __shared__ uint16_t rid_all[SWQ][SW];
@@ -947,7 +979,7 @@ __global__ __launch_bounds__(64 * SWQ) void select_wave_kernel(RegionSource src,
     int64_t id = -1;
     if (i < cnt) {
       const uint64_t key = cand[i];
-      sc = unorderable_f32((uint32_t)(key >> 32));
+      sc = unorderable_f32((uint32_t)(key >> 32)) * smul;
       id = (int64_t)(uint32_t)(~(uint32_t)key);
     }
     out_score[(int64_t)q * k + i] = sc;
@@ -968,13 +1000,13 @@ static bool wave_select() {
 }
 
 static void launch_select(const RegionSource& src, int Q, int k, int mode, uint64_t* thr,
-                          float* out_score, int64_t* out_idx, hipStream_t st) {
+                          float* out_score, int64_t* out_idx, float smul, hipStream_t st) {
   if (wave_select())
     hipLaunchKernelGGL(select_wave_kernel, dim3((unsigned)((Q + SWQ - 1) / SWQ)), dim3(64 * SWQ),
-                       0, st, src, Q, k, mode, thr, out_score, out_idx);
+                       0, st, src, Q, k, mode, thr, out_score, out_idx, smul);
   else
     hipLaunchKernelGGL((select_kernel<RegionSource>), dim3((unsigned)Q), dim3(SEL_NT), 0, st, src,
-                       k, mode, thr, out_score, out_idx);
+                       k, mode, thr, out_score, out_idx, smul);
 }
 
 // ------------------------------------------------------------------ planning
@@ -1019,27 +1051,31 @@ static int pick_nq(int64_t D, int64_t Q) {
   return p;
 }
 
-template <int D>
+template <int D, int EB>
 static size_t tile_lds_bytes() {
-  return (size_t)Geo<D>::NBUF * Geo<D>::TILE_BYTES + Geo<D>::XBUF_BYTES;
+  return (size_t)Geo<D, EB>::NBUF * Geo<D, EB>::TILE_BYTES + Geo<D, EB>::XBUF_BYTES;
 }
 
-static size_t lds_bytes_for(int64_t D) {
+template <int EB>
+static size_t lds_bytes_eb(int64_t D) {
   switch (D) {
-    case 64: return tile_lds_bytes<64>();
-    case 128: return tile_lds_bytes<128>();
-    case 256: return tile_lds_bytes<256>();
-    case 384: return tile_lds_bytes<384>();
-    case 512: return tile_lds_bytes<512>();
-    case 768: return tile_lds_bytes<768>();
-    default: return tile_lds_bytes<1024>();
+    case 64: return tile_lds_bytes<64, EB>();
+    case 128: return tile_lds_bytes<128, EB>();
+    case 256: return tile_lds_bytes<256, EB>();
+    case 384: return tile_lds_bytes<384, EB>();
+    case 512: return tile_lds_bytes<512, EB>();
+    case 768: return tile_lds_bytes<768, EB>();
+    default: return tile_lds_bytes<1024, EB>();
   }
+}
+static size_t lds_bytes_for(int64_t D, int eb) {
+  return eb == 1 ? lds_bytes_eb<1>(D) : lds_bytes_eb<2>(D);
 }
 
 // Workers own contiguous tile ranges; the worker count is a multiple of 8 so the
 // XCD-aware block decode in scan_tile_kernel is a bijection.
-static void plan_workers(int64_t ntiles, int gy, int64_t D, int nw, int* g, int* tpw) {
-  int per_cu = (int)(IRC_LDS_BYTES / lds_bytes_for(D));
+static void plan_workers(int64_t ntiles, int gy, int64_t D, int eb, int nw, int* g, int* tpw) {
+  int per_cu = (int)(IRC_LDS_BYTES / lds_bytes_for(D, eb));
   const int by_waves = 16 / nw > 0 ? 16 / nw : 1;  // keep <= 16 waves per CU
   if (per_cu > by_waves) per_cu = by_waves;
   if (per_cu < 1) per_cu = 1;
@@ -1055,7 +1091,7 @@ static void plan_workers(int64_t ntiles, int gy, int64_t D, int nw, int* g, int*
   *g = (int)gg;
 }
 
-static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k) {
+static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   Plan p{};
   p.ks = pick_ks(D);
   p.nq = pick_nq(D, Q);
@@ -1075,9 +1111,9 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k) {
   if (p.stride < 1) p.stride = 1;
   p.two_phase = p.stride > 1;
   p.S = p.two_phase ? (N + p.stride - 1) / p.stride : N;
-  plan_workers((p.S + TD - 1) / TD, p.gy, D, p.nw, &p.g_s, &p.tpw_s);
+  plan_workers((p.S + TD - 1) / TD, p.gy, D, eb, p.nw, &p.g_s, &p.tpw_s);
   p.cap_s = (int64_t)p.tpw_s * TD;
-  plan_workers((N + TD - 1) / TD, p.gy, D, p.nw, &p.g_f, &p.tpw_f);
+  plan_workers((N + TD - 1) / TD, p.gy, D, eb, p.nw, &p.g_f, &p.tpw_f);
   p.cap_f = (int64_t)p.tpw_f * TD;
   const int gmax = p.g_s > p.g_f ? p.g_s : p.g_f;
   int64_t kmax = (int64_t)p.g_f * p.cap_f;
@@ -1088,7 +1124,8 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k) {
   p.pp_qpad = (int)((Q + 255) / 256 * 256);
   p.pp_cap = 256;  // a 256-doc tile can never overflow its region
   const size_t pp_keys = (size_t)p.pp_G * p.pp_qpad * p.pp_cap * 8;
-  p.pp = Q >= pp_min_q() && N >= 256 && pp_keys <= ((size_t)2 << 30);
+  // the GEMM-kernel filter is bf16 only
+  p.pp = eb == 2 && Q >= pp_min_q() && N >= 256 && pp_keys <= ((size_t)2 << 30);
   if (p.pp) {
     const size_t pc = (size_t)p.pp_G * p.pp_qpad * 4;
     if (pc > cnt_bytes) cnt_bytes = pc;
@@ -1103,31 +1140,31 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k) {
   return p;
 }
 
-template <int D, int NQ, int MODE>
-static void launch_tile(const Plan& p, int g, const unsigned short* qs, const unsigned short* docs,
+template <int D, int NQ, int MODE, int EB>
+static void launch_tile(const Plan& p, int g, const unsigned char* qs, const unsigned char* docs,
                         int Q, int64_t NS, int64_t stride, int tpw, uint32_t idx_base,
                         const uint64_t* thr, uint64_t* keys, uint32_t* counts, int64_t cap,
                         float* scores, hipStream_t st) {
-  const size_t lds = tile_lds_bytes<D>();
+  const size_t lds = tile_lds_bytes<D, EB>();
   constexpr int KS = D > 512 ? 2 : 1;
   static_assert(NQ * KS <= 8 || KS == 1, "wave budget");
-  hipLaunchKernelGGL((scan_tile_kernel<D, NQ, KS, MODE>), dim3(g * p.gy), dim3(NQ * KS * 64), lds, st, qs,
-                     docs, Q, p.qpad, p.gy, (int)NS, (int)stride, tpw, idx_base, thr, keys, counts,
-                     cap, scores);
+  hipLaunchKernelGGL((scan_tile_kernel<D, NQ, KS, MODE, EB>), dim3(g * p.gy), dim3(NQ * KS * 64),
+                     lds, st, qs, docs, Q, p.qpad, p.gy, (int)NS, (int)stride, tpw, idx_base, thr,
+                     keys, counts, cap, scores);
 }
 
-template <int MODE>
-static int dispatch_tile(int64_t D, const Plan& p, int g, const unsigned short* qs,
-                         const unsigned short* docs, int Q, int64_t NS, int64_t stride, int tpw,
-                         uint32_t idx_base, const uint64_t* thr, uint64_t* keys, uint32_t* counts,
-                         int64_t cap, float* scores, hipStream_t st) {
+template <int MODE, int EB>
+static int dispatch_tile_eb(int64_t D, const Plan& p, int g, const unsigned char* qs,
+                            const unsigned char* docs, int Q, int64_t NS, int64_t stride, int tpw,
+                            uint32_t idx_base, const uint64_t* thr, uint64_t* keys,
+                            uint32_t* counts, int64_t cap, float* scores, hipStream_t st) {
 #define IRC_SCAN_ARGS p, g, qs, docs, Q, NS, stride, tpw, idx_base, thr, keys, counts, cap, scores, st
-#define IRC_SCAN_CASE(DD)                                          \
-  case DD:                                                         \
-    if (p.nq == 1) launch_tile<DD, 1, MODE>(IRC_SCAN_ARGS);        \
-    else if (p.nq == 2) launch_tile<DD, 2, MODE>(IRC_SCAN_ARGS);   \
-    else if (p.nq == 4) launch_tile<DD, 4, MODE>(IRC_SCAN_ARGS);   \
-    else launch_tile<DD, (DD > 512 ? 4 : 8), MODE>(IRC_SCAN_ARGS); \
+#define IRC_SCAN_CASE(DD)                                              \
+  case DD:                                                             \
+    if (p.nq == 1) launch_tile<DD, 1, MODE, EB>(IRC_SCAN_ARGS);        \
+    else if (p.nq == 2) launch_tile<DD, 2, MODE, EB>(IRC_SCAN_ARGS);   \
+    else if (p.nq == 4) launch_tile<DD, 4, MODE, EB>(IRC_SCAN_ARGS);   \
+    else launch_tile<DD, (DD > 512 ? 4 : 8), MODE, EB>(IRC_SCAN_ARGS); \
     break;
   switch (D) {
     IRC_SCAN_CASE(64)
@@ -1147,8 +1184,106 @@ static int dispatch_tile(int64_t D, const Plan& p, int g, const unsigned short* 
   return check_launch("scan_tile_kernel");
 }
 
+template <int MODE>
+static int dispatch_tile(int eb, int64_t D, const Plan& p, int g, const void* qs, const void* docs,
+                         int Q, int64_t NS, int64_t stride, int tpw, uint32_t idx_base,
+                         const uint64_t* thr, uint64_t* keys, uint32_t* counts, int64_t cap,
+                         float* scores, hipStream_t st) {
+  const unsigned char* q8 = static_cast<const unsigned char*>(qs);
+  const unsigned char* d8 = static_cast<const unsigned char*>(docs);
+  if (eb == 1)
+    return dispatch_tile_eb<MODE, 1>(D, p, g, q8, d8, Q, NS, stride, tpw, idx_base, thr, keys,
+                                     counts, cap, scores, st);
+  return dispatch_tile_eb<MODE, 2>(D, p, g, q8, d8, Q, NS, stride, tpw, idx_base, thr, keys,
+                                   counts, cap, scores, st);
+}
+
 static bool supported_d(int64_t D) {
   return D == 64 || D == 128 || D == 256 || D == 384 || D == 512 || D == 768 || D == 1024;
+}
+
+static void launch_select(const RegionSource& src, int Q, int k, int mode, uint64_t* thr,
+                          float* out_score, int64_t* out_idx, float smul, hipStream_t st);
+
+// The scan for both element widths (eb = 2: bf16, 1: e4m3; smul scales the
+// returned scores, 1 for bf16).
+static int scan_topk_impl(int eb, float smul, const void* queries, const void* docs, int64_t Q,
+                          int64_t N, int64_t D, int64_t k, int64_t doc_offset, void* workspace,
+                          int64_t workspace_bytes, float* out_score, int64_t* out_idx,
+                          hipStream_t st) {
+  IRC_REQUIRE(Q >= 0 && N >= 0, "scan_topk: negative size");
+  IRC_REQUIRE(k >= 1 && k <= SEL_MAXK, "scan_topk: k=%lld outside [1, %d]", (long long)k,
+              SEL_MAXK);
+  IRC_REQUIRE(supported_d(D), "scan_topk: unsupported D=%lld", (long long)D);
+  IRC_REQUIRE(doc_offset >= 0 && doc_offset + N <= (int64_t)0xFFFFFFFFll,
+              "scan_topk: global doc index must fit 32 bits");
+  IRC_REQUIRE(Q < (1 << 24), "scan_topk: Q too large");
+  IRC_REQUIRE(N < (1ll << 31) - 64, "scan_topk: shard too large (N < 2^31)");
+  IRC_REQUIRE(((uintptr_t)queries % 16) == 0 && ((uintptr_t)docs % 16) == 0,
+              "scan_topk: queries and docs must be 16-byte aligned");
+  if (Q == 0) return IRC_OK;
+  if (N == 0) {
+    // nothing to rank: every slot empty
+    ListSource src{out_score, out_idx, 0, (int)Q, 1};
+    hipLaunchKernelGGL((select_kernel<ListSource>), dim3(Q), dim3(SEL_NT), 0, st, src, (int)k,
+                       (int)SEL_FINAL, nullptr, out_score, out_idx, 1.0f);
+    return check_launch("select_kernel(empty)");
+  }
+  const Plan p = make_plan(Q, N, D, k, eb);
+  IRC_REQUIRE(workspace != nullptr && workspace_bytes >= (int64_t)p.bytes,
+              "scan_topk: workspace %lld < required %lld bytes", (long long)workspace_bytes,
+              (long long)p.bytes);
+  char* ws = static_cast<char*>(workspace);
+  uint64_t* thr = reinterpret_cast<uint64_t*>(ws + p.off_thr);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(ws + p.off_cnt);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(ws + p.off_keys);
+  const uint32_t base = (uint32_t)doc_offset;
+  const double alg_bytes = (double)N * D * eb + (double)Q * D * eb;
+  int rc;
+  if (p.two_phase) {
+    rc = dispatch_tile<GMAX>(eb, D, p, p.g_s, queries, docs, (int)Q, p.S, p.stride, p.tpw_s,
+                             base, nullptr, keys, cnt, p.cap_s, nullptr, st);
+    if (rc) return rc;
+    RegionSource s1{keys, cnt, p.g_s, p.qpad, p.cap_s, 2 * p.ks};
+    launch_select(s1, (int)Q, (int)k, SEL_THRESHOLD, thr, nullptr, nullptr, 1.0f, st);
+    if ((rc = check_launch("select_kernel(threshold)"))) return rc;
+  }
+  if (p.pp) {
+    // filter = NT GEMM C[q][doc] = Q . Docs^T on the ping-pong kernel with a
+    // threshold epilogue; regions are (256-doc tile, query) with cap 256.
+    gpp::PArgs a{};
+    a.A = static_cast<const unsigned short*>(queries);
+    a.B = static_cast<const unsigned short*>(docs);
+    a.M = (int)Q;
+    a.N = (int)N;
+    a.K = (int)D;
+    a.kchunk = (int)D;
+    a.lda = D;
+    a.ldb = D;
+    a.alpha = 1.f;
+    a.thr = p.two_phase ? thr : nullptr;
+    a.keys = keys;
+    a.counts = cnt;
+    a.cap = p.pp_cap;
+    a.qpad = p.pp_qpad;
+    a.stride = 1;
+    a.idx_base = base;
+    prof_begin(st);
+    gpp::run_scan(a, st);
+    prof_end("scan_filter", st, alg_bytes);
+    if ((rc = check_launch("gemm_pp_kernel(scan)"))) return rc;
+    RegionSource s2{keys, cnt, p.pp_G, p.pp_qpad, p.pp_cap, 1};
+    launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
+    return check_launch("select_kernel(final)");
+  }
+  prof_begin(st);
+  rc = dispatch_tile<KEYS>(eb, D, p, p.g_f, queries, docs, (int)Q, N, 1, p.tpw_f, base,
+                           p.two_phase ? thr : nullptr, keys, cnt, p.cap_f, nullptr, st);
+  prof_end("scan_filter", st, alg_bytes);  // algorithmic bytes
+  if (rc) return rc;
+  RegionSource s2{keys, cnt, p.g_f, p.qpad, p.cap_f, 2 * p.ks};
+  launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
+  return check_launch("select_kernel(final)");
 }
 
 }  // namespace scan
@@ -1170,87 +1305,90 @@ extern "C" int irc_scan_dbg_stamps(uint64_t* out /* [4][32] */) {
 
 extern "C" int64_t irc_scan_topk_workspace(int64_t Q, int64_t N, int64_t D, int64_t k) {
   if (Q <= 0 || N <= 0 || k <= 0) return 256;
-  return (int64_t)make_plan(Q, N, D, k).bytes;
+  return (int64_t)make_plan(Q, N, D, k, 2).bytes;
+}
+
+extern "C" int64_t irc_scan_topk_fp8_workspace(int64_t Q, int64_t N, int64_t D, int64_t k) {
+  if (Q <= 0 || N <= 0 || k <= 0) return 256;
+  return (int64_t)make_plan(Q, N, D, k, 1).bytes;
 }
 
 extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, int64_t N,
                              int64_t D, int64_t k, int64_t doc_offset, void* workspace,
                              int64_t workspace_bytes, float* out_score, int64_t* out_idx,
                              irc_stream_t stream) {
-  IRC_REQUIRE(Q >= 0 && N >= 0, "scan_topk: negative size");
-  IRC_REQUIRE(k >= 1 && k <= SEL_MAXK, "scan_topk: k=%lld outside [1, %d]", (long long)k,
-              SEL_MAXK);
-  IRC_REQUIRE(supported_d(D), "scan_topk: unsupported D=%lld", (long long)D);
-  IRC_REQUIRE(doc_offset >= 0 && doc_offset + N <= (int64_t)0xFFFFFFFFll,
-              "scan_topk: global doc index must fit 32 bits");
-  IRC_REQUIRE(Q < (1 << 24), "scan_topk: Q too large");
-  IRC_REQUIRE(N < (1ll << 31) - 64, "scan_topk: shard too large (N < 2^31)");
+  return scan_topk_impl(2, 1.0f, queries, docs, Q, N, D, k, doc_offset, workspace,
+                        workspace_bytes, out_score, out_idx, as_stream(stream));
+}
+
+static bool pow2_scale(float s) {
+  int e;
+  return s > 0.f && std::isfinite(s) && std::frexp(s, &e) == 0.5f;
+}
+
+extern "C" int irc_scan_topk_fp8(const void* queries, const void* docs, int64_t Q, int64_t N,
+                                 int64_t D, int64_t k, int64_t doc_offset, float score_scale,
+                                 void* workspace, int64_t workspace_bytes, float* out_score,
+                                 int64_t* out_idx, irc_stream_t stream) {
+  IRC_REQUIRE(pow2_scale(score_scale), "scan_topk_fp8: score_scale must be a power of two");
+  return scan_topk_impl(1, score_scale, queries, docs, Q, N, D, k, doc_offset, workspace,
+                        workspace_bytes, out_score, out_idx, as_stream(stream));
+}
+
+// ------------------------------------------------------------ fp8 corpus
+namespace irc {
+namespace scan {
+// out[i] = e4m3fn(RNE(x[i] * scale)), saturated to +-448 (OCP e4m3fn, the gfx950
+// v_cvt_pk_fp8_f32 encoding).  8 elements per thread, 8-byte stores.
+template <typename T>
+__global__ __launch_bounds__(256) void quantize_fp8_kernel(const T* __restrict__ x, int64_t n,
+                                                           float scale,
+                                                           unsigned char* __restrict__ out) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i0 >= n) return;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float f = 0.f;
+    if (i0 + j < n) {
+      if constexpr (sizeof(T) == 2)
+        f = bf16_to_f32(reinterpret_cast<const unsigned short*>(x)[i0 + j]);
+      else
+        f = reinterpret_cast<const float*>(x)[i0 + j];
+    }
+    f *= scale;
+    v[j] = f != f ? f : fminf(fmaxf(f, -448.f), 448.f);
+  }
+  uint32_t w0 = 0, w1 = 0;
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], w0, false);
+  w0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], w0, true);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], w1, false);
+  w1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], w1, true);
+  if (i0 + 8 <= n && (((uintptr_t)(out + i0)) & 7) == 0) {
+    *reinterpret_cast<uint2*>(out + i0) = make_uint2(w0, w1);
+  } else {
+    for (int j = 0; j < 8 && i0 + j < n; ++j)
+      out[i0 + j] = (unsigned char)(((j < 4 ? w0 : w1) >> (8 * (j & 3))) & 0xff);
+  }
+}
+}  // namespace scan
+}  // namespace irc
+
+extern "C" int irc_quantize_fp8(int in_dtype, const void* x, int64_t n, float scale, void* out,
+                                irc_stream_t stream) {
+  IRC_REQUIRE(n >= 0, "quantize_fp8: negative size");
+  IRC_REQUIRE(in_dtype == 0 || in_dtype == 1, "quantize_fp8: in_dtype must be 0 (bf16) or 1 (fp32)");
+  if (n == 0) return IRC_OK;
+  const unsigned blocks = (unsigned)((n + 2047) / 2048);
   hipStream_t st = as_stream(stream);
-  if (Q == 0) return IRC_OK;
-  if (N == 0) {
-    // nothing to rank: every slot empty
-    IRC_REQUIRE(workspace_bytes >= 0, "bad workspace");
-    ListSource src{out_score, out_idx, 0, (int)Q, 1};
-    hipLaunchKernelGGL((select_kernel<ListSource>), dim3(Q), dim3(SEL_NT), 0, st, src, (int)k,
-                       (int)SEL_FINAL, nullptr, out_score, out_idx);
-    return check_launch("select_kernel(empty)");
-  }
-  const Plan p = make_plan(Q, N, D, k);
-  IRC_REQUIRE(workspace != nullptr && workspace_bytes >= (int64_t)p.bytes,
-              "scan_topk: workspace %lld < required %lld bytes", (long long)workspace_bytes,
-              (long long)p.bytes);
-  char* ws = static_cast<char*>(workspace);
-  uint64_t* thr = reinterpret_cast<uint64_t*>(ws + p.off_thr);
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(ws + p.off_cnt);
-  uint64_t* keys = reinterpret_cast<uint64_t*>(ws + p.off_keys);
-  const unsigned short* qs = static_cast<const unsigned short*>(queries);
-  const unsigned short* ds = static_cast<const unsigned short*>(docs);
-  const uint32_t base = (uint32_t)doc_offset;
-  int rc;
-  if (p.two_phase) {
-    rc = dispatch_tile<GMAX>(D, p, p.g_s, qs, ds, (int)Q, p.S, p.stride, p.tpw_s,
-                             base, nullptr, keys, cnt, p.cap_s, nullptr, st);
-    if (rc) return rc;
-    RegionSource s1{keys, cnt, p.g_s, p.qpad, p.cap_s, 2 * p.ks};
-    launch_select(s1, (int)Q, (int)k, SEL_THRESHOLD, thr, nullptr, nullptr, st);
-    if ((rc = check_launch("select_kernel(threshold)"))) return rc;
-  }
-  if (p.pp && ((uintptr_t)qs % 16) == 0 && ((uintptr_t)ds % 16) == 0) {
-    // filter = NT GEMM C[q][doc] = Q . Docs^T on the ping-pong kernel with a
-    // threshold epilogue; regions are (256-doc tile, query) with cap 256.
-    gpp::PArgs a{};
-    a.A = qs;
-    a.B = ds;
-    a.M = (int)Q;
-    a.N = (int)N;
-    a.K = (int)D;
-    a.kchunk = (int)D;
-    a.lda = D;
-    a.ldb = D;
-    a.alpha = 1.f;
-    a.thr = p.two_phase ? thr : nullptr;
-    a.keys = keys;
-    a.counts = cnt;
-    a.cap = p.pp_cap;
-    a.qpad = p.pp_qpad;
-    a.stride = 1;
-    a.idx_base = base;
-    prof_begin(st);
-    gpp::run_scan(a, st);
-    prof_end("scan_filter", st, (double)N * D * 2 + (double)Q * D * 2);
-    if ((rc = check_launch("gemm_pp_kernel(scan)"))) return rc;
-    RegionSource s2{keys, cnt, p.pp_G, p.pp_qpad, p.pp_cap, 1};
-    launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, st);
-    return check_launch("select_kernel(final)");
-  }
-  prof_begin(st);
-  rc = dispatch_tile<KEYS>(D, p, p.g_f, qs, ds, (int)Q, N, 1, p.tpw_f, base,
-                           p.two_phase ? thr : nullptr, keys, cnt, p.cap_f, nullptr, st);
-  prof_end("scan_filter", st, (double)N * D * 2 + (double)Q * D * 2);  // algorithmic bytes
-  if (rc) return rc;
-  RegionSource s2{keys, cnt, p.g_f, p.qpad, p.cap_f, 2 * p.ks};
-  launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, st);
-  return check_launch("select_kernel(final)");
+  if (in_dtype == 0)
+    hipLaunchKernelGGL((quantize_fp8_kernel<unsigned short>), dim3(blocks), dim3(256), 0, st,
+                       static_cast<const unsigned short*>(x), n, scale,
+                       static_cast<unsigned char*>(out));
+  else
+    hipLaunchKernelGGL((quantize_fp8_kernel<float>), dim3(blocks), dim3(256), 0, st,
+                       static_cast<const float*>(x), n, scale, static_cast<unsigned char*>(out));
+  return check_launch("quantize_fp8_kernel");
 }
 
 extern "C" int irc_topk_merge(const float* in_score, const int64_t* in_idx, int64_t P, int64_t Q,
@@ -1261,7 +1399,7 @@ extern "C" int irc_topk_merge(const float* in_score, const int64_t* in_idx, int6
   if (Q == 0) return IRC_OK;
   ListSource src{in_score, in_idx, (int)P, (int)Q, (int)kin};
   hipLaunchKernelGGL((select_kernel<ListSource>), dim3(Q), dim3(SEL_NT), 0, as_stream(stream),
-                     src, (int)kout, (int)SEL_FINAL, nullptr, out_score, out_idx);
+                     src, (int)kout, (int)SEL_FINAL, nullptr, out_score, out_idx, 1.0f);
   return check_launch("select_kernel(merge)");
 }
 
@@ -1269,9 +1407,11 @@ extern "C" int irc_scan_scores(const void* queries, const void* docs, int64_t Q,
                                int64_t D, float* out, irc_stream_t stream) {
   IRC_REQUIRE(Q >= 0 && N >= 0, "scan_scores: negative size");
   IRC_REQUIRE(supported_d(D), "scan_scores: unsupported D=%lld", (long long)D);
+  IRC_REQUIRE(((uintptr_t)queries % 16) == 0 && ((uintptr_t)docs % 16) == 0,
+              "scan_scores: queries and docs must be 16-byte aligned");
   if (Q == 0 || N == 0) return IRC_OK;
-  Plan p = make_plan(Q, N, D, 1);
-  if (p.pp && ((uintptr_t)queries % 16) == 0 && ((uintptr_t)docs % 16) == 0) {
+  Plan p = make_plan(Q, N, D, 1, 2);
+  if (p.pp) {
     // same MFMA arithmetic as irc_scan_topk's filter on this path
     gpp::PArgs a{};
     a.A = static_cast<const unsigned short*>(queries);
@@ -1289,7 +1429,20 @@ extern "C" int irc_scan_scores(const void* queries, const void* docs, int64_t Q,
     gpp::run(1, 0, 0, 0, a, 1, 1, as_stream(stream));
     return check_launch("gemm_pp_kernel(scores)");
   }
-  return dispatch_tile<SCORES>(D, p, p.g_f, static_cast<const unsigned short*>(queries),
-                               static_cast<const unsigned short*>(docs), (int)Q, N, 1, p.tpw_f, 0,
-                               nullptr, nullptr, nullptr, 0, out, as_stream(stream));
+  return dispatch_tile<SCORES>(2, D, p, p.g_f, queries, docs, (int)Q, N, 1, p.tpw_f, 0, nullptr,
+                               nullptr, nullptr, 0, out, as_stream(stream));
+}
+
+// Raw (unscaled) dot products of e4m3 queries and docs, fp32 accumulation: the
+// arithmetic of irc_scan_topk_fp8's filter.
+extern "C" int irc_scan_scores_fp8(const void* queries, const void* docs, int64_t Q, int64_t N,
+                                   int64_t D, float* out, irc_stream_t stream) {
+  IRC_REQUIRE(Q >= 0 && N >= 0, "scan_scores_fp8: negative size");
+  IRC_REQUIRE(supported_d(D), "scan_scores_fp8: unsupported D=%lld", (long long)D);
+  IRC_REQUIRE(((uintptr_t)queries % 16) == 0 && ((uintptr_t)docs % 16) == 0,
+              "scan_scores_fp8: queries and docs must be 16-byte aligned");
+  if (Q == 0 || N == 0) return IRC_OK;
+  Plan p = make_plan(Q, N, D, 1, 1);
+  return dispatch_tile<SCORES>(1, D, p, p.g_f, queries, docs, (int)Q, N, 1, p.tpw_f, 0, nullptr,
+                               nullptr, nullptr, 0, out, as_stream(stream));
 }

@@ -53,6 +53,61 @@ def scan_scores(queries: torch.Tensor, docs: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# fp8 corpus (BASELINE config C5): e4m3fn embeddings, stored as uint8 bytes.
+# Unit-norm components times 16 sit in e4m3's normal range and far below its
+# 448 maximum; a power of two keeps the descale exact.
+FP8_SCALE = 16.0
+
+
+def quantize_fp8(x: torch.Tensor, scale: float = FP8_SCALE) -> torch.Tensor:
+    """e4m3fn(RNE(x * scale)) as a uint8 tensor of x's shape (irc_quantize_fp8)."""
+    require_hip(x)
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        x = x.float()
+    xc = x.contiguous()
+    out = torch.empty(xc.shape, dtype=torch.uint8, device=xc.device)
+    _lib.call("irc_quantize_fp8", 0 if xc.dtype == torch.bfloat16 else 1, ptr(xc), xc.numel(),
+              float(scale), ptr(out), stream_ptr(xc.device))
+    return out
+
+
+def _fp8_operands(queries, docs):
+    require_hip(queries, docs)
+    for t in (queries, docs):
+        if t.dtype != torch.uint8:
+            raise TypeError("fp8 scan operands are e4m3 bytes (torch.uint8, see quantize_fp8)")
+    q, d = queries.contiguous(), docs.contiguous()
+    if d.shape[1] != q.shape[1]:
+        raise ValueError(f"dim mismatch: queries D={q.shape[1]}, docs D={d.shape[1]}")
+    return q, d
+
+
+def scan_topk_fp8(queries: torch.Tensor, docs: torch.Tensor, k: int, doc_offset: int = 0,
+                  score_scale: float = 1.0):
+    """Exact top-k over e4m3 queries [Q, D] and docs [N, D] (uint8 bytes); the
+    returned scores are the fp32 dot products of the quantised values times
+    score_scale (a power of two)."""
+    q, d = _fp8_operands(queries, docs)
+    Q, D = q.shape
+    N = d.shape[0]
+    out_s = torch.empty((Q, k), dtype=torch.float32, device=q.device)
+    out_i = torch.empty((Q, k), dtype=torch.int64, device=q.device)
+    nbytes = int(_lib.fn("irc_scan_topk_fp8_workspace")(Q, N, D, k))
+    ws = workspace(nbytes, q.device, "scan")
+    _lib.call("irc_scan_topk_fp8", ptr(q), ptr(d), Q, N, D, k, doc_offset, float(score_scale),
+              ptr(ws), ws.numel(), ptr(out_s), ptr(out_i), stream_ptr(q.device))
+    return out_s, out_i
+
+
+def scan_scores_fp8(queries: torch.Tensor, docs: torch.Tensor) -> torch.Tensor:
+    """Raw fp32 dot products of e4m3 operands (the fp8 filter's arithmetic)."""
+    q, d = _fp8_operands(queries, docs)
+    out = torch.empty((q.shape[0], d.shape[0]), dtype=torch.float32, device=q.device)
+    _lib.call("irc_scan_scores_fp8", ptr(q), ptr(d), q.shape[0], d.shape[0], q.shape[1],
+              ptr(out), stream_ptr(q.device))
+    return out
+
+
 def topk_merge(scores: torch.Tensor, idx: torch.Tensor, k: int):
     """Merge [P, Q, kin] per-shard lists into [Q, k] with the exact rule."""
     require_hip(scores, idx)
@@ -80,16 +135,33 @@ class ShardedDenseIndex:
     global index.  ``search`` is collective over ``group`` when one is given:
     every rank passes its local query slice (may be empty) and receives the
     global top-k for ALL gathered queries (queries ordered by rank).
+
+    ``dtype="fp8"`` keeps the shard as e4m3 bytes (half the HBM bytes per scan,
+    BASELINE config C5): queries are quantised with the same power-of-two
+    ``fp8_scale`` per search and the scores returned are those of the
+    quantised embeddings, descaled exactly.
     """
 
-    def __init__(self, docs: torch.Tensor, doc_offset: int = 0, group=None):
-        self.docs = docs.to(torch.bfloat16).contiguous()
+    def __init__(self, docs: torch.Tensor, doc_offset: int = 0, group=None, dtype: str = "bf16",
+                 fp8_scale: float = FP8_SCALE):
+        if dtype not in ("bf16", "fp8"):
+            raise ValueError(f"dtype must be 'bf16' or 'fp8', not {dtype!r}")
+        self.dtype = dtype
+        self.fp8_scale = float(fp8_scale)
+        if dtype == "fp8":
+            self.docs = quantize_fp8(docs, self.fp8_scale)
+        else:
+            self.docs = docs.to(torch.bfloat16).contiguous()
         self.doc_offset = int(doc_offset)
         self.group = group
 
     # The two device steps are methods so the collective orchestration can be
     # exercised on CPU (gloo) with a test double in tests/test_dist_cpu.py.
     def _local_topk(self, queries, k):
+        if self.dtype == "fp8":
+            q8 = quantize_fp8(queries, self.fp8_scale)
+            return scan_topk_fp8(q8, self.docs, k, self.doc_offset,
+                                 1.0 / (self.fp8_scale * self.fp8_scale))
         return scan_topk(queries, self.docs, k, self.doc_offset)
 
     def _merge(self, scores, idx, k):

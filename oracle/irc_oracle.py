@@ -105,6 +105,59 @@ def scan_topk(queries: np.ndarray, docs: np.ndarray, k: int, doc_offset: int = 0
     return best_i, best_s
 
 
+# ---------------------------------------------------------------------------
+# fp8 corpus (BASELINE.json config C5): OCP e4m3fn quantisation
+# ---------------------------------------------------------------------------
+# Not in the reference (which scores fp32 embeddings, src/evaluation.py:110-112);
+# this restates the published OCP 8-bit floating point spec (E4M3, "fn": no
+# infinities, S.1111.111 = NaN, max 448, subnormals m * 2^-9) with
+# round-to-nearest-even, and saturation to +-448 as the build applies before
+# converting.  Pinned against torch's float8_e4m3fn cast in
+# tests/test_oracle_golden.py (a second, independent implementation of the spec).
+
+
+def e4m3_decode_table() -> np.ndarray:
+    """float32 value of each of the 256 e4m3fn codes (NaN for S.1111.111)."""
+    c = np.arange(256)
+    sign = np.where(c >> 7, -1.0, 1.0)
+    e = (c >> 3) & 15
+    m = c & 7
+    mag = np.where(e == 0, m * 2.0 ** -9, (1.0 + m / 8.0) * 2.0 ** (e - 7.0))
+    v = sign * mag
+    v[(e == 15) & (m == 7)] = np.nan
+    return v.astype(F32)
+
+
+def quantize_e4m3(x: np.ndarray, scale: float = 1.0) -> np.ndarray:
+    """uint8 e4m3fn codes of RNE(x * scale) (fp32 arithmetic), saturated to +-448."""
+    a = np.asarray(x, dtype=F32) * F32(scale)
+    nan = np.isnan(a)
+    neg = np.signbit(a)
+    mag = np.minimum(np.abs(np.where(nan, 0, a)).astype(F64), 448.0)
+    # quantum: 2^(E-3) in the normal range (a = 1.f * 2^E, E >= -6), 2^-9 below
+    _, e2 = np.frexp(mag)
+    E = np.maximum(e2.astype(np.int64) - 1, -6)
+    quantum = np.ldexp(1.0, E - 3)
+    qv = np.rint(mag / quantum) * quantum  # round half to even, exact in fp64
+    # encode the (representable) quantised magnitude
+    table = e4m3_decode_table()[:127].astype(F64)  # codes 0x00..0x7e, ascending
+    code = np.searchsorted(table, qv).astype(np.uint8)
+    code = np.where(neg, code | 0x80, code).astype(np.uint8)
+    return np.where(nan, np.uint8(0x7F), code).astype(np.uint8)
+
+
+def dequantize_e4m3(codes: np.ndarray) -> np.ndarray:
+    return e4m3_decode_table()[np.asarray(codes, dtype=np.uint8)]
+
+
+def scan_topk_fp8(q_codes: np.ndarray, d_codes: np.ndarray, k: int, doc_offset: int = 0,
+                  score_scale: float = 1.0):
+    """The fp8 scan's result: top-k of the quantised embeddings' dot products,
+    times the (power-of-two) score_scale."""
+    idx, sc = scan_topk(dequantize_e4m3(q_codes), dequantize_e4m3(d_codes), k, doc_offset)
+    return idx, (sc * F32(score_scale)).astype(F32)
+
+
 def scan_topk_fast_f32(queries: np.ndarray, docs: np.ndarray, k: int,
                        doc_offset: int = 0, chunk: int = 65536):
     """Same as scan_topk but with fp32 BLAS matmul (the timed CPU baseline).

@@ -168,3 +168,23 @@ def test_lstm_head_init_matches_reference_rng_order():
         sd = h.state_dict()
         for name, _ in h.specs:
             np.testing.assert_array_equal(sd[name].numpy(), g[f"{tag}_{name}"], err_msg=name)
+
+
+def test_e4m3_quantiser_matches_torch_cast():
+    """The oracle's OCP e4m3fn RNE quantiser (fp8 corpus, config C5) agrees code for
+    code with torch's float8_e4m3fn cast, an independent implementation of the spec
+    (inputs clamped to +-448 as the build saturates)."""
+    import torch
+
+    rng = np.random.default_rng(0)
+    mags = rng.choice(np.array([1e-3, 1e-2, 0.1, 1, 10, 100, 500], np.float32), 100_000)
+    x = np.concatenate([
+        rng.standard_normal(100_000).astype(np.float32) * mags,
+        np.array([0.0, -0.0, 2**-10, 2**-9, 1.5 * 2**-9, 2.5 * 2**-9, 3 * 2**-10, 447, 448,
+                  449, 460, 464, 465, 1e4, -1e4, 2**-6], np.float32)])
+    codes = O.quantize_e4m3(x)
+    ref = torch.from_numpy(np.clip(x, -448, 448)).to(torch.float8_e4m3fn).view(torch.uint8).numpy()
+    np.testing.assert_array_equal(codes, ref)
+    # decode table: max, min normal, min subnormal
+    np.testing.assert_array_equal(O.dequantize_e4m3(np.array([0x7E, 0x08, 0x01], np.uint8)),
+                                  np.array([448.0, 2**-6, 2**-9], np.float32))

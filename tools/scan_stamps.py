@@ -50,6 +50,11 @@ def main():
             pts = [(i, (row[i] - t0) / 100.0) for i in range(1, 20) if row[i] > 0 and row[i] >= t0]
             extra = f"  M={row[21]}" if slot < 2 else ""
             print(f"{NAMES[slot]:22s}" + " ".join(f"[{i}]{us:6.2f}" for i, us in pts) + extra)
+        pp = np.zeros(16, dtype=np.uint64)
+        if lib.irc_pp_dbg_stamps(pp.ctypes.data_as(ctypes.c_void_p)) == 0 and pp[0] > 0:
+            row = pp.astype(np.int64)
+            print(f"{'pp filter (EPI_SCAN)':22s}" + " ".join(
+                f"[{i}]{(row[i] - row[0]) / 100.0:6.2f}" for i in range(1, 5) if row[i] >= row[0]))
 
 
 if __name__ == "__main__":
