@@ -47,6 +47,9 @@ BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA spec
 METRIC = "query-doc pairs/sec (train) + queries/sec @ top-k over N docs, 1/2/4/8 GPU"
 TRAIN_B, TRAIN_L, VOCAB = 256, 64, 30522
 SCAN_N_PER_GPU, SCAN_Q, SCAN_D, SCAN_K = 100_000, 256, 768, 100
+# C5 retrieval leg: 5M docs over 8 GPUs = 625k e4m3 docs per GPU (weak scaling)
+FP8_N_PER_GPU = 625_000
+PP_MIN_Q = 192  # irc_scan_topk's filter runs on the ping-pong GEMM kernel from this Q
 
 
 def _cpu_model():
@@ -273,18 +276,29 @@ def cpu_baseline_train(model, budget_s):
                       "numpy fp32 oracle"}
 
 
-def run_scan(args, rank, world, dev):
+def _filter_kernel_name(q, dtype):
+    if q >= PP_MIN_Q:
+        mf = ("v_mfma_scale_f32_16x16x128_f8f6f4" if dtype == "fp8"
+              else "v_mfma_f32_16x16x32_bf16")
+        return f"gemm_pp_kernel<EPI_SCAN> (scan filter, 256x256 tiles, {mf})"
+    mf = "v_mfma_f32_32x32x16_fp8_fp8" if dtype == "fp8" else "v_mfma_f32_32x32x16_bf16"
+    return f"scan_tile_kernel<{SCAN_D}> (scan filter, stationary queries, {mf})"
+
+
+def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16"):
     from irc_amd import _lib, retrieval
 
     lib = _lib.load()
     g = torch.Generator().manual_seed(2024 + rank)
-    shard = torch.nn.functional.normalize(torch.randn(SCAN_N_PER_GPU, SCAN_D, generator=g))
+    shard = torch.nn.functional.normalize(torch.randn(n_per_gpu, SCAN_D, generator=g))
     shard = shard.bfloat16().to(dev)
     gq = torch.Generator().manual_seed(7)
     allq = torch.nn.functional.normalize(torch.randn(SCAN_Q, SCAN_D, generator=gq)).bfloat16()
     myq = allq[rank * SCAN_Q // world:(rank + 1) * SCAN_Q // world].to(dev)
-    index = retrieval.ShardedDenseIndex(shard, doc_offset=rank * SCAN_N_PER_GPU,
-                                        group=dist.group.WORLD if world > 1 else None)
+    index = retrieval.ShardedDenseIndex(shard, doc_offset=rank * n_per_gpu,
+                                        group=dist.group.WORLD if world > 1 else None,
+                                        dtype=dtype)
+    del shard
     for _ in range(args.warmup):
         index.search(myq, SCAN_K)
     torch.cuda.synchronize()
@@ -303,31 +317,33 @@ def run_scan(args, rank, world, dev):
     lib.irc_prof_enable(0)
     dt = _max_over_ranks(dt, dev, world)
     k_s, k_n, k_bytes = _prof(lib, "scan_filter")
-    sweep = scan_q_sweep(shard, dev) if rank == 0 else None
+    sweep = scan_q_sweep(index, dev) if rank == 0 else None
     kavg = k_s / max(k_n, 1)
     achieved = (k_bytes / max(k_n, 1)) / kavg / 1e9 if k_n else None
     return {
         "value": SCAN_Q * args.steps / dt, "unit": "queries/s",
-        "ms_per_batch": dt * 1e3 / args.steps,
-        "docs_total": SCAN_N_PER_GPU * world, "queries": SCAN_Q, "dim": SCAN_D, "k": SCAN_K,
-        "query_doc_pairs_per_s": SCAN_Q * SCAN_N_PER_GPU * world * args.steps / dt,
+        "ms_per_batch": dt * 1e3 / args.steps, "dtype": dtype,
+        "docs_per_gpu": n_per_gpu,
+        "docs_total": n_per_gpu * world, "queries": SCAN_Q, "dim": SCAN_D, "k": SCAN_K,
+        "query_doc_pairs_per_s": SCAN_Q * n_per_gpu * world * args.steps / dt,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS if achieved else None,
-                     "traffic": _pmc_traffic("scan_filter"),
-                     "kernel": "scan_tile_kernel<768,4,2,KEYS> (filter pass)",
+                     "traffic": _pmc_traffic("scan_filter") if dtype == "bf16" else None,
+                     "kernel": _filter_kernel_name(SCAN_Q, dtype),
                      "kernel_avg_us": kavg * 1e6,
                      "alg_bytes_per_launch": k_bytes / max(k_n, 1),
-                     "mfma_tflops": 2 * SCAN_Q * SCAN_N_PER_GPU * SCAN_D / kavg / 1e12
+                     "mfma_tflops": 2 * SCAN_Q * n_per_gpu * SCAN_D / kavg / 1e12
                      if k_n else None},
         "q_sweep_local": sweep,
     }
 
 
-def scan_q_sweep(shard, dev, qs=(1, 16, 64, 256), reps=20):
+def scan_q_sweep(index, dev, qs=(1, 16, 64, 256), reps=20):
     """Local scan filter at several query-batch sizes (SURVEY.md 8d grades the HBM
     fraction at Q in {1, 16, 64, 256}): kernel HIP-event time and algorithmic bytes
-    (N*D*2 + Q*D*2) -> GB/s, plus the whole call's queries/s."""
-    from irc_amd import _lib, retrieval
+    (N*D*b + Q*D*b) -> GB/s, plus the whole call's queries/s (query quantisation
+    included for fp8)."""
+    from irc_amd import _lib
 
     lib = _lib.load()
     out = []
@@ -335,13 +351,13 @@ def scan_q_sweep(shard, dev, qs=(1, 16, 64, 256), reps=20):
         g = torch.Generator().manual_seed(11 + q)
         qq = torch.nn.functional.normalize(torch.randn(q, SCAN_D, generator=g)).bfloat16().to(dev)
         for _ in range(3):
-            retrieval.scan_topk(qq, shard, SCAN_K)
+            index._local_topk(qq, SCAN_K)
         torch.cuda.synchronize()
         lib.irc_prof_reset()
         lib.irc_prof_enable(1)
         t0 = time.perf_counter()
         for _ in range(reps):
-            retrieval.scan_topk(qq, shard, SCAN_K)
+            index._local_topk(qq, SCAN_K)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         lib.irc_prof_enable(0)
@@ -395,8 +411,11 @@ def main():
     bert = None
     if args.part in ("all", "bert"):
         bert = run_train_bert(args, rank, world, dev)
+    scan_fp8 = None
     if args.part in ("all", "scan"):
         scan = run_scan(args, rank, world, dev)
+        torch.cuda.empty_cache()
+        scan_fp8 = run_scan(args, rank, world, dev, FP8_N_PER_GPU, "fp8")
     cpu_t = cpu_s = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if train is not None:
@@ -439,6 +458,10 @@ def main():
             line["train_bert"] = bert
         if scan is not None:
             line["retrieval"] = scan
+        if scan_fp8 is not None:
+            scan_fp8["workload"] = (f"C5 retrieval shard: {FP8_N_PER_GPU} e4m3 docs/GPU "
+                                    f"(5M over 8 GPUs), {SCAN_Q} queries, top-{SCAN_K}")
+            line["retrieval_fp8"] = scan_fp8
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

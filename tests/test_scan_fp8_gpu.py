@@ -37,12 +37,16 @@ def test_quantize_bit_exact(gpu, src_dtype):
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("D", [64, 128, 256, 512, 768, 1024])
-def test_scores_exact_on_grid(gpu, D):
+@pytest.mark.parametrize("Q,D", [(70, 64), (70, 128), (70, 256), (70, 512), (70, 768),
+                                 (70, 1024),
+                                 # Q >= 192, D % 128 == 0: the ping-pong GEMM kernel on
+                                 # v_mfma_scale_f32_16x16x128_f8f6f4
+                                 (256, 768), (300, 128), (192, 1024)])
+def test_scores_exact_on_grid(gpu, Q, D):
     from irc_amd import retrieval
 
-    rng = np.random.default_rng(D)
-    q, d = _grid_codes(rng, (70, D)), _grid_codes(rng, (517, D))
+    rng = np.random.default_rng(D + Q)
+    q, d = _grid_codes(rng, (Q, D)), _grid_codes(rng, (517, D))
     s = retrieval.scan_scores_fp8(_dev(q, gpu), _dev(d, gpu)).cpu().numpy()
     np.testing.assert_array_equal(s, O.scan_scores(O.dequantize_e4m3(q), O.dequantize_e4m3(d)))
 
@@ -55,7 +59,9 @@ def test_scores_exact_on_grid(gpu, D):
     (16, 60_000, 768, 100, 5),   # two-phase
     (64, 40_000, 768, 1024, 3),  # maximum k
     (257, 20_000, 128, 100, 0),  # several query blocks
-    (200, 30_000, 1024, 50, 7),  # D = 1024
+    (200, 30_000, 1024, 50, 7),  # D = 1024, GEMM-kernel filter (scaled fp8 MFMA)
+    (256, 100_000, 768, 100, 0),  # C5 dims, GEMM-kernel filter
+    (384, 9_000, 384, 1024, 0),  # two query tiles, D = 384 (3 K-tiles), max k
 ])
 def test_topk_exact_vs_oracle(gpu, Q, N, D, k, off):
     from irc_amd import retrieval
