@@ -37,8 +37,11 @@ bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, i
                int64_t sA, const void* B, int64_t ldb, int64_t sB, int64_t batch, int splits);
 void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, int splits,
          hipStream_t st);
-// scan filter: A = queries [M=Q][K=D], B = docs [N][D] (row stride ldb), EPI_SCAN
-void run_scan(const PArgs& a, hipStream_t st);
+// scan filter: A = queries [M=Q][K=D], B = docs [N][D] (row stride ldb), EPI_SCAN;
+// fp8: e4m3 operands, K / lda / ldb in 2-byte units (D/2)
+void run_scan(const PArgs& a, hipStream_t st, bool fp8 = false);
+// raw fp32 C = A . B^T of e4m3 operands (K, lda, ldb in 2-byte units; vec_c layout)
+void run_scores_fp8(const PArgs& a, hipStream_t st);
 
 }  // namespace gpp
 }  // namespace irc

@@ -156,7 +156,15 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int row0, int s, int lan
   }
 }
 
-template <bool AK, bool BK_, typename TO, int EPI>
+// F8: both operands are e4m3 bytes (the fp8 corpus scan, BASELINE config C5),
+// passed as 2-byte units (K, ld in units of 2 fp8 values): the DMA and LDS
+// images are byte-identical to bf16, and each 128-byte K-tile row feeds one
+// v_mfma_scale_f32_16x16x128_f8f6f4 (unit E8M0 scales) per accumulator instead
+// of two 16x16x32 bf16 MFMAs -- twice the bf16 rate per element.  A and B
+// fragments take the same bytes of the row, so the k order is consistent.
+typedef int v8i32 __attribute__((ext_vector_type(8)));
+
+template <bool AK, bool BK_, typename TO, int EPI, bool F8 = false>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
   const int tiles_m = (g.M + BM - 1) / BM;
@@ -227,14 +235,27 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
       wg_barrier();
       // ---- M section
       __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
+      if constexpr (F8) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[i][j], 0,
-                                                                0, 0);
+          for (int j = 0; j < 4; ++j) {
+            const bf16x8 a2[2] = {fa[i][0], fa[i][1]};
+            const bf16x8 b2[2] = {fb[j][0], fb[j][1]};
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                __builtin_bit_cast(v8i32, a2), __builtin_bit_cast(v8i32, b2), acc[i][j], 0, 0, 0,
+                127, 0, 127);
+          }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][s], fb[j][s], acc[i][j],
+                                                                  0, 0, 0);
+      }
       __builtin_amdgcn_s_setprio(0);
       if (grp == 0) wait_vmcnt<0>();
       wg_barrier();
@@ -518,9 +539,19 @@ extern "C" int irc_pp_dbg_stamps(uint64_t* out /* [16] */) {
 #endif
 }
 
-void run_scan(const PArgs& a, hipStream_t st) {
+void run_scan(const PArgs& a, hipStream_t st, bool fp8) {
   const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
-  hipLaunchKernelGGL((gemm_pp_kernel<true, true, float, EPI_SCAN>), dim3((unsigned)tiles),
+  if (fp8)
+    hipLaunchKernelGGL((gemm_pp_kernel<true, true, float, EPI_SCAN, true>), dim3((unsigned)tiles),
+                       dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm_pp_kernel<true, true, float, EPI_SCAN>), dim3((unsigned)tiles),
+                       dim3(NT), 0, st, a);
+}
+
+void run_scores_fp8(const PArgs& a, hipStream_t st) {
+  const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
+  hipLaunchKernelGGL((gemm_pp_kernel<true, true, float, EPI_NONE, true>), dim3((unsigned)tiles),
                      dim3(NT), 0, st, a);
 }
 

@@ -1124,8 +1124,9 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   p.pp_qpad = (int)((Q + 255) / 256 * 256);
   p.pp_cap = 256;  // a 256-doc tile can never overflow its region
   const size_t pp_keys = (size_t)p.pp_G * p.pp_qpad * p.pp_cap * 8;
-  // the GEMM-kernel filter is bf16 only
-  p.pp = eb == 2 && Q >= pp_min_q() && N >= 256 && pp_keys <= ((size_t)2 << 30);
+  // the GEMM-kernel filter: bf16, or fp8 with 128-byte K-tiles (D % 128 == 0)
+  p.pp = (eb == 2 || D % 128 == 0) && Q >= pp_min_q() && N >= 256 &&
+         pp_keys <= ((size_t)2 << 30);
   if (p.pp) {
     const size_t pc = (size_t)p.pp_G * p.pp_qpad * 4;
     if (pc > cnt_bytes) cnt_bytes = pc;
@@ -1256,10 +1257,10 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
     a.B = static_cast<const unsigned short*>(docs);
     a.M = (int)Q;
     a.N = (int)N;
-    a.K = (int)D;
-    a.kchunk = (int)D;
-    a.lda = D;
-    a.ldb = D;
+    a.K = (int)(D * eb / 2);  // 2-byte units
+    a.kchunk = a.K;
+    a.lda = a.K;
+    a.ldb = a.K;
     a.alpha = 1.f;
     a.thr = p.two_phase ? thr : nullptr;
     a.keys = keys;
@@ -1269,7 +1270,7 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
     a.stride = 1;
     a.idx_base = base;
     prof_begin(st);
-    gpp::run_scan(a, st);
+    gpp::run_scan(a, st, eb == 1);
     prof_end("scan_filter", st, alg_bytes);
     if ((rc = check_launch("gemm_pp_kernel(scan)"))) return rc;
     RegionSource s2{keys, cnt, p.pp_G, p.pp_qpad, p.pp_cap, 1};
@@ -1443,6 +1444,24 @@ extern "C" int irc_scan_scores_fp8(const void* queries, const void* docs, int64_
               "scan_scores_fp8: queries and docs must be 16-byte aligned");
   if (Q == 0 || N == 0) return IRC_OK;
   Plan p = make_plan(Q, N, D, 1, 1);
+  if (p.pp) {
+    // same MFMA arithmetic as irc_scan_topk_fp8's filter on this path
+    gpp::PArgs a{};
+    a.A = static_cast<const unsigned short*>(queries);
+    a.B = static_cast<const unsigned short*>(docs);
+    a.C = out;
+    a.M = (int)Q;
+    a.N = (int)N;
+    a.K = (int)(D / 2);
+    a.kchunk = a.K;
+    a.lda = a.K;
+    a.ldb = a.K;
+    a.ldc = N;
+    a.alpha = 1.f;
+    a.vec_c = (N % 8 == 0) && ((uintptr_t)out % 16) == 0;
+    gpp::run_scores_fp8(a, as_stream(stream));
+    return check_launch("gemm_pp_kernel(scores fp8)");
+  }
   return dispatch_tile<SCORES>(1, D, p, p.g_f, queries, docs, (int)Q, N, 1, p.tpw_f, 0, nullptr,
                                nullptr, nullptr, 0, out, as_stream(stream));
 }

@@ -29,13 +29,19 @@ def stream_ptr(device: torch.device | None = None):
 _side: dict = {}
 
 
+# Streams created with the high priority (none by default: on MI355X, giving the
+# heads' streams priority over the BERT-feature prefetch measured 3% slower).
+HIGH_PRIORITY_TAGS: tuple = ()
+
+
 def side_stream(device: torch.device, tag: str = "side") -> torch.cuda.Stream:
     """A persistent secondary HIP stream per (device, tag) for overlapping
     independent launches (e.g. the key encoder, weight-gradient GEMMs)."""
     key = (torch.device(device).index, tag)
     s = _side.get(key)
     if s is None:
-        s = _side[key] = torch.cuda.Stream(device=device)
+        prio = torch.cuda.Stream.priority_range()[1] if tag in HIGH_PRIORITY_TAGS else 0
+        s = _side[key] = torch.cuda.Stream(device=device, priority=prio)
     return s
 
 

@@ -88,6 +88,39 @@ class RetrievalModelWrapper(nn.Module):
         return out[:n_anchor], out[n_anchor:]
 
     @torch.no_grad()
+    def bert_extract_async(self, input_ids, attention_mask, n_anchor):
+        """bert_extract_ids issued on the "bert_prefetch" side stream.
+
+        BERT is frozen (contrastive_module.py:34-36: no_grad, eval, never in the
+        optimizer), so the features of micro-batch t+1 do not depend on the heads'
+        update of micro-batch t: issuing them here, before the heads' step of
+        micro-batch t is enqueued, lets the BERT GEMMs fill the CUs the
+        latency-bound BiLSTM recurrences leave idle.  The side stream first waits
+        for the work already on the current stream (the inputs' producers).
+        Returns a handle for features_ready()."""
+        dev = input_ids.device
+        cur = torch.cuda.current_stream(dev)
+        side = side_stream(dev, "bert_prefetch")
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            out = self.bert_model.encode(input_ids, attention_mask)
+            done = torch.cuda.Event()
+            done.record(side)
+        input_ids.record_stream(side)
+        attention_mask.record_stream(side)
+        return out, int(n_anchor), done
+
+    @staticmethod
+    def features_ready(handle):
+        """(anchor, positive) features of a bert_extract_async handle, usable on the
+        current stream (which is made to wait for them)."""
+        out, n_anchor, done = handle
+        cur = torch.cuda.current_stream(out.device)
+        cur.wait_event(done)
+        out.record_stream(cur)
+        return out[:n_anchor], out[n_anchor:]
+
+    @torch.no_grad()
     def _momentum_update_key_encoder(self):
         """theta_k <- m theta_k + (1 - m) theta_q: one fused launch over the flat buffers
         (for the trainable BERT also rewriting encoder_k's bf16 operand shadow)."""

@@ -138,14 +138,38 @@ def train(args):
     print("[Runner] - Start training")
     pbar = tqdm(initial=init_step, total=total_steps, dynamic_ncols=True)
 
+    # LSTM heads on frozen BERT: the next micro-batch's BERT features are issued on
+    # a side stream before this micro-batch's heads step (bert_extract_async), so
+    # the two overlap; the loss values are those of the sequential loop.
+    prefetch = model.use_LSTM and args.device.type == "cuda"
+
+    def _issue(b):
+        idx, a, p = b
+        ids, mask = model.tokenize(list(a) + list(p), args.device)
+        return idx, model.bert_extract_async(ids, mask, len(a))
+
     while st.step_sum < total_steps:
-        for batch in train_loader:
+        it = iter(train_loader)
+        nxt = next(it, None)
+        pending = _issue(nxt) if (prefetch and nxt is not None) else None
+        while nxt is not None:
+            batch, nxt = nxt, next(it, None)
             try:
                 indexes, anchor_sample, positive_sample = batch
-                _, stepped = st.micro_batch(
-                    len(indexes),
-                    lambda: model(anchor_sample, positive_sample, args.device, cluster_result,
-                                  indexes))
+                if prefetch:
+                    cur_idx, handle = pending
+                    pending = _issue(nxt) if nxt is not None else None
+
+                    def fwd(handle=handle, cur_idx=cur_idx):
+                        a_feat, p_feat = model.features_ready(handle)
+                        return model.forward_features(a_feat, p_feat, cluster_result,
+                                                      cur_idx.view(-1))
+                else:
+                    def fwd(indexes=indexes, anchor_sample=anchor_sample,
+                            positive_sample=positive_sample):
+                        return model(anchor_sample, positive_sample, args.device,
+                                     cluster_result, indexes)
+                _, stepped = st.micro_batch(len(indexes), fwd)
                 if stepped:
                     pbar.update(1)
                     if st.step_sum % log_step == 0:

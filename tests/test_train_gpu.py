@@ -42,7 +42,7 @@ def _args_from_golden(fx):
                               sample="uniform")
 
 
-def _replay(gpu, precision):
+def _replay(gpu, precision, pipelined=False):
     from irc_amd.precision import get_precision, set_precision
     from src.model import build_model, get_optimizer
     from src.train import TrainState
@@ -63,12 +63,30 @@ def _replay(gpu, precision):
         losses = []
         total = int(fx["train_cfg"][2])
         acml = int(fx["train_cfg"][1])
-        for i in range(fx["mb_len"].shape[0]):
+        n_mb = fx["mb_len"].shape[0]
+
+        def batch(i):
             L, nb = int(fx["mb_len"][i]), int(fx["mb_B"][i])
             ids = torch.from_numpy(fx["mb_ids"][i, :2 * nb, :L]).to(gpu)
             mask = torch.from_numpy(fx["mb_mask"][i, :2 * nb, :L]).to(gpu)
-            loss, _ = st.micro_batch(
-                nb, lambda: model.forward_features(*model.bert_extract_ids(ids, mask, nb)))
+            return nb, ids, mask
+
+        pending = None
+        if pipelined:  # src/train.py's loop: BERT of micro-batch i+1 overlaps heads of i
+            nb0, ids0, mask0 = batch(0)
+            pending = model.bert_extract_async(ids0, mask0, nb0)
+        for i in range(n_mb):
+            nb, ids, mask = batch(i)
+            if pipelined:
+                handle = pending
+                if i + 1 < n_mb:
+                    nb1, ids1, mask1 = batch(i + 1)
+                    pending = model.bert_extract_async(ids1, mask1, nb1)
+                loss, _ = st.micro_batch(
+                    nb, lambda: model.forward_features(*model.features_ready(handle)))
+            else:
+                loss, _ = st.micro_batch(
+                    nb, lambda: model.forward_features(*model.bert_extract_ids(ids, mask, nb)))
             losses.append(loss.item() * acml)
             if st.step_sum >= total:
                 break
@@ -95,3 +113,16 @@ def test_train_trajectory_bf16(gpu):
     Micro-batch losses (~25-45) within 3% of the fp32 reference."""
     fx, losses, model = _replay(gpu, "bf16")
     np.testing.assert_allclose(losses, fx["mb_loss"], rtol=3e-2)
+
+
+def test_train_pipelined_bert_prefetch_matches_sequential(gpu):
+    """bert_extract_async (the next micro-batch's frozen-BERT features on a side
+    stream, as src/train.py and bench.py run it) changes only the overlap, never
+    the numbers: losses and final parameters bit-identical to the sequential loop."""
+    fx, seq_losses, seq_model = _replay(gpu, "bf16")
+    _, pipe_losses, pipe_model = _replay(gpu, "bf16", pipelined=True)
+    np.testing.assert_array_equal(pipe_losses, seq_losses)
+    a, b = seq_model.state_dict(), pipe_model.state_dict()
+    for k in a:
+        if k.startswith(("encoder_q", "encoder_k", "queue")):
+            assert torch.equal(a[k], b[k]), k
