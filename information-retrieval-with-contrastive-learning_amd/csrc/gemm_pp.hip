@@ -175,7 +175,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
     const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  // EPI_SCAN: query tiles fastest, so the blocks of one doc tile run back to back
+  // on one XCD and read it from that XCD's L2 (C4: 2048 queries = 8 query tiles)
+  const int tm = EPI == EPI_SCAN ? bid % tiles_m : bid / tiles_n;
+  const int tn = EPI == EPI_SCAN ? bid / tiles_m : bid % tiles_n;
   const int batch = blockIdx.y;
   const int kbeg = blockIdx.z * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
@@ -300,7 +303,11 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
     // its private LDS slot (16 x 16-byte writes, unconditional) and only the set
     // bits (a few per lane: the threshold admits ~16k of N per query) read their
     // score back by a dynamic LDS index for the exact-key / slot / store path.
+    // The slot's 16-byte chunk c sits at position c ^ (lane & 15): lanes' slots are
+    // 256 B apart, so unswizzled every lane of a ds_write_b128 would hit the same
+    // 4 banks (16-way conflicts on the 2 x 16 staging writes).
     float* slotv = reinterpret_cast<float*>(lds + 4096) + threadIdx.x * 64;
+    const int sw = lane & 15;
     uint64_t pm[2] = {0, 0};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -326,13 +333,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          *reinterpret_cast<f32x4*>(slotv + 16 * i + 4 * j) = acc[4 * hh + i][j];
+          *reinterpret_cast<f32x4*>(slotv + 4 * ((4 * i + j) ^ sw)) = acc[4 * hh + i][j];
       uint64_t bits = pm[hh];
       while (__ballot(bits != 0) != 0) {
         if (bits != 0) {
           const int b = __builtin_ctzll(bits);
           bits &= bits - 1;
-          const float v = slotv[b];
+          const float v = slotv[4 * ((b >> 2) ^ sw) + (b & 3)];
           const int bit = 64 * hh + b;
           const int ql = 128 * grp + 16 * (bit >> 4) + 4 * (lane >> 4) + (bit & 3);
           const int q = m0 + ql;

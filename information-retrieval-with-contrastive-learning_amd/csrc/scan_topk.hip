@@ -435,7 +435,7 @@ constexpr int SEL_NT = 256;
 constexpr int SEL_NW = SEL_NT / 64;
 constexpr int SEL_MAXK = 1024;
 constexpr int SEL_STAGE = 8192;  // candidates staged in LDS when they fit (64 KB)
-constexpr int SEL_MAXR = 2048;   // region table size for the parallel staging path
+constexpr int SEL_MAXR = 4096;   // region table size for the parallel staging path
 
 enum SelMode { SEL_THRESHOLD = 0, SEL_FINAL = 1 };
 
@@ -530,7 +530,7 @@ __device__ __forceinline__ void sort_and_emit(const uint64_t* cand, int cnt, int
 // One workgroup per query: the exact k-th largest distinct key among the
 // query's candidates by radix select, then the winners sorted.
 //  * Region sources: all region counts are loaded at once (each thread owns up
-//    to 8 consecutive regions), block-scanned, and turned into an LDS region-id
+//    to 16 consecutive regions), block-scanned, and turned into an LDS region-id
 //    map, so every candidate load is independent; the keys are staged in LDS
 //    (<= SEL_STAGE) and their min / max taken on the way.
 //  * Digits are 8 bits wide and start right below the candidates' common
@@ -576,11 +576,11 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
     const int R = src.nregions();
     table = R <= SEL_MAXR;
     if (table) {
-      const int rpt = (R + SEL_NT - 1) / SEL_NT;  // <= 8
-      uint32_t c[8];
+      const int rpt = (R + SEL_NT - 1) / SEL_NT;  // <= 16
+      uint32_t c[16];
       uint32_t mine = 0;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         const int r = tid * rpt + u;
         c[u] = (u < rpt && r < R) ? src.count(q, r) : 0u;
         mine += c[u];
@@ -600,7 +600,7 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
         M += s_wsum[w];
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         const int r = tid * rpt + u;
         if (u < rpt && r < R) {
           roff[r] = off;
@@ -1030,7 +1030,18 @@ struct Plan {
   size_t off_thr, off_cnt, off_keys, bytes;
 };
 
-// IRC_SCAN_PP=0 disables the GEMM-kernel filter; IRC_SCAN_PP_MINQ sets its Q floor.
+// IRC_SCAN_PP=0 disables the GEMM-kernel filter; IRC_SCAN_PP_MINQ sets its Q floor;
+// IRC_SCAN_PP_MAX_GB caps its survivor workspace (256 slots per (256-doc tile,
+// query) region: exact for any input, 8 KB x Q x N/256; default 24 GB of the
+// 288 GB HBM, i.e. up to Q = 2048 over a 1.5M-doc shard).
+static size_t pp_max_bytes() {
+  static const size_t v = [] {
+    const char* e = getenv("IRC_SCAN_PP_MAX_GB");
+    return (size_t)((e ? atof(e) : 24.0) * (double)(1ull << 30));
+  }();
+  return v;
+}
+
 static int pp_min_q() {
   static const int v = [] {
     const char* e = getenv("IRC_SCAN_PP");
@@ -1126,7 +1137,7 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   const size_t pp_keys = (size_t)p.pp_G * p.pp_qpad * p.pp_cap * 8;
   // the GEMM-kernel filter: bf16, or fp8 with 128-byte K-tiles (D % 128 == 0)
   p.pp = (eb == 2 || D % 128 == 0) && Q >= pp_min_q() && N >= 256 &&
-         pp_keys <= ((size_t)2 << 30);
+         pp_keys <= pp_max_bytes() && p.pp_G <= SEL_MAXR;
   if (p.pp) {
     const size_t pc = (size_t)p.pp_G * p.pp_qpad * 4;
     if (pc > cnt_bytes) cnt_bytes = pc;
