@@ -434,7 +434,7 @@ struct ListSource {  // merge input: [P][Q][kin] scores + global idx (-1 = empty
 constexpr int SEL_NT = 256;
 constexpr int SEL_NW = SEL_NT / 64;
 constexpr int SEL_MAXK = 1024;
-constexpr int SEL_STAGE = 8192;  // candidates staged in LDS when they fit (64 KB)
+constexpr int SEL_STAGE = 4096;  // candidates staged in LDS when they fit (32 KB)
 constexpr int SEL_MAXR = 4096;   // region table size for the parallel staging path
 
 enum SelMode { SEL_THRESHOLD = 0, SEL_FINAL = 1 };
@@ -542,8 +542,10 @@ __device__ __forceinline__ void sort_and_emit(const uint64_t* cand, int cnt, int
 //    the common prefix + 16 selected bits, lower bits zero.
 //  * The min(M, k) winners are sorted in registers by wave 0 (wave_sort_desc).
 // smul: power-of-two factor applied to the returned scores (fp8 descale).
-template <class Src>
-__global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode,
+// BIGK: k > 512 (the register sort then holds 16 keys per lane); the common
+// build sorts at most 512 and stays light enough for two workgroups per CU.
+template <class Src, bool BIGK>
+__device__ __forceinline__ void select_body(Src src, int k, int mode,
                                                          uint64_t* __restrict__ thr_out,
                                                          float* __restrict__ out_score,
                                                          int64_t* __restrict__ out_idx,
@@ -769,10 +771,26 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel(Src src, int k, int mode
     if (cnt <= 64) sort_and_emit<1>(cand, cnt, k, q, lane, smul, out_score, out_idx);
     else if (cnt <= 128) sort_and_emit<2>(cand, cnt, k, q, lane, smul, out_score, out_idx);
     else if (cnt <= 256) sort_and_emit<4>(cand, cnt, k, q, lane, smul, out_score, out_idx);
-    else if (cnt <= 512) sort_and_emit<8>(cand, cnt, k, q, lane, smul, out_score, out_idx);
+    else if (cnt <= 512 || !BIGK) sort_and_emit<8>(cand, cnt, k, q, lane, smul, out_score, out_idx);
     else sort_and_emit<16>(cand, cnt, k, q, lane, smul, out_score, out_idx);
   }
   STAMP(mode, 14);
+}
+
+template <class Src>
+__global__ __launch_bounds__(SEL_NT) __attribute__((amdgpu_waves_per_eu(2)))
+void select_kernel(Src src, int k, int mode, uint64_t* __restrict__ thr_out,
+                   float* __restrict__ out_score, int64_t* __restrict__ out_idx, float smul) {
+  select_body<Src, false>(src, k, mode, thr_out, out_score, out_idx, smul);
+}
+
+template <class Src>
+__global__ __launch_bounds__(SEL_NT) void select_kernel_bigk(Src src, int k, int mode,
+                                                             uint64_t* __restrict__ thr_out,
+                                                             float* __restrict__ out_score,
+                                                             int64_t* __restrict__ out_idx,
+                                                             float smul) {
+  select_body<Src, true>(src, k, mode, thr_out, out_score, out_idx, smul);
 }
 
 // Wave-per-query select for region sources (the scan's two selects): the same
@@ -1005,8 +1023,12 @@ static void launch_select(const RegionSource& src, int Q, int k, int mode, uint6
     hipLaunchKernelGGL(select_wave_kernel, dim3((unsigned)((Q + SWQ - 1) / SWQ)), dim3(64 * SWQ),
                        0, st, src, Q, k, mode, thr, out_score, out_idx, smul);
   else
-    hipLaunchKernelGGL((select_kernel<RegionSource>), dim3((unsigned)Q), dim3(SEL_NT), 0, st, src,
-                       k, mode, thr, out_score, out_idx, smul);
+    if (k > 512)
+      hipLaunchKernelGGL((select_kernel_bigk<RegionSource>), dim3((unsigned)Q), dim3(SEL_NT), 0,
+                         st, src, k, mode, thr, out_score, out_idx, smul);
+    else
+      hipLaunchKernelGGL((select_kernel<RegionSource>), dim3((unsigned)Q), dim3(SEL_NT), 0, st,
+                         src, k, mode, thr, out_score, out_idx, smul);
 }
 
 // ------------------------------------------------------------------ planning
@@ -1113,7 +1135,8 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   p.qpad = p.gy * qb;
   // Sample of N/8 docs (>= 32k; GMAX leaves 2*KS keys per 32-doc tile, so >= 2k
   // group maxima per query for the threshold select, capped at its LDS stage).
-  // The filter's survivors ~ k * N / S (~8k per query).
+  // The filter's survivors ~ k * N / S (~8k per query; at the cap, e.g. a 625k
+  // shard, ~k * N / 32768).
   int64_t s_target = 32 * k;
   if (N / 8 > s_target) s_target = N / 8;
   const int64_t s_cap = (int64_t)SEL_STAGE * TD / (2 * p.ks);
@@ -1410,8 +1433,13 @@ extern "C" int irc_topk_merge(const float* in_score, const int64_t* in_idx, int6
   IRC_REQUIRE(kout >= 1 && kout <= SEL_MAXK, "topk_merge: kout outside [1, %d]", SEL_MAXK);
   if (Q == 0) return IRC_OK;
   ListSource src{in_score, in_idx, (int)P, (int)Q, (int)kin};
-  hipLaunchKernelGGL((select_kernel<ListSource>), dim3(Q), dim3(SEL_NT), 0, as_stream(stream),
-                     src, (int)kout, (int)SEL_FINAL, nullptr, out_score, out_idx, 1.0f);
+  if (kout > 512)
+    hipLaunchKernelGGL((select_kernel_bigk<ListSource>), dim3(Q), dim3(SEL_NT), 0,
+                       as_stream(stream), src, (int)kout, (int)SEL_FINAL, nullptr, out_score,
+                       out_idx, 1.0f);
+  else
+    hipLaunchKernelGGL((select_kernel<ListSource>), dim3(Q), dim3(SEL_NT), 0, as_stream(stream),
+                       src, (int)kout, (int)SEL_FINAL, nullptr, out_score, out_idx, 1.0f);
   return check_launch("select_kernel(merge)");
 }
 
