@@ -42,13 +42,16 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
+FP8_PEAK_TFS = 5000.0  # dense fp8 MFMA (MI355X_MICROARCH.md chip table)
 BF16_PEAK_TFS = 2500.0  # dense bf16 MFMA spec
 
 METRIC = "query-doc pairs/sec (train) + queries/sec @ top-k over N docs, 1/2/4/8 GPU"
 TRAIN_B, TRAIN_L, VOCAB = 256, 64, 30522
 SCAN_N_PER_GPU, SCAN_Q, SCAN_D, SCAN_K = 100_000, 256, 768, 100
-# C5 retrieval leg: 5M docs over 8 GPUs = 625k e4m3 docs per GPU (weak scaling)
+# C4 / C5 retrieval legs: 5M docs over 8 GPUs = 625k docs per GPU (weak scaling),
+# 2048 queries per batch; C4 is BERT-large (D = 1024, bf16), C5 fp8 (D = 768, e4m3)
 FP8_N_PER_GPU = 625_000
+C4_Q, C4_D, C5_Q = 2048, 1024, 2048
 PP_MIN_Q = 192  # irc_scan_topk's filter runs on the ping-pong GEMM kernel from this Q
 
 
@@ -303,25 +306,26 @@ def cpu_baseline_train(model, budget_s):
                       "numpy fp32 oracle"}
 
 
-def _filter_kernel_name(q, dtype):
+def _filter_kernel_name(q, d, dtype):
     if q >= PP_MIN_Q:
         mf = ("v_mfma_scale_f32_16x16x128_f8f6f4" if dtype == "fp8"
               else "v_mfma_f32_16x16x32_bf16")
         return f"gemm_pp_kernel<EPI_SCAN> (scan filter, 256x256 tiles, {mf})"
     mf = "v_mfma_f32_32x32x16_fp8_fp8" if dtype == "fp8" else "v_mfma_f32_32x32x16_bf16"
-    return f"scan_tile_kernel<{SCAN_D}> (scan filter, stationary queries, {mf})"
+    return f"scan_tile_kernel<{d}> (scan filter, stationary queries, {mf})"
 
 
-def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16"):
+def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16", nq=SCAN_Q,
+             dim=SCAN_D, sweep=True):
     from irc_amd import _lib, retrieval
 
     lib = _lib.load()
-    g = torch.Generator().manual_seed(2024 + rank)
-    shard = torch.nn.functional.normalize(torch.randn(n_per_gpu, SCAN_D, generator=g))
-    shard = shard.bfloat16().to(dev)
+    g = torch.Generator(device=dev).manual_seed(2024 + rank)
+    shard = torch.randn(n_per_gpu, dim, generator=g, device=dev)
+    shard = torch.nn.functional.normalize(shard).bfloat16()
     gq = torch.Generator().manual_seed(7)
-    allq = torch.nn.functional.normalize(torch.randn(SCAN_Q, SCAN_D, generator=gq)).bfloat16()
-    myq = allq[rank * SCAN_Q // world:(rank + 1) * SCAN_Q // world].to(dev)
+    allq = torch.nn.functional.normalize(torch.randn(nq, dim, generator=gq)).bfloat16()
+    myq = allq[rank * nq // world:(rank + 1) * nq // world].to(dev)
     index = retrieval.ShardedDenseIndex(shard, doc_offset=rank * n_per_gpu,
                                         group=dist.group.WORLD if world > 1 else None,
                                         dtype=dtype)
@@ -344,28 +348,37 @@ def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16"):
     lib.irc_prof_enable(0)
     dt = _max_over_ranks(dt, dev, world)
     k_s, k_n, k_bytes = _prof(lib, "scan_filter")
-    sweep = scan_q_sweep(index, dev) if rank == 0 else None
+    sweep = scan_q_sweep(index, dev, dim) if (rank == 0 and sweep) else None
     kavg = k_s / max(k_n, 1)
-    achieved = (k_bytes / max(k_n, 1)) / kavg / 1e9 if k_n else None
+    gbs = (k_bytes / max(k_n, 1)) / kavg / 1e9 if k_n else None
+    tfs = 2 * nq * n_per_gpu * dim / kavg / 1e12 if k_n else None
+    # bound: arithmetic intensity 2*Q*D flops per D*b doc bytes against the ridge
+    # (bf16 2.5 PF / 8 TB/s = 312 flop/B; fp8 5 PF / 8 TB/s = 625)
+    b = 1 if dtype == "fp8" else 2
+    mfma_peak = FP8_PEAK_TFS if dtype == "fp8" else BF16_PEAK_TFS
+    mfma_bound = 2.0 * nq / b > mfma_peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if mfma_bound:
+        roof = {"bound": "mfma", "achieved": tfs, "peak": mfma_peak, "unit": "TFLOP/s",
+                "frac": tfs / mfma_peak if tfs else None, "traffic": None, "hbm_GB_s": gbs}
+    else:
+        roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS if gbs else None,
+                "traffic": _pmc_traffic("scan_filter") if dtype == "bf16" else None,
+                "mfma_tflops": tfs}
+    roof.update({"kernel": _filter_kernel_name(nq, dim, dtype), "kernel_avg_us": kavg * 1e6,
+                 "alg_bytes_per_launch": k_bytes / max(k_n, 1)})
     return {
-        "value": SCAN_Q * args.steps / dt, "unit": "queries/s",
+        "value": nq * args.steps / dt, "unit": "queries/s",
         "ms_per_batch": dt * 1e3 / args.steps, "dtype": dtype,
         "docs_per_gpu": n_per_gpu,
-        "docs_total": n_per_gpu * world, "queries": SCAN_Q, "dim": SCAN_D, "k": SCAN_K,
-        "query_doc_pairs_per_s": SCAN_Q * n_per_gpu * world * args.steps / dt,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS if achieved else None,
-                     "traffic": _pmc_traffic("scan_filter") if dtype == "bf16" else None,
-                     "kernel": _filter_kernel_name(SCAN_Q, dtype),
-                     "kernel_avg_us": kavg * 1e6,
-                     "alg_bytes_per_launch": k_bytes / max(k_n, 1),
-                     "mfma_tflops": 2 * SCAN_Q * n_per_gpu * SCAN_D / kavg / 1e12
-                     if k_n else None},
+        "docs_total": n_per_gpu * world, "queries": nq, "dim": dim, "k": SCAN_K,
+        "query_doc_pairs_per_s": nq * n_per_gpu * world * args.steps / dt,
+        "roofline": roof,
         "q_sweep_local": sweep,
     }
 
 
-def scan_q_sweep(index, dev, qs=(1, 16, 64, 256), reps=20):
+def scan_q_sweep(index, dev, dim=SCAN_D, qs=(1, 16, 64, 256), reps=20):
     """Local scan filter at several query-batch sizes (SURVEY.md 8d grades the HBM
     fraction at Q in {1, 16, 64, 256}): kernel HIP-event time and algorithmic bytes
     (N*D*b + Q*D*b) -> GB/s, plus the whole call's queries/s (query quantisation
@@ -376,7 +389,7 @@ def scan_q_sweep(index, dev, qs=(1, 16, 64, 256), reps=20):
     out = []
     for q in qs:
         g = torch.Generator().manual_seed(11 + q)
-        qq = torch.nn.functional.normalize(torch.randn(q, SCAN_D, generator=g)).bfloat16().to(dev)
+        qq = torch.nn.functional.normalize(torch.randn(q, dim, generator=g)).bfloat16().to(dev)
         for _ in range(3):
             index._local_topk(qq, SCAN_K)
         torch.cuda.synchronize()
@@ -438,11 +451,14 @@ def main():
     bert = None
     if args.part in ("all", "bert"):
         bert = run_train_bert(args, rank, world, dev)
-    scan_fp8 = None
+    scan_fp8 = scan_c4 = None
     if args.part in ("all", "scan"):
         scan = run_scan(args, rank, world, dev)
         torch.cuda.empty_cache()
-        scan_fp8 = run_scan(args, rank, world, dev, FP8_N_PER_GPU, "fp8")
+        scan_c4 = run_scan(args, rank, world, dev, FP8_N_PER_GPU, "bf16", C4_Q, C4_D,
+                           sweep=False)
+        torch.cuda.empty_cache()
+        scan_fp8 = run_scan(args, rank, world, dev, FP8_N_PER_GPU, "fp8", C5_Q, SCAN_D)
     cpu_t = cpu_s = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if train is not None:
@@ -485,9 +501,14 @@ def main():
             line["train_bert"] = bert
         if scan is not None:
             line["retrieval"] = scan
+        if scan_c4 is not None:
+            scan_c4["workload"] = (f"C4 retrieval shard: {FP8_N_PER_GPU} bf16 docs/GPU x D="
+                                   f"{C4_D} (BERT-large, 5M over 8 GPUs), {C4_Q} queries, "
+                                   f"top-{SCAN_K}")
+            line["retrieval_c4"] = scan_c4
         if scan_fp8 is not None:
             scan_fp8["workload"] = (f"C5 retrieval shard: {FP8_N_PER_GPU} e4m3 docs/GPU "
-                                    f"(5M over 8 GPUs), {SCAN_Q} queries, top-{SCAN_K}")
+                                    f"(5M over 8 GPUs), {C5_Q} queries, top-{SCAN_K}")
             line["retrieval_fp8"] = scan_fp8
         print(json.dumps(line), flush=True)
     if world > 1:
