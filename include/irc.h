@@ -286,6 +286,39 @@ int irc_prof_enable(int on);
 int irc_prof_query(const char* name, double* total_ms, int64_t* count, double* work);
 int irc_prof_reset(void);
 
+/* ---- Sparse hashed n-gram TF-IDF retrieval ----------
+ * The reference's real predict path.  A CSR matrix [hash_size rows][n_cols docs]
+ * (indptr int64 [rows+1], indices int32, data fp64), resident on the device;
+ * queries are lists of (row, weight) in ascending row order, flattened with
+ * offsets q_off [Q+1] (n_pairs = q_off[Q]).
+ *
+ * documents_filtering (src/evaluation.py:57-81): the sorted unique docs with a
+ * nonzero in any of a query's rows.  irc_csr_union_count marks one bitmap per
+ * query (bitmaps: Q * ceil(n_cols/32) words) and writes per-chunk counts
+ * (chunk_sums: Q * irc_csr_union_chunks(n_cols)); the caller sums a query's
+ * chunks into out_off [Q+1] and irc_csr_union_emit writes the indices. */
+int64_t irc_csr_union_chunks(int64_t n_cols);
+int irc_csr_union_count(const int64_t* indptr, const int32_t* indices, int64_t n_cols,
+                        const int64_t* q_off, const int64_t* q_rows, int64_t Q, int64_t n_pairs,
+                        uint32_t* bitmaps, int64_t* chunk_sums, irc_stream_t stream);
+int irc_csr_union_emit(const uint32_t* bitmaps, int64_t n_cols, int64_t Q,
+                       const int64_t* chunk_sums, const int64_t* out_off, int32_t* out_idx,
+                       irc_stream_t stream);
+/* TfidfDocRanker.closest_docs' spvec * doc_mat
+ * (preprocessing/drqa/retriever/tfidf_doc_ranker.py:64-65): dense [Q][n_cols]
+ * (zeroed by the caller) += w * row, rows in the given order, fp64 multiply and
+ * add rounded separately -- scipy's accumulation order, bit-identical scores. */
+int irc_csr_spmv_f64(const int64_t* indptr, const int32_t* indices, const double* data,
+                     int64_t n_cols, const int64_t* q_off, const int64_t* q_rows,
+                     const double* q_w, int64_t Q, double* dense, irc_stream_t stream);
+/* Top-k of the nonzero dense[q][cand] over each query's candidate docs (cand,
+ * ascending, offsets cand_off [Q+1]): (score desc, doc index asc), k <= 1024;
+ * out_n[q] = number of valid entries, the rest (0, -1)
+ * (tfidf_doc_ranker.py:67-73). */
+int irc_topk_f64(const double* dense, int64_t n_cols, const int32_t* cand,
+                 const int64_t* cand_off, int64_t Q, int64_t k, double* out_score,
+                 int64_t* out_idx, int32_t* out_n, irc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,6 +34,11 @@ SIGNATURES = {
     "irc_scan_topk_fp8": (I32, [P, P, I64, I64, I64, I64, I64, F32, P, I64, P, P, P]),
     "irc_scan_scores_fp8": (I32, [P, P, I64, I64, I64, P, P]),
     "irc_quantize_fp8": (I32, [I32, P, I64, F32, P, P]),
+    "irc_csr_union_chunks": (I64, [I64]),
+    "irc_csr_union_count": (I32, [P, P, I64, P, P, I64, I64, P, P, P]),
+    "irc_csr_union_emit": (I32, [P, I64, I64, P, P, P, P]),
+    "irc_csr_spmv_f64": (I32, [P, P, P, I64, P, P, P, I64, P, P]),
+    "irc_topk_f64": (I32, [P, I64, P, P, I64, I64, P, P, P, P]),
     "irc_gemm": (I32, [I32, I32, I32, I32, I32, I64, I64, I64, F32, P, I64, I64, P, I64, I64,
                        P, I64, P, I64, I64, P, I64, I64, I32, I64, P, I64, P]),
     "irc_gemm_workspace": (I64, [I32, I32, I32, I64, I64, I64, I64]),

@@ -6,8 +6,8 @@ out (:110-115).  Here ``predict`` does the dense path the reference sketches:
 ``ctx2vec`` embeddings (contrastive_module.py:96-100) of the evidence corpus are
 sharded into HBM and each claim batch is scored against all of them with the
 exact top-k scan (irc_amd.retrieval, closest_docs ordering,
-tfidf_doc_ranker.py:60-75).  ``documents_filtering`` (the sparse filter) is the
-"next" row of SURVEY.md 8f and raises until it is built.
+tfidf_doc_ranker.py:60-75).  ``documents_filtering`` -- the sparse filter the
+reference's predict actually calls -- runs on the GPU too (irc_amd.sparse).
 """
 import time
 
@@ -15,12 +15,40 @@ import torch
 from tqdm import tqdm
 
 from irc_amd.retrieval import ShardedDenseIndex
+from irc_amd.sparse import SparseIndex
 from src.dataset import get_dataloader
 from src.model import load_model
 
 
+_SPARSE_CACHE = {}
+
+
+def _sparse_index(count_matrix, metadata, device):
+    """The inverted count matrix resident in HBM, built once per matrix object."""
+    key = (id(count_matrix), str(device))
+    idx = _SPARSE_CACHE.get(key)
+    if idx is None:
+        idx = _SPARSE_CACHE[key] = SparseIndex(count_matrix, ngram=metadata["ngram"],
+                                               device=device)
+    return idx
+
+
 def documents_filtering(claim, args, count_matrix, metadata, full_doc_dict, bigram_only=True):
-    raise NotImplementedError("sparse hashed-ngram candidate filter: SURVEY.md 8f row 2")
+    """src/evaluation.py:57-81: {doc_id: doc} of the docs sharing a hashed n-gram
+    with the claim.  Tokenisation and hashing on the host (irc_amd.sparse, the
+    reference's SimpleTokenizer / filter_ngram / murmurhash3); the row union over
+    the inverted count matrix on the GPU (irc_csr_union_*)."""
+    if metadata.get("tokenizer", "simple") != "simple":
+        raise ValueError("only the DrQA 'simple' tokenizer is supported on this path")
+    device = getattr(args, "device", None) or torch.device("cuda")
+    index = _sparse_index(count_matrix, metadata, device)
+    doc_ids = metadata["doc_dict"][1]
+    docs = {}
+    for i in index.documents_filtering([claim], bigram_only)[0]:
+        doc_id = doc_ids[int(i)]
+        if doc_id in full_doc_dict:  # the reference skips ids missing from the dict
+            docs[doc_id] = full_doc_dict[doc_id]
+    return docs
 
 
 @torch.no_grad()

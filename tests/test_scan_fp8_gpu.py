@@ -62,6 +62,7 @@ def test_scores_exact_on_grid(gpu, Q, D):
     (200, 30_000, 1024, 50, 7),  # D = 1024, GEMM-kernel filter (scaled fp8 MFMA)
     (256, 100_000, 768, 100, 0),  # C5 dims, GEMM-kernel filter
     (384, 9_000, 384, 1024, 0),  # two query tiles, D = 384 (3 K-tiles), max k
+    (1024, 12_000, 256, 100, 9),  # four query tiles sharing each doc tile
 ])
 def test_topk_exact_vs_oracle(gpu, Q, N, D, k, off):
     from irc_amd import retrieval

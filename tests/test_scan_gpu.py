@@ -69,6 +69,7 @@ def test_golden_ties(gpu):
     (128, 60000, 768, 100, 0),  # two-phase, C2 dims
     (200, 30000, 256, 1024, 7),  # maximum k, ragged Q
     (384, 9000, 64, 50, 0),     # two query tiles, D = 64 (one K-tile)
+    (1024, 12000, 128, 100, 9),  # four query tiles sharing each doc tile (C3-style batch)
 ])
 def test_topk_exact_vs_oracle(gpu, Q, N, D, k, off):
     from irc_amd import retrieval
