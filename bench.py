@@ -410,6 +410,57 @@ def scan_q_sweep(index, dev, dim=SCAN_D, qs=(1, 16, 64, 256), reps=20):
     return out
 
 
+def run_sparse(args, dev, cpu_baseline):
+    """Sparse hashed n-gram TF-IDF ranking (the reference's own
+    predict path): a synthetic Zipf-distributed TF-IDF matrix [2^22 hashes x 200k
+    docs, ~100 n-grams per doc], 64 claims of 16 hashed n-grams, top-100 --
+    GPU (irc_csr_spmv_f64 + irc_csr_union + irc_topk_f64, scores bit-identical to
+    scipy) vs the reference's CPU arithmetic (scipy spvec * doc_mat + argpartition)."""
+    import scipy.sparse as sp
+
+    from irc_amd import sparse
+
+    rng = np.random.default_rng(11)
+    H, N, per_doc, Qn, per_q, k = 1 << 22, 200_000, 100, 64, 16, 100
+    zipf = lambda size: np.minimum(rng.zipf(1.3, size), H) - 1  # noqa: E731
+    rows = zipf(N * per_doc)
+    cols = np.repeat(np.arange(N), per_doc)
+    m = sp.csr_matrix((np.log1p(rng.integers(1, 4, N * per_doc)).astype(np.float64), (rows, cols)),
+                      shape=(H, N))
+    m.sum_duplicates()
+    index = sparse.SparseIndex(m, device=dev)
+    q_rows = [np.unique(zipf(per_q)) for _ in range(Qn)]
+    q_w = [rng.random(len(r)) + 0.1 for r in q_rows]
+    for _ in range(2):
+        index.topk_rows(q_rows, q_w, k)
+    torch.cuda.synchronize()
+    reps = max(args.steps, 3)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        index.topk_rows(q_rows, q_w, k)
+    torch.cuda.synchronize()
+    gpu_qps = Qn * reps / (time.perf_counter() - t0)
+    out = {"value": gpu_qps, "unit": "queries/s", "queries": Qn, "k": k, "docs": N,
+           "hash_size": H, "nnz": int(m.nnz),
+           "workload": "Zipf(1.3) hashed n-gram TF-IDF, 200k docs x ~100 n-grams, 64 claims "
+                       "x 16 n-grams, top-100 (includes host packing and result copies)"}
+    if cpu_baseline:
+        t0, n = time.perf_counter(), 0
+        while time.perf_counter() - t0 < 5.0 and n < Qn:
+            spv = sp.csr_matrix((q_w[n], q_rows[n], np.array([0, len(q_rows[n])])), shape=(1, H))
+            res = spv * m
+            if len(res.data) > k:
+                o = np.argpartition(-res.data, k)[:k]
+                o[np.argsort(-res.data[o])]
+            n += 1
+        out["cpu_baseline"] = {"value": n / (time.perf_counter() - t0), "unit": "queries/s",
+                               "cores": 1, "kind": "reference",
+                               "sample": f"{n} claims through the reference's arithmetic "
+                                         "(scipy csr product + argpartition/argsort, "
+                                         "tfidf_doc_ranker.py:60-75), single thread"}
+    return out
+
+
 def cpu_baseline_scan(budget_s):
     from oracle import bench_cpu
 
@@ -467,6 +518,10 @@ def main():
             cpu_s = cpu_baseline_scan(args.cpu_budget)
     if scan is not None:
         scan["cpu_baseline"] = cpu_s
+    sparse_leg = None
+    if args.part in ("all", "scan") and rank == 0 and world == 1:
+        torch.cuda.empty_cache()
+        sparse_leg = run_sparse(args, dev, not args.no_cpu_baseline)
     if rank == 0:
         if train is not None:
             head = {"value": train["pairs_per_s"], "unit": "pairs/s",
@@ -506,6 +561,8 @@ def main():
                                    f"{C4_D} (BERT-large, 5M over 8 GPUs), {C4_Q} queries, "
                                    f"top-{SCAN_K}")
             line["retrieval_c4"] = scan_c4
+        if sparse_leg is not None:
+            line["sparse_tfidf"] = sparse_leg
         if scan_fp8 is not None:
             scan_fp8["workload"] = (f"C5 retrieval shard: {FP8_N_PER_GPU} e4m3 docs/GPU "
                                     f"(5M over 8 GPUs), {C5_Q} queries, top-{SCAN_K}")

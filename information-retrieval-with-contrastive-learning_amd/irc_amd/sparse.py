@@ -203,9 +203,13 @@ class SparseIndex:
         if self.doc_freqs is None:
             raise ValueError("closest_docs needs doc_freqs (build with doc_freqs(counts))")
         vecs = [self.text2spvec(q) for q in queries]
-        rows = [v[0] for v in vecs]
-        Q = len(queries)
-        t_off, t_rows, t_w, _ = self._pack(rows, [v[1] for v in vecs])
+        return self.topk_rows([v[0] for v in vecs], [v[1] for v in vecs], k)
+
+    def topk_rows(self, rows, weights, k: int):
+        """Top-k docs of sum_r w_r * A[r] per query (rows ascending, fp64 weights):
+        [(doc indices, fp64 scores)], (score desc, index asc), nonzero scores only."""
+        Q = len(rows)
+        t_off, t_rows, t_w, _ = self._pack(rows, weights)
         dense = torch.zeros((Q, self.n_docs), dtype=torch.float64, device=self.device)
         st = stream_ptr(self.device)
         _lib.call("irc_csr_spmv_f64", ptr(self.indptr), ptr(self.indices), ptr(self.data),
