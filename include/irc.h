@@ -306,7 +306,8 @@ int irc_csr_union_emit(const uint32_t* bitmaps, int64_t n_cols, int64_t Q,
                        irc_stream_t stream);
 /* TfidfDocRanker.closest_docs' spvec * doc_mat
  * (preprocessing/drqa/retriever/tfidf_doc_ranker.py:64-65): dense [Q][n_cols]
- * (zeroed by the caller) += w * row, rows in the given order, fp64 multiply and
+ * (zeroed by the caller) += w * row, rows in the given order (CSR indices sorted
+ * within each row), fp64 multiply and
  * add rounded separately -- scipy's accumulation order, bit-identical scores. */
 int irc_csr_spmv_f64(const int64_t* indptr, const int32_t* indices, const double* data,
                      int64_t n_cols, const int64_t* q_off, const int64_t* q_rows,

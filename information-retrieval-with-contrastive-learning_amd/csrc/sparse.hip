@@ -25,7 +25,9 @@ namespace sparse {
 constexpr int NT = 256;
 constexpr int64_t CHUNK_WORDS = 8192;  // bitmap words per compaction chunk (256 K docs)
 
-// grid.x: (query, row) pairs via q_off; each block ORs one row's doc bits.
+// grid (pairs, SEG): block (pair, s) ORs the doc bits of segment s of the pair's
+// row -- long (Zipf-head) rows are spread over SEG workgroups.
+constexpr int SEG = 16;
 __global__ __launch_bounds__(NT) void union_mark_kernel(const int64_t* __restrict__ indptr,
                                                         const int32_t* __restrict__ indices,
                                                         const int64_t* __restrict__ q_off,
@@ -42,7 +44,9 @@ __global__ __launch_bounds__(NT) void union_mark_kernel(const int64_t* __restric
   const int64_t q = lo;
   const int64_t r = q_rows[pair];
   uint32_t* bm = bitmaps + q * words;
-  for (int64_t j = indptr[r] + threadIdx.x; j < indptr[r + 1]; j += NT) {
+  const int64_t b = indptr[r], len = indptr[r + 1] - b;
+  const int64_t j0 = b + len * blockIdx.y / SEG, j1 = b + len * (blockIdx.y + 1) / SEG;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += NT) {
     const uint32_t d = (uint32_t)indices[j];
     atomicOr(&bm[d >> 5], 1u << (d & 31));
   }
@@ -110,9 +114,22 @@ __global__ __launch_bounds__(NT) void union_emit_kernel(const uint32_t* __restri
   }
 }
 
-// One workgroup per query: dense[q][doc] += w_r * A[r][doc] for the query's rows
-// in the given (ascending) order; a barrier between rows orders the updates of a
-// doc that two rows share.  fp64 multiply and add rounded separately.
+__device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a, int64_t lo,
+                                                   int64_t hi, int32_t x) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// grid (DR doc ranges, Q): dense[q][doc] += w_r * A[r][doc] for the query's rows
+// in the given (ascending) order.  Each doc belongs to one workgroup (its doc
+// range; CSR rows are index-sorted, so a range is a binary-searched slice of
+// every row), and a barrier between rows orders the updates of a doc two rows
+// share -- every doc sees its products in row order.  fp64 multiply and add
+// rounded separately.
+constexpr int DR = 32;
 __global__ __launch_bounds__(NT) void spmv_f64_kernel(const int64_t* __restrict__ indptr,
                                                       const int32_t* __restrict__ indices,
                                                       const double* __restrict__ data,
@@ -122,12 +139,16 @@ __global__ __launch_bounds__(NT) void spmv_f64_kernel(const int64_t* __restrict_
                                                       int64_t n_cols,
                                                       double* __restrict__ dense) {
 #pragma clang fp contract(off)  // a separately rounded product and sum, as scipy
-  const int64_t q = blockIdx.x;
+  const int64_t q = blockIdx.y;
   double* row_out = dense + q * n_cols;
+  const int32_t d0 = (int32_t)(n_cols * blockIdx.x / DR);
+  const int32_t d1 = (int32_t)(n_cols * (blockIdx.x + 1) / DR);
   for (int64_t p = q_off[q]; p < q_off[q + 1]; ++p) {
     const int64_t r = q_rows[p];
     const double w = q_w[p];
-    for (int64_t j = indptr[r] + threadIdx.x; j < indptr[r + 1]; j += NT) {
+    const int64_t lo = lower_bound_i32(indices, indptr[r], indptr[r + 1], d0);
+    const int64_t hi = lower_bound_i32(indices, lo, indptr[r + 1], d1);
+    for (int64_t j = lo + threadIdx.x; j < hi; j += NT) {
       const int32_t d = indices[j];
       const double prod = w * data[j];
       row_out[d] = row_out[d] + prod;
@@ -333,7 +354,7 @@ extern "C" int irc_csr_union_count(const int64_t* indptr, const int32_t* indices
   if (words > 0 && hipMemsetAsync(bitmaps, 0, (size_t)Q * words * 4, st) != hipSuccess)
     return check_launch("csr_union memset");
   if (n_pairs > 0)
-    hipLaunchKernelGGL(union_mark_kernel, dim3((unsigned)n_pairs), dim3(NT), 0, st, indptr,
+    hipLaunchKernelGGL(union_mark_kernel, dim3((unsigned)n_pairs, SEG), dim3(NT), 0, st, indptr,
                        indices, q_off, q_rows, Q, words, bitmaps);
   if (int rc = check_launch("union_mark_kernel")) return rc;
   if (nchunks > 0)
@@ -360,8 +381,8 @@ extern "C" int irc_csr_spmv_f64(const int64_t* indptr, const int32_t* indices, c
                                 irc_stream_t stream) {
   IRC_REQUIRE(n_cols >= 0 && Q >= 0, "csr_spmv_f64: negative size");
   if (Q == 0) return IRC_OK;
-  hipLaunchKernelGGL(spmv_f64_kernel, dim3((unsigned)Q), dim3(NT), 0, as_stream(stream), indptr,
-                     indices, data, q_off, q_rows, q_w, n_cols, dense);
+  hipLaunchKernelGGL(spmv_f64_kernel, dim3(DR, (unsigned)Q), dim3(NT), 0, as_stream(stream),
+                     indptr, indices, data, q_off, q_rows, q_w, n_cols, dense);
   return check_launch("spmv_f64_kernel");
 }
 

@@ -126,6 +126,8 @@ class SparseIndex:
     def __init__(self, matrix, ngram: int = 2, doc_freqs_=None, device=None):
         device = torch.device(device or "cuda")
         m = matrix.tocsr()
+        if not m.has_sorted_indices:  # the doc-range split of irc_csr_spmv_f64 needs them
+            m = m.sorted_indices()
         self.hash_size, self.n_docs = m.shape
         self.ngram = int(ngram)
         self.indptr = torch.from_numpy(m.indptr.astype(np.int64)).to(device)
