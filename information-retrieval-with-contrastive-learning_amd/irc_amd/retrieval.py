@@ -155,6 +155,54 @@ class ShardedDenseIndex:
         self.doc_offset = int(doc_offset)
         self.group = group
 
+    # ------------------------------------------------------------ persistence
+    # On-disk corpus index: one .npy per shard (bf16 as
+    # uint16 bits, or e4m3 bytes), a JSON header, and the DrQA-style doc-id map
+    # (doc_dict = (DOC2IDX, doc_ids), preprocessing/drqa/build_tfidf.py:126,198-205).
+    def save(self, directory: str, rank: int = 0, doc_ids=None) -> None:
+        import json
+        import os
+
+        import numpy as np
+
+        os.makedirs(directory, exist_ok=True)
+        raw = self.docs.view(torch.uint16) if self.dtype == "bf16" else self.docs
+        np.save(os.path.join(directory, f"shard_{rank}.npy"), raw.cpu().numpy())
+        meta = {"dtype": self.dtype, "fp8_scale": self.fp8_scale, "doc_offset": self.doc_offset,
+                "rows": int(self.docs.shape[0]), "dim": int(self.docs.shape[1])}
+        with open(os.path.join(directory, f"shard_{rank}.json"), "w") as f:
+            json.dump(meta, f)
+        if doc_ids is not None:
+            with open(os.path.join(directory, "doc_ids.json"), "w") as f:
+                json.dump(list(doc_ids), f)
+
+    @classmethod
+    def load(cls, directory: str, rank: int = 0, device=None, group=None):
+        """(index, doc_dict or None): the shard saved by save() for this rank,
+        resident on `device` (no re-quantisation: the stored bytes are used)."""
+        import json
+        import os
+
+        import numpy as np
+
+        with open(os.path.join(directory, f"shard_{rank}.json")) as f:
+            meta = json.load(f)
+        raw = torch.from_numpy(np.load(os.path.join(directory, f"shard_{rank}.npy")))
+        raw = raw.to(device or "cuda")
+        self = cls.__new__(cls)
+        self.dtype = meta["dtype"]
+        self.fp8_scale = float(meta["fp8_scale"])
+        self.docs = raw.view(torch.bfloat16) if self.dtype == "bf16" else raw
+        self.doc_offset = int(meta["doc_offset"])
+        self.group = group
+        doc_dict = None
+        ids_path = os.path.join(directory, "doc_ids.json")
+        if os.path.exists(ids_path):
+            with open(ids_path) as f:
+                ids = json.load(f)
+            doc_dict = ({d: i for i, d in enumerate(ids)}, ids)
+        return self, doc_dict
+
     # The two device steps are methods so the collective orchestration can be
     # exercised on CPU (gloo) with a test double in tests/test_dist_cpu.py.
     def _local_topk(self, queries, k):

@@ -117,3 +117,24 @@ def test_fp8_full_c5_shard_properties(gpu):
     masked = full.clone()
     masked.scatter_(1, i, float("-inf"))
     assert bool((masked.max(dim=1).values <= s[:, -1]).all())
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_index_save_load_roundtrip(gpu, tmp_path, dtype):
+    """On-disk corpus shard + doc-id map: the reloaded index holds the same bytes
+    and returns the same top-k bits."""
+    from irc_amd import retrieval
+
+    torch.manual_seed(3)
+    d = torch.nn.functional.normalize(torch.randn(5000, 256)).to(gpu)
+    q = torch.nn.functional.normalize(torch.randn(20, 256)).to(gpu)
+    idx = retrieval.ShardedDenseIndex(d, doc_offset=11, dtype=dtype)
+    ids = [f"page_{i}" for i in range(5011)]
+    idx.save(str(tmp_path), rank=0, doc_ids=ids)
+    back, doc_dict = retrieval.ShardedDenseIndex.load(str(tmp_path), 0, gpu)
+    assert back.dtype == dtype and back.doc_offset == 11
+    assert torch.equal(back.docs.view(torch.uint8), idx.docs.view(torch.uint8))
+    s0, i0 = idx.search(q, 50)
+    s1, i1 = back.search(q, 50)
+    assert torch.equal(s0, s1) and torch.equal(i0, i1)
+    assert doc_dict[1] == ids and doc_dict[0]["page_7"] == 7
