@@ -320,6 +320,26 @@ int irc_topk_f64(const double* dense, int64_t n_cols, const int32_t* cand,
                  const int64_t* cand_off, int64_t Q, int64_t k, double* out_score,
                  int64_t* out_idx, int32_t* out_n, irc_stream_t stream);
 
+/* ---- ProtoNCE / HProtoNCE ----------------------------
+ * NCELoss._compute_proto_loss (src/contrastor/contrastive_loss.py:95-135):
+ * logits [B][C] (C >= B prototypes, row i's positive is column i), column
+ * temperatures temp [C]; row_loss[i] = CE(logits[i] / temp, i) (optional) and
+ * dlogits = gscale * (softmax - onehot) / temp (optional; gscale a device
+ * scalar or NULL = 1). */
+int irc_proto_ce(const float* logits, const float* temp, int64_t B, int64_t C, float* row_loss,
+                 float* dlogits, const float* gscale, irc_stream_t stream);
+/* run_kmeans (src/contrastor/utils.py:50-110; faiss Clustering in the reference):
+ * idx[r] = argmax_j S[r][j] + bias[j] (lowest j on ties), val[r] the maximum --
+ * nearest centroid with S = x . c^T and bias = -|c|^2 / 2. */
+int irc_argmax_bias(const float* S, const float* bias, int64_t rows, int64_t k, int64_t* idx,
+                    float* val, irc_stream_t stream);
+/* sums[assign[r]] += x[r], counts[assign[r]] += 1 (fp32 atomics) */
+int irc_centroid_accumulate(const float* x, const int64_t* assign, int64_t n, int64_t D,
+                            float* sums, float* counts, irc_stream_t stream);
+/* centroids = sums / counts where counts > 0 (else unchanged); bias = -|c|^2 / 2 */
+int irc_centroid_finalize(const float* sums, const float* counts, int64_t k, int64_t D,
+                          float* centroids, float* bias, irc_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

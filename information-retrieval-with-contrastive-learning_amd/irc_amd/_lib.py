@@ -39,6 +39,10 @@ SIGNATURES = {
     "irc_csr_union_emit": (I32, [P, I64, I64, P, P, P, P]),
     "irc_csr_spmv_f64": (I32, [P, P, P, I64, P, P, P, I64, P, P]),
     "irc_topk_f64": (I32, [P, I64, P, P, I64, I64, P, P, P, P]),
+    "irc_proto_ce": (I32, [P, P, I64, I64, P, P, P, P]),
+    "irc_argmax_bias": (I32, [P, P, I64, I64, P, P, P]),
+    "irc_centroid_accumulate": (I32, [P, P, I64, I64, P, P, P]),
+    "irc_centroid_finalize": (I32, [P, P, I64, I64, P, P, P]),
     "irc_gemm": (I32, [I32, I32, I32, I32, I32, I64, I64, I64, F32, P, I64, I64, P, I64, I64,
                        P, I64, P, I64, I64, P, I64, I64, I32, I64, P, I64, P]),
     "irc_gemm_workspace": (I64, [I32, I32, I32, I64, I64, I64, I64]),

@@ -3,13 +3,15 @@
 ``NCELoss._compute_info_loss`` keeps the reference semantics exactly (in-batch
 NT-Xent over [q; k] with the diagonal removed, optional MoCo queue logits reused
 for the k-rows, CE(sum)/2; contrastive_loss.py:56-93) and runs on the irc HIP
-kernels (irc_amd/nce.py).  ``_compute_proto_loss`` (ProtoNCE/HProtoNCE) is the
-"next" row of SURVEY.md 8f and is not part of this build yet.
+kernels (irc_amd/nce.py).  ``_compute_proto_loss`` (ProtoNCE/HProtoNCE,
+contrastive_loss.py:95-135) runs on irc_amd.cluster.proto_loss (same negative
+prototype draw, exact-fp32 logits, prototype CE kernel).
 """
 import random
 
 import torch
 
+from irc_amd.cluster import proto_loss
 from irc_amd.nce import info_nce
 
 random.seed(1126)  # module-level seed, as in the reference (contrastive_loss.py:4)
@@ -27,9 +29,7 @@ class NCELoss(torch.nn.Module):
         return info_nce(q, k, queue, self.T)
 
     def _compute_proto_loss(self, q, cluster_result, index):
-        raise NotImplementedError(
-            "ProtoNCE/HProtoNCE prototype loss is not built yet (SURVEY.md 8f row 3); "
-            "use --loss InfoNCE")
+        return proto_loss(q, cluster_result, index, self.num_cluster, self.num_neg_proto)
 
     def forward(self, q, k, queue, cluster_result=None, index=None):
         loss = self._compute_info_loss(q, k, queue)

@@ -19,6 +19,7 @@ import torch
 from tqdm import tqdm
 
 from src.dataset import get_dataloader
+from src.contrastor.utils import run_hierarchical_clustering, run_kmeans
 from src.model import build_model, get_optimizer, load_model, save_model
 
 OOM_MARKERS = ("CUDA out of memory", "HIP out of memory", "out of memory")
@@ -121,9 +122,22 @@ def train(args):
     model.train()
 
     train_loader = get_dataloader(args, train=True)
-    if args.loss in ["ProtoNCE", "HProtoNCE"]:
-        raise NotImplementedError("ProtoNCE/HProtoNCE: next row (SURVEY.md 8f); use InfoNCE")
+    feat_loader = None
+    if args.loss in ["ProtoNCE", "HProtoNCE"]:  # train.py:62-64
+        feat_loader = get_dataloader(args, train=False)
     cluster_result = None
+
+    def _maybe_recluster(cluster_result):
+        """train.py:96-122: at the start of an accumulation, from cluster_start_steps
+        on, every cluster.update_steps optimizer steps."""
+        if feat_loader is None or st.batch_size != 0:
+            return cluster_result
+        cfg = args.config["loss"][args.loss]
+        if st.step_sum >= cfg["cluster_start_steps"] and \
+                st.step_sum % cfg["cluster"]["update_steps"] == 0:
+            fn = run_kmeans if args.loss == "ProtoNCE" else run_hierarchical_clustering
+            return fn(cfg, feat_loader, model, args.device)
+        return cluster_result
 
     args.logdir = f"{args.logdir}/{args.loss}_{args.model}"
     if os.path.isdir(args.logdir):
@@ -155,6 +169,7 @@ def train(args):
         while nxt is not None:
             batch, nxt = nxt, next(it, None)
             try:
+                cluster_result = _maybe_recluster(cluster_result)
                 indexes, anchor_sample, positive_sample = batch
                 if prefetch:
                     cur_idx, handle = pending
