@@ -1,0 +1,55 @@
+"""End-to-end drop-in run: the package's main.py / src.train.train loop on a tiny
+synthetic docs_sentence.pkl (C1-shaped: 2-layer BERT H=128, 2-layer BiLSTM head),
+for InfoNCE and for ProtoNCE with re-clustering -- exercises the dataset,
+tokenizer, frozen-BERT prefetch pipeline, clustering, loss, optimizer and the
+checkpoint writer together (the numbers themselves are pinned elsewhere)."""
+import os
+import pickle
+
+import pytest
+import yaml
+
+from conftest import PKG
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_inputs(tmp_path, loss):
+    import random
+
+    rnd = random.Random(0)
+    docs = [[" ".join(f"w{rnd.randrange(900)}" for _ in range(rnd.randrange(4, 12)))
+             for _ in range(rnd.randrange(3, 7))] for _ in range(200)]
+    data = tmp_path / "docs_sentence.pkl"
+    with open(data, "wb") as f:
+        pickle.dump(docs, f)
+    with open(os.path.join(PKG, "config.yaml")) as f:
+        cfg = yaml.safe_load(f)
+    cfg["dataset"]["docs_sentence"] = str(data)
+    cfg["bert"] = {"name": "tiny", "vocab": None, "seed": 0, "precision": "bf16",
+                   "config": {"vocab_size": 1000, "hidden_size": 128, "num_hidden_layers": 2,
+                              "num_attention_heads": 2, "intermediate_size": 512,
+                              "max_position_embeddings": 64}}
+    cfg["model"]["LSTM"].update(num_layers=2, input_size=128, hidden_size=64, output_size=32)
+    cfg["train"].update(batch_size=16, acml_batch_size=32, total_steps=4, log_step=2, n_jobs=0)
+    cfg["eval"].update(batch_size=32, n_jobs=0)
+    for name in ("InfoNCE", "ProtoNCE"):
+        cfg["loss"][name].update(queue_size=64, queue_start_steps=2)
+    cfg["loss"]["ProtoNCE"].update(cluster_start_steps=1)
+    cfg["loss"]["ProtoNCE"]["cluster"].update(update_steps=2, num_cluster=[40, 48],
+                                              num_neg_proto=4, niter=3, nredo=1)
+    path = tmp_path / "config.yaml"
+    with open(path, "w") as f:
+        yaml.safe_dump(cfg, f)
+    return str(path)
+
+
+@pytest.mark.parametrize("loss", ["InfoNCE", "ProtoNCE"])
+def test_main_train_end_to_end(gpu, tmp_path, loss):
+    import main as entry
+
+    cfg = _write_inputs(tmp_path, loss)
+    entry.main(["--config", cfg, "--loss", loss, "--gpu", "0", "--logdir",
+                str(tmp_path / "log"), "--ckptdir", str(tmp_path / "ckpt")])
+    ckpts = sorted(os.listdir(tmp_path / "ckpt"))
+    assert ckpts == [f"uniform_{loss}_LSTM_2.pth", f"uniform_{loss}_LSTM_4.pth"], ckpts
