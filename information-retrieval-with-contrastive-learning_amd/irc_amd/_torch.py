@@ -34,9 +34,27 @@ _side: dict = {}
 HIGH_PRIORITY_TAGS: tuple = ()
 
 
+_serial = [0]
+
+
+class serial_streams:
+    """Context: side_stream() hands out the current stream, so every launch runs
+    in issue order with nothing beside it (kernel-efficiency measurements)."""
+
+    def __enter__(self):
+        _serial[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _serial[0] -= 1
+        return False
+
+
 def side_stream(device: torch.device, tag: str = "side") -> torch.cuda.Stream:
     """A persistent secondary HIP stream per (device, tag) for overlapping
     independent launches (e.g. the key encoder, weight-gradient GEMMs)."""
+    if _serial[0]:
+        return torch.cuda.current_stream(device)
     key = (torch.device(device).index, tag)
     s = _side.get(key)
     if s is None:
