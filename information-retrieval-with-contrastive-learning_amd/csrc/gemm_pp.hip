@@ -59,13 +59,13 @@ __device__ uint64_t pp_stamps[16];
 #endif
 
 constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
-// K-outer half-tile image: 16 blocks of 4 k-rows, each block = [16 column chunks]
-// [4 k-rows][16 B] (1 KB) + a 64-B pad (BPITCH).  One DMA wave-instruction fills
-// one block from 4 whole 256-B k-rows of global memory; a fragment's transpose
-// reads sit at base + immediate offsets (+128 B per 16 columns, +BPITCH per 4
-// k-rows), and the two 16-lane groups of a 32-lane half (k-rows 8 apart = 2
-// blocks apart) land on disjoint bank halves thanks to the pad.  K-major images
-// are 128 rows x 128 B.
+// K-outer half-tile image: 16 blocks of 4 k-rows, each block = [4 k-rows][16
+// column-chunk slots][16 B] (1 KB) + a 64-B pad (BPITCH); slot c of k-row a holds
+// chunk c ^ 2a.  One DMA wave-instruction fills one block from 4 whole 256-B
+// k-rows of global memory, 16 consecutive lanes per k-row (coalesced); a 16-lane
+// group's transposed reads (4 k-rows x 2 chunks) cover one aligned 128-B window,
+// and the two groups of a 32-lane half (k-rows 8 apart = 2 blocks apart) land on
+// disjoint bank halves thanks to the pad.  K-major images are 128 rows x 128 B.
 constexpr int BPITCH = 1024 + 64;
 // half-tile slot bytes of a K-major / K-outer operand; one K-tile = A0 A1 B0 B1
 constexpr int slot_bytes(bool kmajor) { return kmajor ? 16384 : 16 * BPITCH; }
@@ -123,10 +123,15 @@ __device__ __forceinline__ void stage_half(const unsigned short* __restrict__ X,
       gr = gr < nrows ? gr : nrows - 1;
       glds16(X + (int64_t)gr * ld + k0 + c * 8, img + (i * 4 + wq) * 1024);
     } else {
-      const int blk = i * 4 + wq;  // 4 k-rows; lane -> (chunk lane >> 2, k-row lane & 3)
-      int gc = r0 + (lane >> 2) * 8;
+      // 4 k-rows per block; lane -> (k-row a = lane >> 4, LDS slot lane & 15), and
+      // the slot holds column chunk (slot ^ 2a): 16 consecutive lanes read one
+      // k-row's 256 contiguous bytes (coalesced), and the transposed reads of the
+      // 4 k-rows (256 B apart) land on distinct banks.
+      const int blk = i * 4 + wq;
+      const int a = lane >> 4;
+      int gc = r0 + ((lane & 15) ^ (2 * a)) * 8;
       gc = gc + 8 <= nrows ? gc : nrows - 8;
-      glds16(X + (int64_t)(k0 + 4 * blk + (lane & 3)) * ld + gc, img + blk * BPITCH);
+      glds16(X + (int64_t)(k0 + 4 * blk + a) * ld + gc, img + blk * BPITCH);
     }
   }
 }
@@ -145,10 +150,12 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int row0, int s, int lan
     return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * (c ^ (row & 7)));
   } else {
     // 16-lane group q reads k-rows 32s+8q+{0..3} then +{4..7}; lane 4a+b of the
-    // group addresses row a, columns row0 + 4b .. +3
+    // group addresses row a, columns row0 + 4b .. +3 (chunk col >> 3 sits in slot
+    // (col >> 3) ^ 2a of the block's k-row a, see stage_half)
     const int q = lane >> 4, a = (lane >> 2) & 3, b = lane & 3;
     const int col = row0 + 4 * b;
-    const char* p = img + (8 * s + 2 * q) * BPITCH + (col >> 3) * 64 + a * 16 + (col & 7) * 2;
+    const char* p =
+        img + (8 * s + 2 * q) * BPITCH + a * 256 + (((col >> 3) ^ (2 * a)) * 16) + (col & 7) * 2;
     const v4s lo = ds_tr16(p);            // k-rows 32s + 8q + a
     const v4s hi = ds_tr16(p + BPITCH);   // k-rows 32s + 8q + 4 + a
     const v4s both[2] = {lo, hi};
