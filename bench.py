@@ -86,6 +86,14 @@ def _pmc_traffic(tag: str):
         return None
 
 
+def _pmc_source(tag: str):
+    p = os.path.join("profiles", f"pmc_{tag}.json")
+    if not os.path.exists(os.path.join(ROOT, p)):
+        return None
+    return (f"{p}: HBM bytes per launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 from separate "
+            "rocprofv3 --pmc passes of the same bench part (tools/pmc_traffic.sh)")
+
+
 def _prof(lib, name):
     tot, cnt, work = ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_double(0)
     lib.irc_prof_query(name.encode(), ctypes.byref(tot), ctypes.byref(cnt), ctypes.byref(work))
@@ -201,6 +209,7 @@ def run_train(args, rank, world, dev):
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS,
                      "unit": "TFLOP/s", "frac": achieved / BF16_PEAK_TFS if achieved else None,
                      "traffic": _pmc_traffic("gemm_bf16"),
+                     "traffic_source": _pmc_source("gemm_bf16"),
                      "kernel": "bf16 GEMM kernels (gemm_big_kernel / gemm_pp_kernel / "
                                "gemm_kernel; all GEMM launches of a single-stream pass of "
                                "the same steps)",
@@ -288,6 +297,7 @@ def run_train_bert(args, rank, world, dev):
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS,
                      "unit": "TFLOP/s", "frac": achieved / BF16_PEAK_TFS if achieved else None,
                      "traffic": _pmc_traffic("gemm_bf16_bert"),
+                     "traffic_source": _pmc_source("gemm_bf16_bert"),
                      "kernel": "gemm kernels, bf16 operands (all GEMM launches of a "
                                "single-stream pass of the same steps: fwd, dX, dW)",
                      "launches_per_step": g_n / args.steps,
@@ -385,6 +395,7 @@ def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16", nq=
         roof = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS if gbs else None,
                 "traffic": _pmc_traffic("scan_filter") if dtype == "bf16" else None,
+                "traffic_source": _pmc_source("scan_filter") if dtype == "bf16" else None,
                 "mfma_tflops": tfs}
     roof.update({"kernel": _filter_kernel_name(nq, dim, dtype), "kernel_avg_us": kavg * 1e6,
                  "alg_bytes_per_launch": k_bytes / max(k_n, 1)})
@@ -502,7 +513,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--part", default="all", choices=["all", "train", "scan", "bert"])
+    ap.add_argument("--part", default="all", choices=["all", "train", "scan", "scan_c2", "bert"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     args = ap.parse_args()
@@ -524,6 +535,8 @@ def main():
     if args.part in ("all", "bert"):
         bert = run_train_bert(args, rank, world, dev)
     scan_fp8 = scan_c4 = None
+    if args.part == "scan_c2":  # the C2 leg alone (PMC passes: tools/pmc_traffic.sh)
+        scan = run_scan(args, rank, world, dev, sweep=False)
     if args.part in ("all", "scan"):
         scan = run_scan(args, rank, world, dev)
         torch.cuda.empty_cache()
