@@ -85,6 +85,42 @@ __device__ __forceinline__ float gelu_f(float x) {
   const float e = 1.0f - p * t * __expf(-az * az);
   return 0.5f * x * (1.0f + copysignf(e, z));
 }
+// Two lanes' worth of gelu_f / gelu_grad_f on <2 x float>: the polynomial, scale and
+// blend steps issue as v_pk_fma_f32 / v_pk_mul_f32 (2 results per lane per op), only
+// rcp / exp / copysign stay scalar. Same operations in the same order as the scalar
+// forms, so the results are the same bits. The epilogue of the 256x256 tile is
+// VALU-bound (one workgroup per CU, nothing to overlap it with), so this is the
+// FFN1 + GELU launch's tail.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void erf_as_parts(f32x2 x, f32x2& z, f32x2& t, f32x2& ez) {
+  z = x * 0.70710678118654752f;
+  f32x2 az = {fabsf(z.x), fabsf(z.y)};
+  const f32x2 d = 1.0f + 0.3275911f * az;
+  t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  const f32x2 n = -az * az;
+  ez = f32x2{__expf(n.x), __expf(n.y)};
+}
+__device__ __forceinline__ f32x2 erf_as_poly(f32x2 t) {
+  f32x2 p = 1.061405429f * t - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  return p;
+}
+__device__ __forceinline__ f32x2 gelu_f2(f32x2 x) {
+  f32x2 z, t, ez;
+  erf_as_parts(x, z, t, ez);
+  const f32x2 e = 1.0f - erf_as_poly(t) * t * ez;
+  const f32x2 s = {copysignf(e.x, z.x), copysignf(e.y, z.y)};
+  return 0.5f * x * (1.0f + s);
+}
+__device__ __forceinline__ f32x2 gelu_grad_f2(f32x2 x) {
+  f32x2 z, t, ez;
+  erf_as_parts(x, z, t, ez);
+  const f32x2 e = 1.0f - erf_as_poly(t) * t * ez;
+  const f32x2 s = {copysignf(e.x, z.x), copysignf(e.y, z.y)};
+  return 0.5f * (1.0f + s) + x * 0.3989422804014327f * ez;
+}
 __device__ __forceinline__ float gelu_grad_f(float x) {
   const float z = x * 0.70710678118654752f;
   const float az = fabsf(z);
@@ -384,14 +420,20 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
+          f32x2 v[2];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * alpha + bv[j];
+          if (!slab && EPI == EPI_BIAS_GELU) {
+            v[0] = gelu_f2(v[0]);
+            v[1] = gelu_f2(v[1]);
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int rl = 16 * ii + 4 * (lane >> 4) + e;
-            float v = acc[2 * p + ii][j][e] * alpha + bv[j];
-            if (!slab && EPI == EPI_BIAS_GELU) v = gelu_f(v);
-            st[rl * EP_PITCH + 16 * j + (lane & 15)] = v;
+            st[rl * EP_PITCH + 16 * j + (lane & 15)] = v[e >> 1][e & 1];
           }
+        }
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const int rbase = rbase0 + 32 * p;
@@ -424,17 +466,27 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
           float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
           if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
             const u16x8 rr = *reinterpret_cast<const u16x8*>(R + (int64_t)row * g.ldr + col);
+            if constexpr (EPI == EPI_DGELU) {
 #pragma unroll
-            for (int t = 0; t < 8; ++t)
-              v[t] = EPI == EPI_DGELU ? v[t] * gelu_grad_f(bf16_to_f32(rr[t]))
-                                      : v[t] + bf16_to_f32(rr[t]);
+              for (int t = 0; t < 8; t += 2) {
+                const f32x2 g2 = gelu_grad_f2(f32x2{bf16_to_f32(rr[t]), bf16_to_f32(rr[t + 1])});
+                v[t] *= g2.x;
+                v[t + 1] *= g2.y;
+              }
+            } else {
+#pragma unroll
+              for (int t = 0; t < 8; ++t) v[t] += bf16_to_f32(rr[t]);
+            }
           }
           if (EPI == EPI_BIAS_GELU_SAVE) {
             u16x8 pre;
 #pragma unroll
-            for (int t = 0; t < 8; ++t) {
+            for (int t = 0; t < 8; t += 2) {
               pre[t] = f32_to_bf16(v[t]);
-              v[t] = gelu_f(v[t]);
+              pre[t + 1] = f32_to_bf16(v[t + 1]);
+              const f32x2 g2 = gelu_f2(f32x2{v[t], v[t + 1]});
+              v[t] = g2.x;
+              v[t + 1] = g2.y;
             }
             *reinterpret_cast<u16x8*>(const_cast<unsigned short*>(R) + (int64_t)row * g.ldr + col) =
                 pre;
