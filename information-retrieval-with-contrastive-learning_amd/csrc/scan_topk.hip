@@ -1124,6 +1124,20 @@ static void plan_workers(int64_t ntiles, int gy, int64_t D, int eb, int nw, int*
   *g = (int)gg;
 }
 
+// Threshold sample = N / sample_div() docs (IRC_SCAN_SAMPLE_DIV, read once; default 16:
+// C2 whole call at Q = 64 / 256 / 1024 75.3 / 98.0 / 258 us against 75.8 / 101.6 / 274 at 8,
+// and 98 / 115 / 296 at 32, tools/g4.sh).
+// Any value keeps the result exact (the threshold is the 2*KS-th group maximum of real
+// scores); it trades the sample pass against the filter's survivor count.
+static int64_t sample_div() {
+  static const int64_t v = [] {
+    const char* e = getenv("IRC_SCAN_SAMPLE_DIV");
+    const long x = e ? atol(e) : 16;
+    return (int64_t)(x >= 1 ? x : 16);
+  }();
+  return v;
+}
+
 static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   Plan p{};
   p.ks = pick_ks(D);
@@ -1133,12 +1147,13 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   p.gy = (int)((Q + qb - 1) / qb);
   if (p.gy < 1) p.gy = 1;
   p.qpad = p.gy * qb;
-  // Sample of N/8 docs (>= 32k; GMAX leaves 2*KS keys per 32-doc tile, so >= 2k
+  // Sample of N/16 docs (>= 32k; GMAX leaves 2*KS keys per 32-doc tile, so >= 2k
   // group maxima per query for the threshold select, capped at its LDS stage).
-  // The filter's survivors ~ k * N / S (~8k per query; at the cap, e.g. a 625k
+  // The filter's survivors ~ k * N / S (~1.6k per query at k = 100, N / S = 16; at the cap, e.g. a 625k
   // shard, ~k * N / 32768).
   int64_t s_target = 32 * k;
-  if (N / 8 > s_target) s_target = N / 8;
+  const int64_t sdiv = sample_div();
+  if (N / sdiv > s_target) s_target = N / sdiv;
   const int64_t s_cap = (int64_t)SEL_STAGE * TD / (2 * p.ks);
   if (s_target > s_cap) s_target = s_cap;
   p.stride = s_target > 0 ? N / s_target : 1;
