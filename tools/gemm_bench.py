@@ -18,6 +18,7 @@ SHAPES = [  # (name, M, N, K, epilogue)
     ("qkv", 32768, 2304, 768, 1),
     ("attn_out+res", 32768, 768, 768, 3),
     ("ffn1+gelu", 32768, 3072, 768, 2),
+    ("ffn1+bias", 32768, 3072, 768, 1),   # the GELU epilogue's cost = the difference
     ("ffn2+res", 32768, 768, 3072, 3),
     ("lstm_xp_l0", 16384, 2048, 768, 1),
     ("lstm_xp_l12", 16384, 2048, 512, 1),
