@@ -46,9 +46,25 @@ __global__ __launch_bounds__(NT) void union_mark_kernel(const int64_t* __restric
   uint32_t* bm = bitmaps + q * words;
   const int64_t b = indptr[r], len = indptr[r + 1] - b;
   const int64_t j0 = b + len * blockIdx.y / SEG, j1 = b + len * (blockIdx.y + 1) / SEG;
-  for (int64_t j = j0 + threadIdx.x; j < j1; j += NT) {
-    const uint32_t d = (uint32_t)indices[j];
-    atomicOr(&bm[d >> 5], 1u << (d & 31));
+  // A row's doc indices ascend, so a wave's 64 docs fall in a few bitmap words:
+  // OR the bits of each run of equal words across lanes (segmented suffix scan,
+  // run head = first lane of the run) and let only run heads issue the atomic.
+  // Any order stays correct: a lane only ever merges bits of its own word.
+  const int lane = threadIdx.x & 63;
+  for (int64_t base = j0; base < j1; base += NT) {  // uniform trip count
+    const int64_t j = base + threadIdx.x;
+    const bool valid = j < j1;
+    const uint32_t d = valid ? (uint32_t)indices[j] : 0u;
+    const uint32_t word = valid ? d >> 5 : 0xffffffffu;
+    uint32_t bits = valid ? 1u << (d & 31) : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t w2 = __shfl_down(word, o, 64);
+      const uint32_t b2 = __shfl_down(bits, o, 64);
+      if (lane + o < 64 && w2 == word) bits |= b2;
+    }
+    const uint32_t prev = __shfl_up(word, 1, 64);
+    if (valid && (lane == 0 || prev != word)) atomicOr(&bm[word], bits);
   }
 }
 
@@ -163,12 +179,16 @@ __device__ __forceinline__ uint64_t orderable_f64(double x) {
 }
 
 constexpr int TK_MAX = 1024;
+// 1024 threads per query: the candidate passes are dependent gathers
+// (row[cand[i]]), latency-bound, and only Q workgroups exist -- 16 waves per
+// query keep 4x the loads in flight of a 256-thread block.
+constexpr int TNT = 1024;
 
 // One workgroup per query over its candidate docs (ascending indices) with
 // nonzero scores: exact k-th largest score, boundary ties to the lower index,
 // then a (score desc, index asc) bitonic sort in LDS.  Writes out_n[q] valid
 // entries (fewer than k when fewer docs scored), the rest (0, -1).
-__global__ __launch_bounds__(NT) void topk_f64_kernel(const double* __restrict__ dense,
+__global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict__ dense,
                                                       int64_t n_cols,
                                                       const int32_t* __restrict__ cand,
                                                       const int64_t* __restrict__ cand_off,
@@ -179,7 +199,7 @@ __global__ __launch_bounds__(NT) void topk_f64_kernel(const double* __restrict__
   __shared__ uint64_t s_key[TK_MAX];
   __shared__ int32_t s_idx[TK_MAX];
   __shared__ uint32_t s_misc[4];  // 0: nonzero count, 1: kr, 2: digit, 3: collect ctr
-  __shared__ int64_t s_wsum[NT / 64];
+  __shared__ int64_t s_wsum[TNT / 64];
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double* row = dense + q * n_cols;
@@ -190,7 +210,7 @@ __global__ __launch_bounds__(NT) void topk_f64_kernel(const double* __restrict__
   }
   __syncthreads();
   uint32_t nz = 0;
-  for (int64_t i = c0 + tid; i < c1; i += NT) nz += row[cand[i]] != 0.0;
+  for (int64_t i = c0 + tid; i < c1; i += TNT) nz += row[cand[i]] != 0.0;
   atomicAdd(&s_misc[0], nz);
   __syncthreads();
   const uint32_t M = s_misc[0];
@@ -200,9 +220,9 @@ __global__ __launch_bounds__(NT) void topk_f64_kernel(const double* __restrict__
   if (M > (uint32_t)k) {
     uint32_t kr = (uint32_t)k;
     for (int shift = 56; shift >= 0; shift -= 8) {
-      hist[tid] = 0;
+      if (tid < 256) hist[tid] = 0;
       __syncthreads();
-      for (int64_t i = c0 + tid; i < c1; i += NT) {
+      for (int64_t i = c0 + tid; i < c1; i += TNT) {
         const double s = row[cand[i]];
         if (s == 0.0) continue;
         const uint64_t key = orderable_f64(s);
@@ -245,7 +265,7 @@ __global__ __launch_bounds__(NT) void topk_f64_kernel(const double* __restrict__
     // keys > kth: all taken; keys == kth: the lowest `need` indices (ordered scan)
     const uint32_t need = kr;
     int64_t taken_eq_before = 0;
-    for (int64_t b0 = c0; b0 < c1; b0 += NT) {
+    for (int64_t b0 = c0; b0 < c1; b0 += TNT) {
       const int64_t i = b0 + tid;
       uint64_t key = 0;
       bool gt = false, eq = false;
@@ -264,7 +284,7 @@ __global__ __launch_bounds__(NT) void topk_f64_kernel(const double* __restrict__
       __syncthreads();
       int64_t r_eq = taken_eq_before + r_in_wave;
       int64_t blk_eq = 0;
-      for (int w = 0; w < NT / 64; ++w) {
+      for (int w = 0; w < TNT / 64; ++w) {
         if (w < wave) r_eq += s_wsum[w];
         blk_eq += s_wsum[w];
       }
@@ -277,7 +297,7 @@ __global__ __launch_bounds__(NT) void topk_f64_kernel(const double* __restrict__
       __syncthreads();
     }
   } else {
-    for (int64_t i = c0 + tid; i < c1; i += NT) {
+    for (int64_t i = c0 + tid; i < c1; i += TNT) {
       const double s = row[cand[i]];
       if (s == 0.0) continue;
       const uint32_t slot = atomicAdd(&s_misc[3], 1u);
@@ -289,14 +309,14 @@ __global__ __launch_bounds__(NT) void topk_f64_kernel(const double* __restrict__
   // bitonic sort of cnt entries by (key desc, idx asc)
   int npow = 1;
   while (npow < cnt) npow <<= 1;
-  for (int i = cnt + tid; i < npow; i += NT) {
+  for (int i = cnt + tid; i < npow; i += TNT) {
     s_key[i] = 0;
     s_idx[i] = 0x7fffffff;
   }
   __syncthreads();
   for (int size = 2; size <= npow; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < npow; i += NT) {
+      for (int i = tid; i < npow; i += TNT) {
         const int j = i ^ stride;
         if (j > i) {
           const bool desc = (i & size) == 0;
@@ -315,7 +335,7 @@ __global__ __launch_bounds__(NT) void topk_f64_kernel(const double* __restrict__
       __syncthreads();
     }
   }
-  for (int i = tid; i < k; i += NT) {
+  for (int i = tid; i < k; i += TNT) {
     double sc = 0.0;
     int64_t id = -1;
     if (i < cnt) {
@@ -392,7 +412,7 @@ extern "C" int irc_topk_f64(const double* dense, int64_t n_cols, const int32_t* 
   IRC_REQUIRE(k >= 1 && k <= TK_MAX, "topk_f64: k=%lld outside [1, %d]", (long long)k, TK_MAX);
   IRC_REQUIRE(Q >= 0, "topk_f64: negative Q");
   if (Q == 0) return IRC_OK;
-  hipLaunchKernelGGL(topk_f64_kernel, dim3((unsigned)Q), dim3(NT), 0, as_stream(stream), dense,
+  hipLaunchKernelGGL(topk_f64_kernel, dim3((unsigned)Q), dim3(TNT), 0, as_stream(stream), dense,
                      n_cols, cand, cand_off, (int)k, out_score, out_idx, out_n);
   return check_launch("topk_f64_kernel");
 }

@@ -114,3 +114,41 @@ def test_reference_api_dropins(gpu, corpus, tmp_path):
     ids, scores = ranker.closest_docs(claim, 10)
     np.testing.assert_array_equal(scores, g["top_score_0"])
     assert ids[0] == doc_ids[int(g["top_idx_0"][0])]
+
+
+def test_dense_rows_union_and_topk_ties(gpu):
+    """Zipf-head-like rows covering most docs (runs of equal bitmap words within a
+    wave, merged before the atomic) and small-integer data (many exact score ties
+    at the k-th boundary, candidate counts far above one workgroup's threads)."""
+    import scipy.sparse as sp
+
+    from irc_amd import sparse
+
+    rng = np.random.default_rng(11)
+    n_docs, hash_size = 70_001, 64
+    dens = [0.9, 0.6, 0.3, 0.05, 0.002] + [0.01] * (hash_size - 5)
+    rr, cc = [], []
+    for r, p in enumerate(dens):
+        docs = np.nonzero(rng.random(n_docs) < p)[0]
+        rr.append(np.full(len(docs), r))
+        cc.append(docs)
+    rr, cc = np.concatenate(rr), np.concatenate(cc)
+    m = sp.csr_matrix((rng.integers(1, 4, len(rr)).astype(np.float64), (rr, cc)),
+                      shape=(hash_size, n_docs))
+    m.sort_indices()
+    index = sparse.SparseIndex(m, device=gpu)
+    rows = [np.array([0]), np.array([1, 2]), np.array([0, 3, 4, 9]), np.array([4]),
+            np.array([2, 5, 6, 7, 8])]
+    idx, off = index.union(rows)
+    idx, off = idx.cpu().numpy(), off.cpu().numpy()
+    for q, r in enumerate(rows):
+        np.testing.assert_array_equal(idx[off[q]:off[q + 1]], np.unique(m[r].nonzero()[1]))
+    weights = [np.ones(len(r)) * (1.0 + 0.5 * q) for q, r in enumerate(rows)]
+    for k in (1, 100, 1024):
+        got = index.topk_rows(rows, weights, k)
+        for q, (r, w) in enumerate(zip(rows, weights)):
+            row = np.asarray(m[r].T @ w).ravel()
+            nz = np.nonzero(row)[0]
+            order = nz[np.lexsort((nz, -row[nz]))][:k]
+            np.testing.assert_array_equal(got[q][0], order, err_msg=f"q={q} k={k}")
+            np.testing.assert_array_equal(got[q][1], row[order])
