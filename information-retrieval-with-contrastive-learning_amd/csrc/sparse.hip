@@ -183,6 +183,7 @@ constexpr int TK_MAX = 1024;
 // (row[cand[i]]), latency-bound, and only Q workgroups exist -- 16 waves per
 // query keep 4x the loads in flight of a 256-thread block.
 constexpr int TNT = 1024;
+constexpr int TK_STAGE = 8192;  // 64 KB of LDS keys
 
 // One workgroup per query over its candidate docs (ascending indices) with
 // nonzero scores: exact k-th largest score, boundary ties to the lower index,
@@ -198,7 +199,10 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
   __shared__ uint32_t hist[256];
   __shared__ uint64_t s_key[TK_MAX];
   __shared__ int32_t s_idx[TK_MAX];
-  __shared__ uint32_t s_misc[4];  // 0: nonzero count, 1: kr, 2: digit, 3: collect ctr
+  __shared__ uint64_t c_key[TK_STAGE];  // keys of the selected bucket, once they fit
+  // 0: nonzero count, 1: kr, 2: digit, 3: collect ctr, 4: selected bucket size,
+  // 5: staged count
+  __shared__ uint32_t s_misc[6];
   __shared__ int64_t s_wsum[TNT / 64];
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -207,28 +211,59 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
   if (tid == 0) {
     s_misc[0] = 0;
     s_misc[3] = 0;
+    s_misc[5] = 0;
   }
+  if (tid < 256) hist[tid] = 0;
   __syncthreads();
+  // first pass: nonzero count and the top digit's histogram together
   uint32_t nz = 0;
-  for (int64_t i = c0 + tid; i < c1; i += TNT) nz += row[cand[i]] != 0.0;
+  for (int64_t i = c0 + tid; i < c1; i += TNT) {
+    const double s = row[cand[i]];
+    if (s == 0.0) continue;
+    ++nz;
+    atomicAdd(&hist[orderable_f64(s) >> 56], 1u);
+  }
   atomicAdd(&s_misc[0], nz);
   __syncthreads();
   const uint32_t M = s_misc[0];
   const int cnt = (int)(M < (uint32_t)k ? M : (uint32_t)k);
-  // k-th largest orderable key among nonzero scores (exact, 8 x 8-bit digits)
+  // k-th largest orderable key among nonzero scores (exact, 8 x 8-bit digits).
+  // Once the selected bucket (the keys matching the prefix so far) fits
+  // TK_STAGE, one more gather stages it in LDS and the later digits read LDS.
   uint64_t kth = 0, pmask = 0, prefix = 0;
   if (M > (uint32_t)k) {
     uint32_t kr = (uint32_t)k;
+    uint32_t nsel = M;
+    bool staged = false;
     for (int shift = 56; shift >= 0; shift -= 8) {
-      if (tid < 256) hist[tid] = 0;
-      __syncthreads();
-      for (int64_t i = c0 + tid; i < c1; i += TNT) {
-        const double s = row[cand[i]];
-        if (s == 0.0) continue;
-        const uint64_t key = orderable_f64(s);
-        if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+      if (shift != 56) {
+        if (!staged && nsel <= (uint32_t)TK_STAGE) {
+          for (int64_t i = c0 + tid; i < c1; i += TNT) {
+            const double s = row[cand[i]];
+            if (s == 0.0) continue;
+            const uint64_t key = orderable_f64(s);
+            if ((key & pmask) == prefix) c_key[atomicAdd(&s_misc[5], 1u)] = key;
+          }
+          staged = true;
+        }
+        if (tid < 256) hist[tid] = 0;
+        __syncthreads();
+        if (staged) {
+          const int ns = (int)s_misc[5];
+          for (int i = tid; i < ns; i += TNT) {
+            const uint64_t key = c_key[i];
+            if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+          }
+        } else {
+          for (int64_t i = c0 + tid; i < c1; i += TNT) {
+            const double s = row[cand[i]];
+            if (s == 0.0) continue;
+            const uint64_t key = orderable_f64(s);
+            if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
+          }
+        }
+        __syncthreads();
       }
-      __syncthreads();
       if (wave == 0) {
         uint32_t bb[4];
 #pragma unroll
@@ -244,21 +279,25 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
         if (suf >= kr && above < kr) {
           uint32_t acc = above;
           int sel = 4 * lane;
+          uint32_t bsz = bb[0];
           for (int j = 3; j >= 0; --j) {
             if (acc + bb[j] >= kr) {
               sel = 4 * lane + j;
+              bsz = bb[j];
               break;
             }
             acc += bb[j];
           }
           s_misc[2] = (uint32_t)sel;
           s_misc[1] = kr - acc;
+          s_misc[4] = bsz;
         }
       }
       __syncthreads();
       prefix |= (uint64_t)s_misc[2] << shift;
       pmask |= (uint64_t)0xff << shift;
       kr = s_misc[1];
+      nsel = s_misc[4];
       __syncthreads();
     }
     kth = prefix;  // the exact k-th largest key; kr = how many of the ties to take
