@@ -23,7 +23,9 @@ namespace irc {
 namespace sparse {
 
 constexpr int NT = 256;
-constexpr int64_t CHUNK_WORDS = 8192;  // bitmap words per compaction chunk (256 K docs)
+constexpr int64_t CHUNK_WORDS = 1024;  // bitmap words per compaction chunk (32 K docs): a
+// dense union emits up to 32 docs per word serially, so chunks are kept small for
+// parallelism (7 workgroups per query at 200k docs instead of 1)
 
 // grid (pairs, SEG): block (pair, s) ORs the doc bits of segment s of the pair's
 // row -- long (Zipf-head) rows are spread over SEG workgroups.
@@ -102,7 +104,7 @@ __global__ __launch_bounds__(NT) void union_emit_kernel(const uint32_t* __restri
   const uint32_t* bm = bitmaps + q * words;
   int64_t base = out_off[q];
   for (int64_t i = 0; i < c; ++i) base += chunk_sums[q * nchunks + i];
-  constexpr int WPT = CHUNK_WORDS / NT;  // 32 consecutive words per thread
+  constexpr int WPT = CHUNK_WORDS / NT;  // 4 consecutive words per thread
   const int64_t w0 = c * CHUNK_WORDS + (int64_t)threadIdx.x * WPT;
   int64_t mine = 0;
   for (int i = 0; i < WPT; ++i)
