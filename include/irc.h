@@ -315,7 +315,9 @@ int irc_csr_spmv_f64(const int64_t* indptr, const int32_t* indices, const double
 /* Top-k of the nonzero dense[q][cand] over each query's candidate docs (cand,
  * ascending, offsets cand_off [Q+1]): (score desc, doc index asc), k <= 1024;
  * out_n[q] = number of valid entries, the rest (0, -1)
- * (tfidf_doc_ranker.py:67-73). */
+ * (tfidf_doc_ranker.py:67-73). cand == NULL (cand_off unused): every doc of the
+ * row is a candidate -- the same result over a dense buffer that is zero outside
+ * the union (what irc_csr_spmv_f64 leaves in a zeroed buffer), read contiguously. */
 int irc_topk_f64(const double* dense, int64_t n_cols, const int32_t* cand,
                  const int64_t* cand_off, int64_t Q, int64_t k, double* out_score,
                  int64_t* out_idx, int32_t* out_n, irc_stream_t stream);

@@ -209,7 +209,11 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double* row = dense + q * n_cols;
-  const int64_t c0 = cand_off[q], c1 = cand_off[q + 1];
+  // cand == nullptr: every doc of the row is a candidate (a dense union reads the
+  // row contiguously instead of gathering through the candidate list)
+  const bool all_docs = cand == nullptr;
+  const int64_t c0 = all_docs ? 0 : cand_off[q], c1 = all_docs ? n_cols : cand_off[q + 1];
+  auto doc = [&](int64_t i) -> int64_t { return all_docs ? i : (int64_t)cand[i]; };
   if (tid == 0) {
     s_misc[0] = 0;
     s_misc[3] = 0;
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
   // first pass: nonzero count and the top digit's histogram together
   uint32_t nz = 0;
   for (int64_t i = c0 + tid; i < c1; i += TNT) {
-    const double s = row[cand[i]];
+    const double s = row[doc(i)];
     if (s == 0.0) continue;
     ++nz;
     atomicAdd(&hist[orderable_f64(s) >> 56], 1u);
@@ -241,7 +245,7 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
       if (shift != 56) {
         if (!staged && nsel <= (uint32_t)TK_STAGE) {
           for (int64_t i = c0 + tid; i < c1; i += TNT) {
-            const double s = row[cand[i]];
+            const double s = row[doc(i)];
             if (s == 0.0) continue;
             const uint64_t key = orderable_f64(s);
             if ((key & pmask) == prefix) c_key[atomicAdd(&s_misc[5], 1u)] = key;
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
           }
         } else {
           for (int64_t i = c0 + tid; i < c1; i += TNT) {
-            const double s = row[cand[i]];
+            const double s = row[doc(i)];
             if (s == 0.0) continue;
             const uint64_t key = orderable_f64(s);
             if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
       uint64_t key = 0;
       bool gt = false, eq = false;
       if (i < c1) {
-        const double s = row[cand[i]];
+        const double s = row[doc(i)];
         if (s != 0.0) {
           key = orderable_f64(s);
           gt = key > kth;
@@ -332,18 +336,18 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
       if (gt || (eq && r_eq < (int64_t)need)) {
         const uint32_t slot = atomicAdd(&s_misc[3], 1u);
         s_key[slot] = key;
-        s_idx[slot] = cand[i];
+        s_idx[slot] = (int32_t)doc(i);
       }
       taken_eq_before += blk_eq;
       __syncthreads();
     }
   } else {
     for (int64_t i = c0 + tid; i < c1; i += TNT) {
-      const double s = row[cand[i]];
+      const double s = row[doc(i)];
       if (s == 0.0) continue;
       const uint32_t slot = atomicAdd(&s_misc[3], 1u);
       s_key[slot] = orderable_f64(s);
-      s_idx[slot] = cand[i];
+      s_idx[slot] = (int32_t)doc(i);
     }
   }
   __syncthreads();
@@ -452,6 +456,8 @@ extern "C" int irc_topk_f64(const double* dense, int64_t n_cols, const int32_t* 
                             int64_t* out_idx, int32_t* out_n, irc_stream_t stream) {
   IRC_REQUIRE(k >= 1 && k <= TK_MAX, "topk_f64: k=%lld outside [1, %d]", (long long)k, TK_MAX);
   IRC_REQUIRE(Q >= 0, "topk_f64: negative Q");
+  IRC_REQUIRE(cand != nullptr || n_cols < (1ll << 31), "topk_f64: n_cols must fit int32 doc ids");
+  IRC_REQUIRE(cand == nullptr || cand_off != nullptr, "topk_f64: cand without cand_off");
   if (Q == 0) return IRC_OK;
   hipLaunchKernelGGL(topk_f64_kernel, dim3((unsigned)Q), dim3(TNT), 0, as_stream(stream), dense,
                      n_cols, cand, cand_off, (int)k, out_score, out_idx, out_n);

@@ -130,6 +130,7 @@ class SparseIndex:
             m = m.sorted_indices()
         self.hash_size, self.n_docs = m.shape
         self.ngram = int(ngram)
+        self._row_len = np.diff(m.indptr).astype(np.int64)  # host: union-size bounds
         self.indptr = torch.from_numpy(m.indptr.astype(np.int64)).to(device)
         self.indices = torch.from_numpy(m.indices.astype(np.int32)).to(device)
         self.data = torch.from_numpy(m.data.astype(np.float64)).to(device)
@@ -207,20 +208,35 @@ class SparseIndex:
         vecs = [self.text2spvec(q) for q in queries]
         return self.topk_rows([v[0] for v in vecs], [v[1] for v in vecs], k)
 
-    def topk_rows(self, rows, weights, k: int):
+    def topk_rows(self, rows, weights, k: int, candidates: str = "auto"):
         """Top-k docs of sum_r w_r * A[r] per query (rows ascending, fp64 weights):
-        [(doc indices, fp64 scores)], (score desc, index asc), nonzero scores only."""
+        [(doc indices, fp64 scores)], (score desc, index asc), nonzero scores only.
+
+        candidates: "union" gathers each query's scores through its row union;
+        "all" scans the whole score row contiguously (same result: the buffer is
+        zero outside the union); "auto" takes "all" when the rows' total length,
+        an upper bound of the union, averages >= n_docs / 8 per query."""
         Q = len(rows)
         t_off, t_rows, t_w, _ = self._pack(rows, weights)
         dense = torch.zeros((Q, self.n_docs), dtype=torch.float64, device=self.device)
         st = stream_ptr(self.device)
         _lib.call("irc_csr_spmv_f64", ptr(self.indptr), ptr(self.indices), ptr(self.data),
                   self.n_docs, ptr(t_off), ptr(t_rows), ptr(t_w), Q, ptr(dense), st)
-        cand, cand_off = self.union(rows)
+        if candidates == "auto":
+            bound = sum(min(int(self._row_len[np.asarray(r, np.int64)].sum()), self.n_docs)
+                        for r in rows)
+            candidates = "all" if Q and bound * 8 >= Q * self.n_docs else "union"
+        if candidates == "all":
+            cand_p = cand_off_p = None
+        elif candidates == "union":
+            cand, cand_off = self.union(rows)
+            cand_p, cand_off_p = ptr(cand), ptr(cand_off)
+        else:
+            raise ValueError(f"candidates must be 'auto', 'union' or 'all', not {candidates!r}")
         out_s = torch.empty((Q, k), dtype=torch.float64, device=self.device)
         out_i = torch.empty((Q, k), dtype=torch.int64, device=self.device)
         out_n = torch.empty((Q,), dtype=torch.int32, device=self.device)
-        _lib.call("irc_topk_f64", ptr(dense), self.n_docs, ptr(cand), ptr(cand_off), Q, k,
+        _lib.call("irc_topk_f64", ptr(dense), self.n_docs, cand_p, cand_off_p, Q, k,
                   ptr(out_s), ptr(out_i), ptr(out_n), st)
         s, i, n = out_s.cpu().numpy(), out_i.cpu().numpy(), out_n.cpu().numpy()
         return [(i[r, :n[r]], s[r, :n[r]]) for r in range(Q)]

@@ -144,11 +144,12 @@ def test_dense_rows_union_and_topk_ties(gpu):
     for q, r in enumerate(rows):
         np.testing.assert_array_equal(idx[off[q]:off[q + 1]], np.unique(m[r].nonzero()[1]))
     weights = [np.ones(len(r)) * (1.0 + 0.5 * q) for q, r in enumerate(rows)]
-    for k in (1, 100, 1024):
-        got = index.topk_rows(rows, weights, k)
-        for q, (r, w) in enumerate(zip(rows, weights)):
-            row = np.asarray(m[r].T @ w).ravel()
-            nz = np.nonzero(row)[0]
-            order = nz[np.lexsort((nz, -row[nz]))][:k]
-            np.testing.assert_array_equal(got[q][0], order, err_msg=f"q={q} k={k}")
-            np.testing.assert_array_equal(got[q][1], row[order])
+    for mode in ("union", "all", "auto"):  # gathered through the union / whole row
+        for k in (1, 100, 1024):
+            got = index.topk_rows(rows, weights, k, candidates=mode)
+            for q, (r, w) in enumerate(zip(rows, weights)):
+                row = np.asarray(m[r].T @ w).ravel()
+                nz = np.nonzero(row)[0]
+                order = nz[np.lexsort((nz, -row[nz]))][:k]
+                np.testing.assert_array_equal(got[q][0], order, err_msg=f"{mode} q={q} k={k}")
+                np.testing.assert_array_equal(got[q][1], row[order])
