@@ -186,6 +186,7 @@ constexpr int TK_MAX = 1024;
 // query keep 4x the loads in flight of a 256-thread block.
 constexpr int TNT = 1024;
 constexpr int TK_STAGE = 8192;  // 64 KB of LDS keys
+constexpr int TK_U = 8;          // score loads in flight per thread
 
 // One workgroup per query over its candidate docs (ascending indices) with
 // nonzero scores: exact k-th largest score, boundary ties to the lower index,
@@ -214,6 +215,21 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
   const bool all_docs = cand == nullptr;
   const int64_t c0 = all_docs ? 0 : cand_off[q], c1 = all_docs ? n_cols : cand_off[q + 1];
   auto doc = [&](int64_t i) -> int64_t { return all_docs ? i : (int64_t)cand[i]; };
+  // Unordered pass over the candidates' scores, TK_U loads in flight per thread
+  // (one load per iteration left each thread waiting out a full memory latency).
+  auto each_score = [&](auto&& f) {
+    for (int64_t b = c0 + tid; b < c1; b += (int64_t)TNT * TK_U) {
+      double v[TK_U];
+#pragma unroll
+      for (int u = 0; u < TK_U; ++u) {
+        const int64_t i = b + (int64_t)u * TNT;
+        v[u] = i < c1 ? row[doc(i)] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < TK_U; ++u)
+        if (v[u] != 0.0) f(v[u], b + (int64_t)u * TNT);
+    }
+  };
   if (tid == 0) {
     s_misc[0] = 0;
     s_misc[3] = 0;
@@ -223,12 +239,10 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
   __syncthreads();
   // first pass: nonzero count and the top digit's histogram together
   uint32_t nz = 0;
-  for (int64_t i = c0 + tid; i < c1; i += TNT) {
-    const double s = row[doc(i)];
-    if (s == 0.0) continue;
+  each_score([&](double s, int64_t) {
     ++nz;
     atomicAdd(&hist[orderable_f64(s) >> 56], 1u);
-  }
+  });
   atomicAdd(&s_misc[0], nz);
   __syncthreads();
   const uint32_t M = s_misc[0];
@@ -244,12 +258,10 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
     for (int shift = 56; shift >= 0; shift -= 8) {
       if (shift != 56) {
         if (!staged && nsel <= (uint32_t)TK_STAGE) {
-          for (int64_t i = c0 + tid; i < c1; i += TNT) {
-            const double s = row[doc(i)];
-            if (s == 0.0) continue;
+          each_score([&](double s, int64_t) {
             const uint64_t key = orderable_f64(s);
             if ((key & pmask) == prefix) c_key[atomicAdd(&s_misc[5], 1u)] = key;
-          }
+          });
           staged = true;
         }
         if (tid < 256) hist[tid] = 0;
@@ -261,12 +273,10 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
             if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
           }
         } else {
-          for (int64_t i = c0 + tid; i < c1; i += TNT) {
-            const double s = row[doc(i)];
-            if (s == 0.0) continue;
+          each_score([&](double s, int64_t) {
             const uint64_t key = orderable_f64(s);
             if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
-          }
+          });
         }
         __syncthreads();
       }
@@ -309,8 +319,20 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
     kth = prefix;  // the exact k-th largest key; kr = how many of the ties to take
     // keys > kth: all taken; keys == kth: the lowest `need` indices (ordered scan)
     const uint32_t need = kr;
+    // nsel = the last digit's bucket = the keys equal to kth. When all of them
+    // are taken, nothing depends on the order: one unordered pass.
+    const bool all_eq = nsel == need;
+    if (all_eq)
+      each_score([&](double s, int64_t i) {
+        const uint64_t key = orderable_f64(s);
+        if (key >= kth) {
+          const uint32_t slot = atomicAdd(&s_misc[3], 1u);
+          s_key[slot] = key;
+          s_idx[slot] = (int32_t)doc(i);
+        }
+      });
     int64_t taken_eq_before = 0;
-    for (int64_t b0 = c0; b0 < c1; b0 += TNT) {
+    for (int64_t b0 = all_eq ? c1 : c0; b0 < c1; b0 += TNT) {
       const int64_t i = b0 + tid;
       uint64_t key = 0;
       bool gt = false, eq = false;
@@ -342,13 +364,11 @@ __global__ __launch_bounds__(TNT) void topk_f64_kernel(const double* __restrict_
       __syncthreads();
     }
   } else {
-    for (int64_t i = c0 + tid; i < c1; i += TNT) {
-      const double s = row[doc(i)];
-      if (s == 0.0) continue;
+    each_score([&](double s, int64_t i) {
       const uint32_t slot = atomicAdd(&s_misc[3], 1u);
       s_key[slot] = orderable_f64(s);
       s_idx[slot] = (int32_t)doc(i);
-    }
+    });
   }
   __syncthreads();
   // bitonic sort of cnt entries by (key desc, idx asc)
