@@ -210,8 +210,16 @@ int irc_lstm_hprev(const void* hout, void* hprev, int64_t B, int64_t L, int64_t 
  * irc_lstm_coop_pack: W_hh fp32 [ndir][4H][H] -> wf, wb bf16 (4H*H per dir each).
  * irc_lstm_fwd_coop: xp_packed as irc_lstm_fwd_mfma; gsave/csave (NULL for the
  *   no-grad encoder) in a layout private to the coop pair.  sync is zeroed by the
- *   call; its last word is nonzero after a cluster timed out (never expected).
- * irc_lstm_bwd_coop: dy fp32 [B*L][ndir*H] -> dgates bf16 [B*L][ndir*4H]. */
+ *   call; its last word is nonzero after a cluster timed out (never expected: the
+ *   launch is sized from the device's CU count so both encoders' clusters are
+ *   co-resident).  On a timeout the call itself overwrites its output (hout /
+ *   dgates) with NaN on the device, so no caller can consume stale state.
+ * irc_lstm_bwd_coop: dy fp32 [B*L][ndir*H] -> dgates bf16 [B*L][ndir*4H].
+ * irc_lstm_coop_fault: *fault (uint32, device) |= the call's timeout word, on
+ *   the stream without a host sync; the head keeps one sticky word per encoder
+ *   and the train loop reads it at its existing sync points.
+ * IRC_LSTM_COOP_SPIN_MAX (environment, read per call) bounds the spins of every
+ *   cross-CU wait (debug knob; 0 = time out at the first unsatisfied wait). */
 int irc_lstm_coop_supported(int64_t H);
 int64_t irc_lstm_coop_sizes(int64_t B, int64_t L, int64_t H, int64_t ndir, int which);
 int irc_lstm_coop_pack(const float* whh, int64_t H, int64_t ndir, void* wf, void* wb,
@@ -222,6 +230,8 @@ int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* hout, float*
 int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* gsave, const float* csave,
                       void* dgates, void* xch, void* sync, int64_t B, int64_t L, int64_t H,
                       int64_t ndir, irc_stream_t stream);
+int irc_lstm_coop_fault(const void* sync, int64_t B, int64_t ndir, void* fault,
+                        irc_stream_t stream);
 
 /* ------------------------------------------------- seq2vec tail + InfoNCE + optimizer
  * seq2vec mean-over-L (PAD included) + F.normalize (contrastive_module.py:102-112);

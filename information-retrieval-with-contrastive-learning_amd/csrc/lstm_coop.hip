@@ -30,6 +30,8 @@
 // Co-residency: <= 16 groups per launch (<= 128 workgroups per direction pair,
 // one per CU by LDS), so two concurrent launches (query and key encoders) fit
 // the 256 CUs; spins are bounded and set a timeout word instead of hanging.
+#include <cstdlib>
+
 #include "irc_common.h"
 
 namespace irc {
@@ -48,7 +50,7 @@ constexpr int WSLICE = 4 * UPW * H;          // bf16 elements of one member's W 
 constexpr int GSTEP = BG * 4 * H;            // floats of gates per (dir, group, t)
 constexpr int CSTEP = BG * H;                // floats of c per (dir, group, t)
 constexpr int MAX_GROUPS = 16;               // per launch (co-residency bound)
-constexpr unsigned SPIN_MAX = 1u << 24;
+constexpr unsigned SPIN_MAX = 1u << 24;      // default spin bound (IRC_LSTM_COOP_SPIN_MAX)
 
 typedef __attribute__((address_space(1))) unsigned int gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -82,7 +84,7 @@ __device__ __forceinline__ void st_sc1_pair(void* p, unsigned long long a, unsig
 // epoch; values out.  Wave-uniform loop; on timeout sets tmo + the LDS abort word.
 template <int N, typename F>
 __device__ __forceinline__ void sweep(F addr, unsigned epoch, unsigned (&v)[N], unsigned* tmo,
-                                      int* abort_lds) {
+                                      int* abort_lds, unsigned spin_max) {
   for (unsigned spins = 0;;) {
     bool ok = true;
 #pragma unroll
@@ -92,7 +94,7 @@ __device__ __forceinline__ void sweep(F addr, unsigned epoch, unsigned (&v)[N], 
       ok &= (unsigned)(x >> 32) == epoch;
     }
     if (__all(ok)) return;
-    if (++spins > SPIN_MAX) {
+    if (++spins > spin_max) {
       if ((threadIdx.x & 63) == 0) {
         __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *abort_lds = 1;
@@ -128,7 +130,7 @@ __device__ __forceinline__ void publish_flag(unsigned* flag, unsigned epoch) {
 
 // R1 consume: wave 0 polls the P flags (relaxed, >= epoch), then a barrier.
 __device__ __forceinline__ void poll_flags(unsigned* flags, unsigned epoch, unsigned* tmo,
-                                           int* abort_lds) {
+                                           int* abort_lds, unsigned spin_max) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     for (unsigned spins = 0;;) {
@@ -137,7 +139,7 @@ __device__ __forceinline__ void poll_flags(unsigned* flags, unsigned epoch, unsi
         ok = __hip_atomic_load((gu32*)(flags + lane), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT) >= epoch;
       if (__all(ok)) break;
-      if (++spins > SPIN_MAX) {
+      if (++spins > spin_max) {
         if (lane == 0) {
           __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           *abort_lds = 1;
@@ -154,14 +156,15 @@ __device__ __forceinline__ void poll_flags(unsigned* flags, unsigned epoch, unsi
 // producers may still be computing) until every tag == epoch, then a barrier; the
 // full sweep that follows then normally needs a single pass.
 __device__ __forceinline__ void poll_sentinels(const unsigned long long* const* sent,
-                                               unsigned epoch, unsigned* tmo, int* abort_lds) {
+                                               unsigned epoch, unsigned* tmo, int* abort_lds,
+                                               unsigned spin_max) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     for (unsigned spins = 0;;) {
       bool ok = true;
       if (lane < P) ok = (unsigned)(ld_sc1(sent[lane]) >> 32) == epoch;
       if (__all(ok)) break;
-      if (++spins > SPIN_MAX) {
+      if (++spins > spin_max) {
         if (lane == 0) {
           __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           *abort_lds = 1;
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     const float* __restrict__ xp, const unsigned short* __restrict__ wpk,
     unsigned short* __restrict__ hout, float* __restrict__ gsave, float* __restrict__ csave,
     unsigned short* xch, unsigned* flags, unsigned* tmo, int B, int L, int ndir, int grp0,
-    int ngrp_launch, int ngrp_total) {
+    int ngrp_launch, int ngrp_total, unsigned spin_max) {
   __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
   __shared__ __attribute__((aligned(16))) unsigned short hb[BG][HP];
   __shared__ int abort_lds;
@@ -301,7 +304,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         const unsigned long long* sent[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) sent[q] = Xp + q * (UPW / 2);
-        poll_sentinels(sent, ep, tmo, &abort_lds);
+        poll_sentinels(sent, ep, tmo, &abort_lds, spin_max);
       }
       constexpr int NG = 3 * BG * UPW / 2 / NTH;
       unsigned v[NG];
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         const int mm = (m + 1 + idx / (BG * UPW / 2)) & 3, loc = idx % (BG * UPW / 2);
         return Xp + (loc / (UPW / 2)) * (H / 2) + mm * (UPW / 2) + loc % (UPW / 2);
       };
-      sweep<NG>(addr, ep, v, tmo, &abort_lds);
+      sweep<NG>(addr, ep, v, tmo, &abort_lds, spin_max);
 #pragma unroll
       for (int k = 0; k < NG; ++k) {
         const int idx = k * NTH + threadIdx.x;
@@ -356,7 +359,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     const float* __restrict__ dy, const unsigned short* __restrict__ wtpk,
     const float* __restrict__ gsave, const float* __restrict__ csave,
     unsigned short* __restrict__ dg, float* xch, unsigned* flags, unsigned* tmo, int B, int L,
-    int ndir, int grp0, int ngrp_launch, int ngrp_total) {
+    int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max) {
   __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
   __shared__ __attribute__((aligned(16))) unsigned short dgl[BG][HP];  // own dgates, k = g*64+lu
   __shared__ int abort_lds;
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
           st_sc1_x4(Xp + ((((w * 4 + cb) * 2 + rb) * 64 + lane) * 4),
                     __builtin_bit_cast(u32x4, acc[rb][cb]));
       publish_flag(fl + m, ep);
-      poll_flags(fl, ep, tmo, &abort_lds);
+      poll_flags(fl, ep, tmo, &abort_lds, spin_max);
       if (abort_lds) return;
       // own units live in every member's block m, cb = w: sum in member order
       u32x4 v[P][2];
@@ -532,6 +535,26 @@ __global__ void pack_coop_kernel(const float* __restrict__ whh, unsigned short* 
   }
 }
 
+// After a launch whose clusters timed out (tmo != 0), the output is overwritten
+// with bf16 NaN on the device, so a timeout can never pass for a result: the
+// NaN reaches the embeddings / gradients and the loss, whoever the caller is.
+// Every block reads the one word and leaves at once in the normal case.
+__global__ void poison_on_timeout_kernel(const unsigned* __restrict__ tmo,
+                                         unsigned short* __restrict__ out, int64_t n) {
+  if (__hip_atomic_load((const gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+    return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = 0x7FC0;  // bf16 quiet NaN
+}
+
+// Sticky fault word: *fault |= timeout word (device side, no host sync).
+__global__ void fault_or_kernel(const unsigned* __restrict__ tmo, unsigned* fault) {
+  const unsigned t = __hip_atomic_load((const gu32*)tmo, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  if (t) atomicOr(fault, t);
+}
+
 }  // namespace lstmc
 }  // namespace irc
 
@@ -561,6 +584,34 @@ extern "C" int irc_lstm_coop_pack(const float* whh, int64_t H, int64_t ndir, voi
   return check_launch("lstm_coop_pack");
 }
 
+// Spin bound of the cross-CU hand-off (IRC_LSTM_COOP_SPIN_MAX overrides; a
+// debug knob: 0 makes every wait that is not satisfied at once time out, which
+// the fault-path tests use).  ~1.6e9 cycles by default -- a true deadlock only.
+static unsigned coop_spin_max() {
+  const char* e = getenv("IRC_LSTM_COOP_SPIN_MAX");
+  return e ? (unsigned)strtoul(e, nullptr, 10) : lstmc::SPIN_MAX;
+}
+
+// Clusters per launch such that every workgroup of the q- and k-encoder launches
+// (which may run concurrently on two streams) is co-resident: one workgroup per
+// CU (128 KB LDS each), so 2 * groups * P * ndir <= CUs.  The CU count comes
+// from the device, not a constant; on MI355X (256 CUs, ndir 2) this is 16.
+static int coop_groups_per_launch(int64_t ndir) {
+  int dev = 0, cus = 0;
+  hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  int g = cus / (2 * lstmc::P * (int)ndir);
+  g = g < lstmc::MAX_GROUPS ? g : lstmc::MAX_GROUPS;
+  return g < 1 ? 1 : g;
+}
+
+static void coop_poison(const unsigned* tmo, void* out, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(lstmc::poison_on_timeout_kernel, dim3(256), dim3(256), 0, st, tmo,
+                     (unsigned short*)out, n);
+}
+
 // sync: flags (ndir*ngrp*P words) followed by the timeout word; zeroed here.
 extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* hout, float* gsave,
                                  float* csave, void* xch, void* sync, int64_t B, int64_t L,
@@ -570,19 +621,23 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
   if (B == 0 || L == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
   const int ngrp = (int)((B + lstmc::BG - 1) / lstmc::BG);
+  const int gpl = coop_groups_per_launch(ndir);
+  const unsigned spin_max = coop_spin_max();
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::P;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
   hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 2), st);
   prof_begin(st);
-  for (int g0 = 0; g0 < ngrp; g0 += lstmc::MAX_GROUPS) {
-    const int n = ngrp - g0 < lstmc::MAX_GROUPS ? ngrp - g0 : lstmc::MAX_GROUPS;
+  for (int g0 = 0; g0 < ngrp; g0 += gpl) {
+    const int n = ngrp - g0 < gpl ? ngrp - g0 : gpl;
     const dim3 grid((unsigned)((n + 7) / 8 * 32), (unsigned)ndir);
     hipLaunchKernelGGL(lstmc::lstm_fwd_coop, grid, dim3(lstmc::NTH), 0, st, xp_packed,
                        (const unsigned short*)wf, (unsigned short*)hout, gsave, csave,
-                       (unsigned short*)xch, flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp);
+                       (unsigned short*)xch, flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp,
+                       spin_max);
   }
   prof_end("lstm_fwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
+  coop_poison(tmo, hout, B * L * ndir * H, st);
   return check_launch("lstm_fwd_coop");
 }
 
@@ -593,17 +648,30 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
   if (B == 0 || L == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
   const int ngrp = (int)((B + lstmc::BG - 1) / lstmc::BG);
+  const int gpl = coop_groups_per_launch(ndir);
+  const unsigned spin_max = coop_spin_max();
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::P;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
   prof_begin(st);
-  for (int g0 = 0; g0 < ngrp; g0 += lstmc::MAX_GROUPS) {
-    const int n = ngrp - g0 < lstmc::MAX_GROUPS ? ngrp - g0 : lstmc::MAX_GROUPS;
+  for (int g0 = 0; g0 < ngrp; g0 += gpl) {
+    const int n = ngrp - g0 < gpl ? ngrp - g0 : gpl;
     const dim3 grid((unsigned)((n + 7) / 8 * 32), (unsigned)ndir);
     hipLaunchKernelGGL(lstmc::lstm_bwd_coop, grid, dim3(lstmc::NTH), 0, st, dy,
                        (const unsigned short*)wb, gsave, csave, (unsigned short*)dg, (float*)xch,
-                       flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp);
+                       flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp, spin_max);
   }
   prof_end("lstm_bwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
+  coop_poison(tmo, dg, B * L * ndir * 4 * H, st);
   return check_launch("lstm_bwd_coop");
+}
+
+extern "C" int irc_lstm_coop_fault(const void* sync, int64_t B, int64_t ndir, void* fault,
+                                   irc_stream_t stream) {
+  IRC_REQUIRE(sync != nullptr && fault != nullptr, "lstm_coop_fault: null pointer");
+  const int64_t ngrp = (B + lstmc::BG - 1) / lstmc::BG;
+  const unsigned* tmo = static_cast<const unsigned*>(sync) + ndir * ngrp * lstmc::P;
+  hipLaunchKernelGGL(lstmc::fault_or_kernel, dim3(1), dim3(64), 0, as_stream(stream), tmo,
+                     static_cast<unsigned*>(fault));
+  return check_launch("lstm_coop_fault");
 }

@@ -97,6 +97,9 @@ class LSTMHead(nn.Module):
         self.offsets, self.numel_flat = _layout(self.specs)
         self.flat = nn.Parameter(torch.zeros(self.numel_flat), requires_grad=True)
         self.register_buffer("flat_grad", torch.zeros(self.numel_flat), persistent=False)
+        # sticky device word: OR of every cluster recurrence's timeout word since the
+        # last check_fault() (the calls also NaN-poison their outputs on a timeout)
+        self.register_buffer("coop_fault", torch.zeros(1, dtype=torch.int32), persistent=False)
         if init:
             self.reset_parameters()
 
@@ -208,7 +211,9 @@ class LSTMHead(nn.Module):
             xp = ops.gemm(x, wp, bias=bp, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
             if kind == "coop":
                 wf, wb = ops.lstm_coop_pack(whh, H, nd)
-                hout, gsave, csave, hprev, _ = ops.lstm_fwd_coop(xp, wf, B, L, H, nd, save=save)
+                hout, gsave, csave, hprev, sync = ops.lstm_fwd_coop(xp, wf, B, L, H, nd,
+                                                                    save=save)
+                ops.lstm_coop_fault(sync, B, nd, self.coop_fault)
                 wT = wb
             else:
                 hout, gsave, csave, hprev = ops.lstm_fwd_mfma(xp, w, B, L, H, nd, save=save)
@@ -290,7 +295,8 @@ class LSTMHead(nn.Module):
         g = self.flat_grad
         o = self.offsets
         if kind == "coop":
-            dg, _ = ops.lstm_bwd_coop(dy, whhT, gsave, csave, B, L, H, nd)
+            dg, sync = ops.lstm_bwd_coop(dy, whhT, gsave, csave, B, L, H, nd)
+            ops.lstm_coop_fault(sync, B, nd, self.coop_fault)
         else:
             dg = ops.lstm_bwd_mfma(dy, whhT, gsave, csave, B, L, H, nd)
         In = x.shape[1]
@@ -323,6 +329,17 @@ class LSTMHead(nn.Module):
             t.record_stream(side)
         self._wgrad_pending = side
         return dx
+
+    def check_fault(self):
+        """Raise if any cluster recurrence timed out since the last check (host
+        sync: called at the train loop's existing sync points)."""
+        if self.coop_fault.device.type != "cuda":
+            return
+        if int(self.coop_fault.item()) != 0:
+            self.coop_fault.zero_()
+            raise ops.IRCError(
+                "LSTM cluster recurrence (irc_lstm_fwd_coop / irc_lstm_bwd_coop) timed out: "
+                "its workgroups were not co-resident; the affected outputs were NaN-poisoned")
 
     def forward(self, features, **kwargs):
         """Per-position head output [B, L, D] (reference LSTM.forward semantics);

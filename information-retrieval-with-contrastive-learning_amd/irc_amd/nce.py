@@ -3,12 +3,17 @@
 Reference: ``NCELoss._compute_info_loss`` (src/contrastor/contrastive_loss.py:56-93):
 F = [q; k], S = F F^T with the diagonal dropped, positive column (i+N) mod 2N,
 optional queue logits q.queue REUSED for the k-rows (.repeat(2, 1)), logits / T,
-CrossEntropy(sum) with target 0, divided by 2.  Gradient flows into q only.
+CrossEntropy(sum) with target 0, divided by 2.  With the momentum encoder (the
+reference default) k is a no-grad key and the gradient flows into q only; with
+``use_momentum: False`` the reference's k = seq2vec(positive) comes from
+encoder_q WITH autograd (contrastive_module.py:82-83), so k receives
+dk = G[N:] F + G[:, N:]^T F as well (S = F F^T; the queue logits use q only).
 
 Forward: S = F F^T and LQ = q queue as exact-fp32 MFMA GEMMs, one row kernel
 for log-sum-exp + NLL, a deterministic sum.  Backward: one elementwise kernel
 for the softmax gradients (scaled on device by the upstream gradient -- no host
-sync), then dq = G[:N] F + G[:, :N]^T F + GQ queue^T as three accumulating GEMMs.
+sync), then dq = G[:N] F + G[:, :N]^T F + GQ queue^T as three accumulating GEMMs (and
+dk as two more when k requires grad).
 """
 from __future__ import annotations
 
@@ -55,10 +60,15 @@ class _InfoNCE(torch.autograd.Function):
         ops.gemm(GS[:, :N], F, trans_a=True, b_is_nk=False, out=dq, accumulate=True)  # G_jn F_j
         if Kq > 0:
             ops.gemm(GQ, ctx.queue, out=dq, accumulate=True)  # GQ @ queue^T
+        dk = None
+        if ctx.needs_input_grad[1]:
+            dk = ops.gemm(GS[N:], F, b_is_nk=False)
+            ops.gemm(GS[:, N:], F, trans_a=True, b_is_nk=False, out=dk, accumulate=True)
         ctx.LQ = ctx.queue = None
-        return dq, None, None, None
+        return dq, dk, None, None
 
 
 def info_nce(q, k, queue, T):
-    """0-d fp32 loss tensor with autograd into q."""
-    return _InfoNCE.apply(q, k.detach(), None if queue is None else queue.detach(), float(T))
+    """0-d fp32 loss tensor with autograd into q (and into k when k requires grad:
+    the reference's use_momentum False configuration)."""
+    return _InfoNCE.apply(q, k, None if queue is None else queue.detach(), float(T))

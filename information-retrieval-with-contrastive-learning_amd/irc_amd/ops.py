@@ -9,6 +9,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from ._lib import IRCError  # noqa: F401  (re-exported for callers of ops)
 from ._torch import ptr, require_hip, stream_ptr
 
 BF16, F32 = torch.bfloat16, torch.float32
@@ -221,6 +222,13 @@ def lstm_bwd_coop(dy, wb, gsave, csave, B, L, H, ndir):
     _lib.call("irc_lstm_bwd_coop", ptr(dy), ptr(wb), ptr(gsave), ptr(csave), ptr(dg), ptr(xch),
               ptr(sync), B, L, H, ndir, stream_ptr(dev))
     return dg, sync
+
+
+def lstm_coop_fault(sync, B, ndir, fault):
+    """fault (int32 device word) |= the coop call's timeout word -- stream-ordered,
+    no host sync (the call has already NaN-poisoned its output on a timeout)."""
+    require_hip(sync, fault)
+    _lib.call("irc_lstm_coop_fault", ptr(sync), B, ndir, ptr(fault), stream_ptr(sync.device))
 
 
 def lstm_coop_timed_out(sync, B, ndir):

@@ -201,7 +201,9 @@ class RetrievalModelWrapper(nn.Module):
         group = getattr(self, "dist_group", None)
         if group is not None:  # global in-batch negatives (irc_amd.dist)
             emb_q = gather_rows(emb_q, group)
-            emb_k = gather_rows(emb_k.detach(), group)
+            # keys carry autograd only without the momentum encoder (then they come
+            # from encoder_q, contrastive_module.py:82-83 of the reference)
+            emb_k = gather_rows(emb_k if not self.use_momentum else emb_k.detach(), group)
         queue = None if not self.use_queue or not self.add_queue_to_loss else self.queue
         loss = self.criterion(emb_q, emb_k, queue, cluster_result, indexes)
         if self.use_queue and self.training:
