@@ -1,11 +1,12 @@
 """Drop-in for the reference main.py (same flags; main.py:14-112).
 
     python main.py [--config config.yaml] [--data doc|fever] [--gpu 0] [--ckpt X]
-                   [--model LSTM] [--loss InfoNCE] [--opt adam] [--sample uniform|tf_idf]
-                   [--seed 1337] [--logdir log] [--ckptdir ckpt]
+                   [--model LSTM|BERT] [--loss InfoNCE] [--opt adam] [--sample uniform|tf_idf]
+                   [--seed 1337] [--logdir log] [--ckptdir ckpt] [--retrieval sparse|dense]
 
---data doc trains (src.train.train); --data fever runs dense retrieval
-(src.evaluation.predict).  The compute runs on the MI355X HIP kernels only:
+--data doc trains (src.train.train); --data fever runs src.evaluation.predict:
+the reference's sparse candidate filter per claim (default) or, with
+``--retrieval dense``, the bi-encoder's exact top-k over the evidence corpus.  The compute runs on the MI355X HIP kernels only:
 ``--gpu -1`` (CPU) is rejected -- there is no CPU fallback in this build.
 """
 import argparse
@@ -34,11 +35,16 @@ def get_args(argv=None):
     p.add_argument("--seed", default=1337, type=int, help="Random seed.")
     p.add_argument("--gpu", default="0", type=str, help="GPU id (-1: CPU, not supported)")
     p.add_argument("--ckpt", type=str, help="Path to load target pretrain model")
-    p.add_argument("--model", default="LSTM", type=str, choices=["LSTM"])
+    p.add_argument("--model", default="LSTM", type=str, choices=["LSTM", "BERT"],
+                   help="LSTM: frozen BERT + BiLSTM head (reference); BERT: trainable "
+                        "BERT bi-encoder (superset)")
     p.add_argument("--loss", default="InfoNCE", type=str,
                    choices=["InfoNCE", "ProtoNCE", "HProtoNCE"])
     p.add_argument("--opt", default="adam", type=str, choices=["adam", "sgd"])
     p.add_argument("--sample", default="uniform", type=str, choices=["uniform", "tf_idf"])
+    p.add_argument("--retrieval", default="sparse", type=str, choices=["sparse", "dense"],
+                   help="--data fever: sparse n-gram filter as the reference (default) or "
+                        "dense bi-encoder top-k (superset)")
     return p.parse_args(argv)
 
 

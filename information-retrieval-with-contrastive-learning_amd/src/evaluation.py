@@ -1,21 +1,24 @@
-"""Drop-in for src/evaluation.py: dense retrieval with the trained bi-encoder.
+"""Drop-in for src/evaluation.py: claim -> evidence retrieval.
 
-The reference's ``predict`` (src/evaluation.py:86-116) runs a sparse hashed
-n-gram candidate filter and leaves the dense claim/evidence cosine commented
-out (:110-115).  Here ``predict`` does the dense path the reference sketches:
-``ctx2vec`` embeddings (contrastive_module.py:96-100) of the evidence corpus are
-sharded into HBM and each claim batch is scored against all of them with the
-exact top-k scan (irc_amd.retrieval, closest_docs ordering,
-tfidf_doc_ranker.py:60-75).  ``documents_filtering`` -- the sparse filter the
-reference's predict actually calls -- runs on the GPU too (irc_amd.sparse).
+``predict`` (src/evaluation.py:86-116) keeps the reference's behaviour by
+default (``args.retrieval`` "sparse", main.py ``--retrieval``): per claim the
+hashed n-gram candidate filter ``documents_filtering`` (here on the GPU,
+irc_amd.sparse) with its latency and ``len(docs)`` printed, as the reference
+prints them.  ``--retrieval dense`` (superset) runs the dense path the reference
+sketches in its commented-out tail (:110-115): ``ctx2vec`` embeddings
+(contrastive_module.py:96-100) of the evidence corpus sharded into HBM and each
+claim batch scored against all of them with the exact top-k scan
+(irc_amd.retrieval, closest_docs ordering, tfidf_doc_ranker.py:60-75), then
+evidence recall@k printed.
 """
+import pickle
 import time
 
 import torch
 from tqdm import tqdm
 
 from irc_amd.retrieval import ShardedDenseIndex
-from irc_amd.sparse import SparseIndex
+from irc_amd.sparse import SparseIndex, load_sparse_csr
 from src.dataset import get_dataloader
 from src.model import load_model
 
@@ -61,6 +64,36 @@ def encode_corpus(model, texts, device, batch_size=256):
 
 @torch.no_grad()
 def predict(args, k=100):
+    """evaluation.py:86-108: load the checkpoint, then per claim the sparse filter
+    (latency and candidate count printed); ``args.retrieval == "dense"``:
+    predict_dense.  Returns the per-claim candidate counts (sparse) or recall@k."""
+    if getattr(args, "retrieval", "sparse") == "dense":
+        return predict_dense(args, k)
+    assert args.ckpt is not None
+    _, model, _, _ = load_model(args.ckpt)
+    model = model.to(args.device)
+    fever_loader = get_dataloader(args, train=False)
+    ds = args.config["dataset"]
+    _, metadata = load_sparse_csr(ds["tfidf"])
+    count_matrix, _ = load_sparse_csr(ds["inverted_file"])
+    with open(ds["full_docs_dict"], "rb") as f:  # the user's own preprocessing output
+        full_docs_dict = pickle.load(f)
+    counts = []
+    for batch in tqdm(fever_loader, desc="Iteration"):
+        claim = [data["claim"] for data in batch]
+        s = time.time()
+        docs = documents_filtering(claim[0], args, count_matrix, metadata, full_docs_dict, False)
+        e = time.time()
+        print(e - s)
+        print(len(docs))
+        counts.append(len(docs))
+    return counts
+
+
+@torch.no_grad()
+def predict_dense(args, k=100):
+    """Dense claim -> evidence-line retrieval with the trained bi-encoder: prints
+    each batch's latency and the evidence recall@k; returns recall@k."""
     assert args.ckpt is not None
     _, model, _, _ = load_model(args.ckpt)
     model = model.to(args.device).eval()

@@ -6,6 +6,8 @@
 (model.py:44-58 semantics); checkpoints keep the reference layout
 {Model, Optimizer, Current_step, Args} and file name (model.py:76-99).
 """
+import argparse
+
 import torch
 
 from irc_amd.bert_train import BertEncoder
@@ -67,10 +69,19 @@ def save_model(model, optimizer, args, current_step):
     torch.save(all_states, path)
 
 
-def load_model(path):
-    # Our own checkpoints hold an argparse.Namespace ("Args"), as the reference's do.
-    ckpt = torch.load(path, map_location="cpu", weights_only=False)
+def load_model(path, bert_config=None):
+    """Reference load_model (model.py:87-99): (args, model, optimizer, step) from a
+    checkpoint written by this package or by the reference itself.
+
+    Loaded weights-only: the checkpoint's "Args" is an argparse.Namespace (config
+    dict, strings, a torch.device), which is allow-listed; nothing in the file is
+    executed.  ``bert_config`` (superset) replaces ``args.config['bert']`` -- for a
+    reference checkpoint whose frozen BERT is not bert-base-uncased."""
+    torch.serialization.add_safe_globals([argparse.Namespace])
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
     args = ckpt["Args"]
+    if bert_config is not None:
+        args.config["bert"] = bert_config
     model = build_model(args)
     print("[Runner] - Loading model parameters")
     res = model.load_state_dict(ckpt["Model"], strict=False)

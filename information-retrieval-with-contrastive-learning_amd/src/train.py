@@ -69,12 +69,25 @@ class TrainState:
         # over the group with one RCCL all-reduce before the fused clip + Adam, so
         # every rank applies the identical update.
         self.process_group = None
+        self.world = 1
 
     def set_process_group(self, group):
         """Data-parallel training over ``group``: embeddings all-gathered for global
         in-batch negatives (model.dist_group) + head gradients all-reduced."""
+        from irc_amd.dist import world_of
+
         self.process_group = group
+        self.world = world_of(group)
         self.model.dist_group = group
+
+    def check_faults(self):
+        """Raise if a cluster recurrence of either encoder timed out since the last
+        check (reads the heads' sticky device fault words: a host sync, so it runs
+        only where the loop already syncs)."""
+        for name in ("encoder_q", "encoder_k"):
+            enc = getattr(self.model, name, None)
+            if enc is not None and hasattr(enc, "check_fault"):
+                enc.check_fault()
 
     def _maybe_enable_queue(self):
         m = self.model
@@ -86,10 +99,14 @@ class TrainState:
         """forward_fn() -> loss tensor of this micro-batch (model(...) call)."""
         self._maybe_enable_queue()
         self.batch_size += n_pairs
-        loss = forward_fn() / self.acml
+        # data parallel: the loss is the GLOBAL micro-batch's (gathered negatives),
+        # so it is divided by the global accumulation size acml * world, as one
+        # process stepping the whole global batch would (train.py:137-146)
+        loss = forward_fn() / (self.acml * self.world)
         loss.backward()
         if sync_loss:
             self.loss_sum += loss.item()  # the reference logs every micro-batch (train.py:148)
+            self.check_faults()
         else:
             self.loss_sum = self.loss_sum + loss.detach()
         stepped = False
@@ -191,6 +208,7 @@ def train(args):
                         loss_avg = float(np.mean(st.loss_record))
                         st.loss_record = []
                         grad_norm = float(st.grad_norm[0].item())
+                        st.check_faults()
                         if math.isnan(grad_norm) or math.isinf(grad_norm):
                             print(f"[Runner] - Error : grad norm is nan/inf at step {st.step_sum}")
                         log.add_scalar("train_loss", loss_avg, st.step_sum)

@@ -207,7 +207,7 @@ def _logsumexp(x: np.ndarray, axis: int = -1) -> np.ndarray:
 
 
 def nce_info_loss(q: np.ndarray, k: np.ndarray, queue: np.ndarray | None, T: float,
-                  want_grad: bool = True):
+                  want_grad: bool = True, want_dk: bool = False):
     """Loss and dL/dq of ``NCELoss._compute_info_loss`` (fp64 internally).
 
     * F = cat[q; k] (2N x D), S = F F^T (contrastive_loss.py:61-62);
@@ -217,7 +217,9 @@ def nce_info_loss(q: np.ndarray, k: np.ndarray, queue: np.ndarray | None, T: flo
       (:79-80) -- a reference quirk reproduced here;
     * CrossEntropy(sum) with target 0, divided by 2 (:51, :91-92).
     Gradient flows into q only (k comes from the no-grad momentum encoder,
-    contrastive_module.py:82-83, 109-110).
+    contrastive_module.py:82-83, 109-110).  ``want_dk``: also return dL/dk, the
+    use_momentum False case where k = seq2vec(positive) through encoder_q with
+    autograd (contrastive_module.py:82-83); the queue logits use q only.
     """
     q = np.asarray(q, F64)
     k = np.asarray(k, F64)
@@ -250,6 +252,8 @@ def nce_info_loss(q: np.ndarray, k: np.ndarray, queue: np.ndarray | None, T: flo
     if Qrep is not None:
         GQ = P[:, 2 * n:] * (0.5 / T)
         dq += (GQ[:n] + GQ[n:]) @ np.asarray(queue, F64).T
+    if want_dk:
+        return loss, dq, dF[n:].copy()
     return loss, dq
 
 

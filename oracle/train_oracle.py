@@ -30,6 +30,7 @@ def run_trajectory(fx: dict):
     nheads = 2
     in_dim, hsz, nlayers, outd = (int(x) for x in fx["lstm_cfg"])
     T, mom, qsize, qstart = fx["loss_cfg"]
+    use_mom = int(fx["use_momentum"]) if "use_momentum" in fx else 1
     B, acml, total, log_step = (int(x) for x in fx["train_cfg"])
     lr, b1, b2, clip = fx["adam"]
     pq = split_state(init, "encoder_q.")
@@ -53,8 +54,16 @@ def run_trajectory(fx: dict):
         feats = O.bert_forward(ids, mask, bert_w, nl_bert, nheads).astype(np.float64)
         a, p = feats[:nb], feats[nb:]
         emb_q, cq = O.seq2vec(a, pq, nlayers)
-        emb_k, _ = O.seq2vec(p, pk, nlayers)
-        loss, dq = O.nce_info_loss(emb_q, emb_k, queue if add_q else None, float(T))
+        if use_mom:
+            emb_k, _ = O.seq2vec(p, pk, nlayers)
+            loss, dq = O.nce_info_loss(emb_q, emb_k, queue if add_q else None, float(T))
+        else:  # keys through encoder_q with autograd (contrastive_module.py:82-83)
+            emb_k, ck = O.seq2vec(p, pq, nlayers)
+            loss, dq, dk = O.nce_info_loss(emb_q, emb_k, queue if add_q else None, float(T),
+                                           want_dk=True)
+            gk = O.seq2vec_bwd(dk / acml, pq, ck, nlayers)
+            for k in grads:
+                grads[k] += gk[k]
         losses.append(loss)
         g = O.seq2vec_bwd(dq / acml, pq, cq, nlayers)
         for k in grads:

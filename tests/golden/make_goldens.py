@@ -125,6 +125,62 @@ def gen_nce(out):
           res["n4_d8_k16_noq_loss"], res["n4_d8_k16_q_loss"])
 
 
+def gen_nce_c2(out):
+    """NCELoss at the C2 shapes (N = 256, K = 12544, D = 128 and
+    768), with and without the queue.  Inputs are regenerated from numpy streams
+    (tests/synth_inputs.py); the fixture holds the loss, dL/dq's first / last 16
+    rows, every row norm and every column sum of dL/dq."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import synth_inputs as SI
+    from src.contrastor.contrastive_loss import NCELoss
+
+    res = {}
+    for (n, d, kq, seed) in SI.NCE_C2_CASES:
+        q, k, queue = SI.nce_c2_inputs(n, d, kq, seed)
+        crit = NCELoss({"temperature": 0.05})
+        for with_q in (False, True):
+            qq = torch.from_numpy(q).clone().requires_grad_(True)
+            loss = crit(qq, torch.from_numpy(k), torch.from_numpy(queue) if with_q else None)
+            loss.backward()
+            dq = _np(qq.grad)
+            tag = f"n{n}_d{d}_k{kq}_{'q' if with_q else 'noq'}"
+            res[f"{tag}_loss"] = np.float64(loss.item())
+            res[f"{tag}_dq_head"] = dq[:16]
+            res[f"{tag}_dq_tail"] = dq[-16:]
+            res[f"{tag}_dq_rownorm"] = np.linalg.norm(dq.astype(np.float64), axis=1)
+            res[f"{tag}_dq_colsum"] = dq.astype(np.float64).sum(axis=0)
+            res[f"{tag}_in_sums"] = np.array([q.astype(np.float64).sum(),
+                                              k.astype(np.float64).sum(),
+                                              queue.astype(np.float64).sum()])
+    np.savez_compressed(os.path.join(out, "nce_c2.npz"), **res)
+    print("nce_c2:", {k: v for k, v in res.items() if k.endswith("_loss")})
+
+
+def gen_bert_base(out):
+    """HF BertModel at BERT-base size (12 layers, H = 768, A = 12, I = 3072) with
+    padding, B = 4, L = 64 -- the frozen encoder of config C2 as the reference
+    calls it (contrastive_module.py:36-41).  Weights from per-parameter numpy
+    streams (tests/synth_inputs.py), so only the output is committed."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import synth_inputs as SI
+    from transformers import BertConfig, BertModel
+
+    m = BertModel(BertConfig(**SI.BERT_BASE)).eval()
+    sd = {n: torch.from_numpy(SI.bert_param(n, tuple(v.shape)))
+          for n, v in m.state_dict().items() if "position_ids" not in n}
+    missing = m.load_state_dict(sd, strict=False).missing_keys
+    assert not [n for n in missing if "position_ids" not in n], missing
+    ids, mask = SI.bert_base_batch()
+    with torch.no_grad():
+        hs = m(input_ids=torch.from_numpy(ids), attention_mask=torch.from_numpy(mask))
+    hs = _np(hs.last_hidden_state)
+    pooled = hs.astype(np.float64).mean(axis=1)
+    np.savez_compressed(os.path.join(out, "bert_base.npz"), input_ids=ids, attention_mask=mask,
+                        last_hidden_state=hs,
+                        seq2vec=(pooled / np.linalg.norm(pooled, axis=1, keepdims=True)))
+    print("bert_base:", hs.shape, float(np.abs(hs).mean()))
+
+
 def _lstm_cfg(inp, hid, layers, outd):
     return {"model": {"LSTM": {"num_layers": layers, "bidirectional": True, "input_size": inp,
                                "hidden_size": hid, "output_size": outd,
@@ -280,7 +336,13 @@ def gen_scan(out):
 
 
 # ---------------------------------------------------------------------------
-def gen_train_traj(out, tmp):
+def gen_train_traj_nomom(out, tmp):
+    """The same run with loss.use_momentum False: keys come from encoder_q with
+    autograd (contrastive_module.py:82-83), no encoder_k, no momentum update."""
+    gen_train_traj(out, tmp, use_momentum=False, fname="train_traj_nomom.npz")
+
+
+def gen_train_traj(out, tmp, use_momentum=True, fname="train_traj.npz"):
     """Run the reference train() loop on a tiny config; record the trajectory."""
     import yaml
     import src.contrastor.contrastive_module as cm
@@ -305,7 +367,7 @@ def gen_train_traj(out, tmp):
         cfg = yaml.load(f, Loader=yaml.FullLoader)
     cfg["model"]["LSTM"].update(input_size=TINY_BERT["hidden_size"], hidden_size=16,
                                 num_layers=2, output_size=8)
-    cfg["loss"]["InfoNCE"].update(queue_size=32, queue_start_steps=2)
+    cfg["loss"]["InfoNCE"].update(queue_size=32, queue_start_steps=2, use_momentum=use_momentum)
     cfg["train"].update(batch_size=8, acml_batch_size=16, total_steps=4, log_step=2, n_jobs=0)
     cfg["dataset"]["docs_sentence"] = dpath
 
@@ -347,7 +409,12 @@ def gen_train_traj(out, tmp):
         cm.RetrievalModelWrapper.bert_extract = orig_extract
         cm.RetrievalModelWrapper.forward = orig_forward
 
-    ck = torch.load(os.path.join(args.ckptdir, "uniform_InfoNCE_LSTM_4.pth"), map_location="cpu",
+    ck_path = os.path.join(args.ckptdir, "uniform_InfoNCE_LSTM_4.pth")
+    if use_momentum:  # the reference-written checkpoint itself: load_model parity fixture
+        import shutil
+
+        shutil.copyfile(ck_path, os.path.join(out, "ref_ckpt_InfoNCE_LSTM_4.pth"))
+    ck = torch.load(ck_path, map_location="cpu",
                     weights_only=False)  # our own freshly written file
     final = ck["Model"]
     res = {}
@@ -371,7 +438,9 @@ def gen_train_traj(out, tmp):
                loss_cfg=np.array([0.05, 0.9, 32, 2]),
                train_cfg=np.array([8, 16, 4, 2]),
                adam=np.array([2.5e-4, 0.9, 0.999, 1.0]))
-    np.savez_compressed(os.path.join(out, "train_traj.npz"), **res)
+    if not use_momentum:
+        res["use_momentum"] = np.int64(0)
+    np.savez_compressed(os.path.join(out, fname), **res)
     print("train traj: micro-batch losses", rec["loss"])
 
 
@@ -381,14 +450,18 @@ def main():
         if len(sys.argv) > 1:  # regenerate selected fixtures only
             for name in sys.argv[1:]:
                 fn = globals()[f"gen_{name}"]
-                fn(HERE, tmp) if fn.__code__.co_argcount == 2 else fn(HERE)
+                fn(HERE, tmp) if "tmp" in fn.__code__.co_varnames[:fn.__code__.co_argcount] \
+                    else fn(HERE)
             return
         gen_nce(HERE)
+        gen_nce_c2(HERE)
+        gen_bert_base(HERE)
         gen_lstm_init(HERE)
         gen_seq2vec(HERE, tmp)
         gen_bert(HERE, tmp)
         gen_scan(HERE)
         gen_train_traj(HERE, tmp)
+        gen_train_traj_nomom(HERE, tmp)
 
 
 if __name__ == "__main__":

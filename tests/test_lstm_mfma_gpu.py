@@ -148,3 +148,68 @@ def test_coop_matches_single_cu_and_no_timeout(gpu, B, L):
     # bitwise reproducible (fixed member summation order)
     dg_c2, _ = ops.lstm_bwd_coop(dy, wb, g_c, c_c, B, L, H, nd)
     assert torch.equal(dg_c, dg_c2)
+
+
+@pytest.fixture
+def forced_coop_timeout():
+    """IRC_LSTM_COOP_SPIN_MAX=0 (read per call by the library): every cross-CU
+    wait that is not satisfied at once times out -- the debug path that must
+    never yield numbers."""
+    import os
+
+    os.environ["IRC_LSTM_COOP_SPIN_MAX"] = "0"
+    yield
+    del os.environ["IRC_LSTM_COOP_SPIN_MAX"]
+
+
+def test_coop_forced_timeout_poisons_outputs(gpu, forced_coop_timeout):
+    """A timed-out cluster call NaN-poisons its own output on the device and sets
+    the sticky fault word -- whatever the caller does with the sync word."""
+    from irc_amd import ops
+
+    torch.manual_seed(3)
+    B, L, nd = 64, 9, 2
+    whh = (torch.randn(nd * 4 * H, H) * 0.06).to(gpu)
+    xp = torch.randn(B * L, nd * 4 * H, device=gpu)
+    wf, wb = ops.lstm_coop_pack(whh, H, nd)
+    fault = torch.zeros(1, dtype=torch.int32, device=gpu)
+    h, g, c, _, sync = ops.lstm_fwd_coop(xp, wf, B, L, H, nd, save=True)
+    ops.lstm_coop_fault(sync, B, nd, fault)
+    assert ops.lstm_coop_timed_out(sync, B, nd)
+    assert int(fault.item()) != 0
+    assert bool(torch.isnan(h.float()).all())
+    dg, sync_b = ops.lstm_bwd_coop(torch.randn(B * L, nd * H, device=gpu), wb, g, c, B, L, H, nd)
+    assert ops.lstm_coop_timed_out(sync_b, B, nd)
+    assert bool(torch.isnan(dg.float()).all())
+
+
+def test_coop_forced_timeout_raises_in_train_step(gpu, forced_coop_timeout):
+    """The production step (H = 256 BiLSTM head on the cluster recurrence) raises
+    at its next sync point instead of training on stale state."""
+    import argparse
+
+    import yaml
+
+    from conftest import PKG
+    from irc_amd._lib import IRCError
+    from src.model import build_model, get_optimizer
+    from src.train import TrainState
+
+    with open(f"{PKG}/config.yaml") as f:
+        cfg = yaml.safe_load(f)
+    cfg["bert"] = {"name": "tiny", "config": {"vocab_size": 200, "hidden_size": 64,
+                                              "num_hidden_layers": 1, "num_attention_heads": 2,
+                                              "intermediate_size": 128,
+                                              "max_position_embeddings": 64}}
+    cfg["model"]["LSTM"].update(input_size=64, hidden_size=H, num_layers=2, output_size=32)
+    cfg["loss"]["InfoNCE"].update(queue_size=64)
+    cfg["train"].update(batch_size=32, acml_batch_size=32)
+    args = argparse.Namespace(config=cfg, loss="InfoNCE", model="LSTM", opt="adam",
+                              sample="uniform")
+    torch.manual_seed(0)
+    model = build_model(args).to(gpu).train()
+    st = TrainState(args, model, get_optimizer(args, model))
+    ids = torch.randint(5, 200, (64, 16), device=gpu)
+    mask = torch.ones_like(ids)
+    with pytest.raises(IRCError, match="timed out"):
+        st.micro_batch(32, lambda: model.forward_features(*model.bert_extract_ids(ids, mask, 32)))

@@ -132,8 +132,9 @@ def test_merge_equals_global():
     np.testing.assert_array_equal(ms, full_s)
 
 
-def test_train_trajectory_matches_reference():
-    fx = load_golden("train_traj.npz")
+@pytest.mark.parametrize("fixture", ["train_traj.npz", "train_traj_nomom.npz"])
+def test_train_trajectory_matches_reference(fixture):
+    fx = load_golden(fixture)
     losses, final = train_oracle.run_trajectory(fx)
     np.testing.assert_allclose(losses, fx["mb_loss"], rtol=2e-5, atol=1e-4)
     for k, v in final.items():
@@ -188,3 +189,52 @@ def test_e4m3_quantiser_matches_torch_cast():
     # decode table: max, min normal, min subnormal
     np.testing.assert_array_equal(O.dequantize_e4m3(np.array([0x7E, 0x08, 0x01], np.uint8)),
                                   np.array([448.0, 2**-6, 2**-9], np.float32))
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_nce_c2_shapes_match_reference(case):
+    """NCELoss at the C2 shapes (N=256, K=12544, D=128/768), inputs regenerated
+    from tests/synth_inputs.py, against the reference's own values."""
+    import synth_inputs as SI
+
+    g = load_golden("nce_c2.npz")
+    n, d, kq, seed = SI.NCE_C2_CASES[case]
+    q, k, queue = SI.nce_c2_inputs(n, d, kq, seed)
+    for with_q in (False, True):
+        tag = f"n{n}_d{d}_k{kq}_{'q' if with_q else 'noq'}"
+        np.testing.assert_array_equal(
+            g[f"{tag}_in_sums"], [q.astype(np.float64).sum(), k.astype(np.float64).sum(),
+                                  queue.astype(np.float64).sum()])  # inputs regenerate
+        loss, dq = O.nce_info_loss(q, k, queue if with_q else None, 0.05)
+        assert abs(loss - g[f"{tag}_loss"]) <= 1e-5 * abs(g[f"{tag}_loss"])
+        np.testing.assert_allclose(dq[:16], g[f"{tag}_dq_head"], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(dq[-16:], g[f"{tag}_dq_tail"], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(np.linalg.norm(dq, axis=1), g[f"{tag}_dq_rownorm"], rtol=1e-5)
+        np.testing.assert_allclose(dq.sum(axis=0), g[f"{tag}_dq_colsum"], rtol=1e-4, atol=1e-5)
+
+
+def test_bert_base_12_layers_matches_reference():
+    """The oracle's BERT at BERT-base size (12 layers, H=768) against HF's
+    last_hidden_state (the reference's frozen encoder), padded B=4, L=64."""
+    import synth_inputs as SI
+
+    g = load_golden("bert_base.npz")
+    names = ["embeddings.word_embeddings.weight", "embeddings.position_embeddings.weight",
+             "embeddings.token_type_embeddings.weight", "embeddings.LayerNorm.weight",
+             "embeddings.LayerNorm.bias"]
+    cfg = SI.BERT_BASE
+    H, I = cfg["hidden_size"], cfg["intermediate_size"]
+    shapes = {names[0]: (cfg["vocab_size"], H), names[1]: (cfg["max_position_embeddings"], H),
+              names[2]: (2, H), names[3]: (H,), names[4]: (H,)}
+    for l in range(cfg["num_hidden_layers"]):
+        p = f"encoder.layer.{l}."
+        for n, s in (("attention.self.query", (H, H)), ("attention.self.key", (H, H)),
+                     ("attention.self.value", (H, H)), ("attention.output.dense", (H, H)),
+                     ("intermediate.dense", (I, H)), ("output.dense", (H, I))):
+            shapes[p + n + ".weight"], shapes[p + n + ".bias"] = s, (s[0],)
+        for n in ("attention.output.LayerNorm", "output.LayerNorm"):
+            shapes[p + n + ".weight"] = shapes[p + n + ".bias"] = (H,)
+    w = {n: SI.bert_param(n, s) for n, s in shapes.items()}
+    hs = O.bert_forward(g["input_ids"], g["attention_mask"], w, cfg["num_hidden_layers"],
+                        cfg["num_attention_heads"])
+    np.testing.assert_allclose(hs, g["last_hidden_state"], rtol=1e-4, atol=1e-4)

@@ -27,7 +27,9 @@ def _args_from_golden(fx):
     cfg["model"]["LSTM"].update(input_size=in_dim, hidden_size=hsz, num_layers=nlayers,
                                 output_size=outd)
     cfg["loss"]["InfoNCE"].update(temperature=float(T), momentum=float(mom),
-                                  queue_size=int(qsize), queue_start_steps=int(qstart))
+                                  queue_size=int(qsize), queue_start_steps=int(qstart),
+                                  use_momentum=bool(int(fx["use_momentum"]))
+                                  if "use_momentum" in fx else True)
     cfg["train"].update(batch_size=B, acml_batch_size=acml, total_steps=total, log_step=log_step)
     init = {k[len("init_bert_model."):]: v for k, v in fx.items()
             if k.startswith("init_bert_model.")}
@@ -42,12 +44,12 @@ def _args_from_golden(fx):
                               sample="uniform")
 
 
-def _replay(gpu, precision, pipelined=False):
+def _replay(gpu, precision, pipelined=False, fixture="train_traj.npz"):
     from irc_amd.precision import get_precision, set_precision
     from src.model import build_model, get_optimizer
     from src.train import TrainState
 
-    fx = load_golden("train_traj.npz")
+    fx = load_golden(fixture)
     old = get_precision()
     set_precision(precision)
     try:
@@ -95,8 +97,11 @@ def _replay(gpu, precision, pipelined=False):
         set_precision(old)
 
 
-def test_train_trajectory_fp32(gpu):
-    fx, losses, model = _replay(gpu, "fp32")
+@pytest.mark.parametrize("fixture", ["train_traj.npz", "train_traj_nomom.npz"])
+def test_train_trajectory_fp32(gpu, fixture):
+    """fixture train_traj_nomom: loss.use_momentum False -- no encoder_k, the keys
+    come from encoder_q with autograd, so the InfoNCE backward feeds dk too."""
+    fx, losses, model = _replay(gpu, "fp32", fixture=fixture)
     np.testing.assert_allclose(losses, fx["mb_loss"], rtol=2e-4, atol=1e-4)
     sd = model.state_dict()
     for k in ("queue", "queue_ptr"):
@@ -110,9 +115,14 @@ def test_train_trajectory_fp32(gpu):
 
 def test_train_trajectory_bf16(gpu):
     """Production precision: bf16 BERT/LSTM operands, fp32 state/loss/optimizer.
-    Micro-batch losses (~25-45) within 3% of the fp32 reference."""
+    Micro-batch losses (~25-45) within 5e-3 relative of the reference's fp32 run
+    (achieved <= 2.7e-3 on MI355X: a 2-layer H=32 BERT, where one bf16 rounding is
+    a larger share of each feature; at the C2 shapes the bf16 step's loss is
+    within 1.2e-5 of fp32 mode, tests/test_configs_gpu.py)."""
     fx, losses, model = _replay(gpu, "bf16")
-    np.testing.assert_allclose(losses, fx["mb_loss"], rtol=3e-2)
+    rel = np.abs(losses - fx["mb_loss"]) / np.abs(fx["mb_loss"])
+    print("bf16 trajectory: per-micro-batch loss rel err", " ".join(f"{r:.1e}" for r in rel))
+    np.testing.assert_allclose(losses, fx["mb_loss"], rtol=5e-3)
 
 
 def test_train_pipelined_bert_prefetch_matches_sequential(gpu):
