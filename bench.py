@@ -315,23 +315,27 @@ def _lstm_flops_per_pair(cfg):
     return 4 * per_tok * TRAIN_L  # q fwd+bwd (3x) + k fwd (1x)
 
 
-def cpu_baseline_train(model, budget_s):
-    from oracle import bench_cpu
+def cpu_baseline_train(model, steps):
+    """The reference's step restated with the same torch CPU ops (nn.LSTM, matmul,
+    cross_entropy, HF BERT math, torch.optim.Adam) at the C2 shapes and B = 256
+    (oracle/torch_cpu_step.py), on the host's torch threads."""
+    from oracle import torch_cpu_step
 
     cfgb = model.bert_model.config
-    bert_w = {k: v.detach().float().cpu().numpy() for k, v in model.bert_model.state_dict().items()}
-    hp = {n: model.encoder_q.view(n).cpu().numpy() for n, _ in model.encoder_q.specs}
-    queue = model.queue.detach().cpu().numpy()
-    n_pairs = 4
-    ids, mask = synthetic_batch(2 * n_pairs, TRAIN_L, 99)
-    v, reps = bench_cpu.train_step_baseline(
-        bert_w, cfgb.num_hidden_layers, cfgb.num_attention_heads, hp,
-        model.encoder_q.num_layers, queue, ids.numpy(), mask.numpy(), budget_s=budget_s)
-    return {"value": v, "unit": "pairs/s", "cores": _blas_threads(), "kind": "port",
-            "cpu_model": _cpu_model(),
-            "sample": f"{reps} x one training micro-batch of {n_pairs} pairs at the C2 shapes "
-                      f"(BERT-base L={TRAIN_L}, 3-layer BiLSTM 768->256->128, queue 12544), "
-                      "numpy fp32 oracle"}
+    bert_w = {k: v.detach().float().cpu() for k, v in model.bert_model.state_dict().items()}
+    head = model.encoder_q
+    hs = {k: v.cpu() for k, v in head.state_dict().items()}
+    dims = (head.input_size, head.hidden, head.num_layers, head.output_size)
+    ids, mask = synthetic_batch(2 * TRAIN_B, TRAIN_L, 99)
+    v, sec = torch_cpu_step.train_step_baseline(
+        bert_w, cfgb.num_hidden_layers, cfgb.num_attention_heads, hs, dims,
+        model.queue.detach().cpu(), ids, mask, steps=steps)
+    return {"value": v, "unit": "pairs/s", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu_model": _cpu_model(), "s_per_step": sec,
+            "sample": f"{steps} reference training steps of {TRAIN_B} pairs at the C2 shapes "
+                      f"(BERT-base L={TRAIN_L} frozen, nn.LSTM 768->256x2 x3 + Linear 128, "
+                      "queue 12544, clip + Adam + momentum + enqueue) in torch CPU ops, after "
+                      "a 4-pair warm-up"}
 
 
 def _filter_kernel_name(q, d, dtype):
@@ -494,18 +498,18 @@ def run_sparse(args, dev, cpu_baseline):
 
 
 def cpu_baseline_scan(budget_s):
-    from oracle import bench_cpu
+    from oracle import torch_cpu_step
 
     g = torch.Generator().manual_seed(2024)
     d = torch.nn.functional.normalize(torch.randn(SCAN_N_PER_GPU, SCAN_D, generator=g))
     gq = torch.Generator().manual_seed(7)
     q = torch.nn.functional.normalize(torch.randn(SCAN_Q, SCAN_D, generator=gq))
-    v, reps = bench_cpu.scan_baseline(q.bfloat16().float().numpy(), d.bfloat16().float().numpy(),
-                                      SCAN_K, budget_s)
-    return {"value": v, "unit": "queries/s", "cores": _blas_threads(), "kind": "port",
+    v, reps = torch_cpu_step.scan_baseline(q.bfloat16().float(), d.bfloat16().float(), SCAN_K,
+                                           budget_s)
+    return {"value": v, "unit": "queries/s", "cores": torch.get_num_threads(), "kind": "port",
             "cpu_model": _cpu_model(),
             "sample": f"{reps} x full C2 batch (Q={SCAN_Q}, N={SCAN_N_PER_GPU}, D={SCAN_D}, "
-                      f"k={SCAN_K}), numpy fp32 BLAS + exact top-k"}
+                      f"k={SCAN_K}): torch CPU fp32 matmul over 64k-doc chunks + topk merge"}
 
 
 def _free_port():
@@ -538,6 +542,7 @@ def main():
     ap.add_argument("--part", default="all", choices=["all", "train", "scan", "scan_c2", "bert"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--cpu-steps", type=int, default=2)
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -573,7 +578,7 @@ def main():
     cpu_t = cpu_s = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if train is not None:
-            cpu_t = cpu_baseline_train(model, args.cpu_budget)
+            cpu_t = cpu_baseline_train(model, args.cpu_steps)
         if scan is not None:
             cpu_s = cpu_baseline_scan(args.cpu_budget)
     if scan is not None:

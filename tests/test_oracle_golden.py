@@ -238,3 +238,22 @@ def test_bert_base_12_layers_matches_reference():
     hs = O.bert_forward(g["input_ids"], g["attention_mask"], w, cfg["num_hidden_layers"],
                         cfg["num_attention_heads"])
     np.testing.assert_allclose(hs, g["last_hidden_state"], rtol=1e-4, atol=1e-4)
+
+
+def test_torch_cpu_baseline_restatement_matches_reference():
+    """The timed torch-CPU baseline (oracle/torch_cpu_step.py) computes the
+    reference's numbers: BERT vs the HF golden, NCELoss vs the reference golden."""
+    import torch
+
+    from oracle import torch_cpu_step as T
+
+    g = load_golden("bert_tiny.npz")
+    w = {k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("w_")}
+    hs = T.bert_forward(w, torch.from_numpy(g["input_ids"]), torch.from_numpy(g["attention_mask"]),
+                        int(g["cfg"][2]), int(g["cfg"][3]))
+    np.testing.assert_allclose(hs.numpy(), g["last_hidden_state"], rtol=1e-4, atol=1e-5)
+    n = load_golden("nce.npz")
+    tag = "n32_d128_k512_q"
+    loss = T.nce_loss(torch.from_numpy(n[f"{tag}_q"]), torch.from_numpy(n[f"{tag}_k"]),
+                      torch.from_numpy(n[f"{tag}_queue"]), 0.05)
+    assert abs(loss.item() - float(n[f"{tag}_loss"])) <= 1e-5 * float(n[f"{tag}_loss"])
