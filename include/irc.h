@@ -287,6 +287,27 @@ int irc_colsum_batched(int dtype, const void* x, int64_t batch, int64_t R, int64
                        int64_t sx, float* out, int64_t so, int accumulate, float* partial,
                        int64_t partial_floats, irc_stream_t stream);
 
+/* ------------------------------------------------- input pipeline (csrc/wordpiece.hip)
+ * BERT WordPiece tokenisation + joint padding on the device: replaces the
+ * reference's per-micro-batch host call bert_tokenizer(d1 + d2, padding=True,
+ * truncation=True) (src/contrastor/contrastive_module.py:36-41, 96-100).
+ * irc_wordpiece: n sentences as UTF-8 bytes (offsets int64 [n+1]); cmap uint32
+ *   [0x110000] (normaliser output per code point: kind 0 drop, 1 single cp << 8,
+ *   2 (pool offset << 8 | len << 2)), cpool uint32, cls uint8 [0x110000]
+ *   (1 whitespace, 2 punctuation); vocab as an open-addressing FNV-1a table
+ *   (htab_id int32 / htab_hash uint32, power-of-two size) with the pieces' code
+ *   points (vocab_off int32 [V+1], vocab_cps uint32, vocab_cont uint8 [V]) ->
+ *   tok int32 [n][max_tokens], tok_len int32 [n], *max_len = max row length + 2.
+ * irc_wordpiece_pad: ids / mask int64 [n][L] = [CLS] tokens [SEP] [PAD]... */
+int irc_wordpiece(const void* bytes, const int64_t* offsets, int64_t n, const void* cmap,
+                  const void* cpool, const void* cls, const int* htab_id, const void* htab_hash,
+                  int64_t htab_size, const int* vocab_off, const void* vocab_cps,
+                  const void* vocab_cont, int64_t max_piece, int64_t unk_id, int64_t max_tokens,
+                  int* tok, int* tok_len, int* max_len, irc_stream_t stream);
+int irc_wordpiece_pad(const int* tok, const int* tok_len, int64_t n, int64_t max_tokens,
+                      int64_t L, int64_t cls_id, int64_t sep_id, int64_t pad_id, int64_t* ids,
+                      int64_t* mask, irc_stream_t stream);
+
 /* ------------------------------------------------------------------ profiling
  * HIP-event timing of the dominant kernel of each entry point, recorded on the
  * caller's stream (bench.py's roofline "achieved" figure), with the launches'

@@ -88,6 +88,8 @@ SIGNATURES = {
     "irc_colsum": (I32, [I32, P, P, I64, I64, I64, I32, P, P]),
     "irc_colsum_batched_workspace": (I64, [I64, I64, I64]),
     "irc_colsum_batched": (I32, [I32, P, I64, I64, I64, I64, I64, P, I64, I32, P, I64, P]),
+    "irc_wordpiece": (I32, [P, P, I64, P, P, P, P, P, I64, P, P, P, I64, I64, I64, P, P, P, P]),
+    "irc_wordpiece_pad": (I32, [P, P, I64, I64, I64, I64, I64, I64, P, P, P]),
     "irc_prof_enable": (I32, [I32]),
     "irc_prof_query": (I32, [_c.c_char_p, _c.POINTER(_c.c_double), _c.POINTER(I64),
                              _c.POINTER(_c.c_double)]),

@@ -1,0 +1,196 @@
+"""GPU WordPiece tokenisation + joint padding.
+
+Drop-in for the reference's per-micro-batch host call
+``bert_tokenizer(texts, padding=True, truncation=True, return_tensors='pt')``
+(src/contrastor/contrastive_module.py:36-41, 96-100): the host only joins the
+sentences' UTF-8 bytes; normalisation, pre-tokenisation, WordPiece and padding
+run in csrc/wordpiece.hip (irc_wordpiece / irc_wordpiece_pad).
+
+The device tables are derived from the tokenizer object itself, so the result
+is the tokenizer's, character for character:
+  * cmap / cpool: the BertNormalizer's output for every code point (it acts per
+    character: clean text, CJK spacing, NFD + accent strip, lowercase);
+  * cls: whitespace / punctuation as the BertPreTokenizer splits them;
+  * the vocab as an open-addressing FNV-1a table over code points, pieces
+    stored without their "##" (continuation flag kept separately).
+Building cmap / cls calls the tokenizer's Rust normaliser and pre-tokeniser once
+per code point (~4 s); the result is cached in the temp directory, keyed by the
+tokenizers version and the normaliser / pre-tokeniser configuration.
+
+Not reproduced: special-token strings typed literally in the input text
+("[SEP]" inside a sentence), which the host tokenizer matches before
+normalisation; they are tokenised as ordinary text here.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import tempfile
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._torch import ptr, stream_ptr
+
+N_CP = 0x110000
+FNV_P = 16777619
+SEED_WORD = 2166136261
+SEED_CONT = 0x9E3779B9
+MAXW = 100
+MAXP = 64
+
+
+def _fnv(seed, cps):
+    h = seed
+    for c in cps:
+        h = ((h ^ c) * FNV_P) & 0xFFFFFFFF
+    return h
+
+
+def _char_tables(backend):
+    """(cmap uint32 [N_CP], cpool uint32, cls uint8 [N_CP]) from the tokenizer."""
+    import tokenizers
+
+    norm, pre = backend.normalizer, backend.pre_tokenizer
+    key = json.dumps([tokenizers.__version__, str(norm.__getstate__()),
+                      str(pre.__getstate__())])
+    tag = hashlib.sha1(key.encode()).hexdigest()[:16]
+    path = os.path.join(tempfile.gettempdir(), f"irc_wordpiece_chars_{tag}.npz")
+    if os.path.exists(path):
+        with np.load(path, allow_pickle=False) as z:  # our own cache file
+            return z["cmap"], z["cpool"], z["cls"]
+    cmap = np.zeros(N_CP, np.uint32)
+    cls = np.zeros(N_CP, np.uint8)
+    pool = []
+    for c in range(N_CP):
+        if 0xD800 <= c < 0xE000:
+            continue
+        ch = chr(c)
+        out = norm.normalize_str(ch)
+        if len(out) == 1:
+            cmap[c] = (ord(out) << 8) | 1
+        elif len(out) > 1:
+            if len(out) > 15:
+                raise ValueError(f"normaliser maps U+{c:04X} to {len(out)} characters")
+            cmap[c] = (len(pool) << 8) | (len(out) << 2) | 2
+            pool.extend(ord(o) for o in out)
+        pieces = pre.pre_tokenize_str("a" + ch + "a")
+        if len(pieces) == 2 and [p[0] for p in pieces] == ["a", "a"]:
+            cls[c] = 1
+        elif len(pieces) == 3 and pieces[1][0] == ch:
+            cls[c] = 2
+    cpool = np.array(pool if pool else [0], np.uint32)
+    tmp = path + f".{os.getpid()}.npz"
+    np.savez(tmp, cmap=cmap, cpool=cpool, cls=cls)
+    os.replace(tmp, path)
+    return cmap, cpool, cls
+
+
+def _vocab_tables(vocab: dict, prefix: str):
+    """Open-addressing table (size 4V rounded up to a power of two) of the
+    pieces' code points, continuation pieces keyed with their own seed."""
+    V = max(vocab.values()) + 1
+    pieces = [None] * V
+    for tok, i in vocab.items():
+        pieces[i] = tok
+    voff = np.zeros(V + 1, np.int32)
+    vcont = np.zeros(V, np.uint8)
+    cps = []
+    for i, tok in enumerate(pieces):
+        tok = tok or ""
+        cont = tok.startswith(prefix) and len(tok) > len(prefix)
+        body = tok[len(prefix):] if cont else tok
+        vcont[i] = cont
+        cps.extend(ord(ch) for ch in body)
+        voff[i + 1] = len(cps)
+    size = 1
+    while size < 4 * V:
+        size <<= 1
+    hid = np.full(size, -1, np.int32)
+    hh = np.zeros(size, np.uint32)
+    max_piece = 1
+    for i in range(V):
+        body = cps[voff[i]:voff[i + 1]]
+        if not body:
+            continue
+        if len(body) > MAXP:
+            continue  # longer than any word the GPU matches (MAXW caps words at 100)
+        max_piece = max(max_piece, len(body))
+        h = _fnv(SEED_CONT if vcont[i] else SEED_WORD, body)
+        j = h & (size - 1)
+        while hid[j] >= 0:
+            j = (j + 1) & (size - 1)
+        hid[j], hh[j] = i, h
+    return hid, hh, voff, np.array(cps if cps else [0], np.uint32), vcont, max_piece
+
+
+class GpuWordPiece:
+    """``__call__(texts) -> (input_ids, attention_mask)`` int64 [n, L] on the
+    device, equal to the host tokenizer's padding=True, truncation=True output
+    (max_length = min(tokenizer.model_max_length, 512), the reference's
+    bert-base-uncased limit)."""
+
+    def __init__(self, hf_tokenizer, device, max_length: int | None = None):
+        be = hf_tokenizer.backend_tokenizer
+        model = be.model
+        if type(model).__name__ != "WordPiece":
+            raise ValueError("GpuWordPiece needs a WordPiece tokenizer")
+        if int(model.max_input_chars_per_word) != MAXW:
+            raise ValueError("max_input_chars_per_word != 100")
+        self.device = torch.device(device)
+        ml = max_length or min(int(hf_tokenizer.model_max_length), 512)
+        self.max_tokens = ml - 2
+        vocab = hf_tokenizer.get_vocab()
+        self.unk = vocab[model.unk_token]
+        self.cls_id = hf_tokenizer.cls_token_id
+        self.sep_id = hf_tokenizer.sep_token_id
+        self.pad_id = hf_tokenizer.pad_token_id
+        cmap, cpool, cls = _char_tables(be)
+        hid, hh, voff, vcps, vcont, self.max_piece = _vocab_tables(
+            vocab, model.continuing_subword_prefix)
+        up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.device)  # noqa: E731
+        self._t = {"cmap": up(cmap.view(np.int32)), "cpool": up(cpool.view(np.int32)),
+                   "cls": up(cls), "hid": up(hid), "hh": up(hh.view(np.int32)),
+                   "voff": up(voff), "vcps": up(vcps.view(np.int32)), "vcont": up(vcont)}
+        self.hsize = hid.shape[0]
+        # high priority: its few waves are dispatched ahead of the training step's
+        # GEMM workgroups queued on the other streams (the host waits on it)
+        self.stream = torch.cuda.Stream(self.device, priority=-1)
+        self._max_len = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._host_len = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+
+    def __call__(self, texts):
+        texts = list(texts)
+        n = len(texts)
+        enc = [t.encode("utf-8") for t in texts]
+        offs = np.zeros(n + 1, np.int64)
+        np.cumsum([len(e) for e in enc], out=offs[1:])
+        blob = np.frombuffer(b"".join(enc) or b"\0", np.uint8)
+        cur = torch.cuda.current_stream(self.device)
+        st = self.stream  # independent of the compute in flight on `cur`: no wait
+        with torch.cuda.stream(st):
+            b = torch.from_numpy(blob.copy()).pin_memory().to(self.device, non_blocking=True)
+            o = torch.from_numpy(offs).pin_memory().to(self.device, non_blocking=True)
+            tok = torch.empty((max(n, 1), max(self.max_tokens, 1)), dtype=torch.int32,
+                              device=self.device)
+            tlen = torch.empty((max(n, 1),), dtype=torch.int32, device=self.device)
+            t = self._t
+            _lib.call("irc_wordpiece", ptr(b), ptr(o), n, ptr(t["cmap"]), ptr(t["cpool"]),
+                      ptr(t["cls"]), ptr(t["hid"]), ptr(t["hh"]), self.hsize, ptr(t["voff"]),
+                      ptr(t["vcps"]), ptr(t["vcont"]), self.max_piece, self.unk,
+                      self.max_tokens, ptr(tok), ptr(tlen), ptr(self._max_len), stream_ptr(st))
+            self._host_len.copy_(self._max_len, non_blocking=True)
+            st.synchronize()  # this stream only: the tokenizer's own work
+            L = max(int(self._host_len[0]), 2)
+            ids = torch.empty((n, L), dtype=torch.int64, device=self.device)
+            mask = torch.empty((n, L), dtype=torch.int64, device=self.device)
+            _lib.call("irc_wordpiece_pad", ptr(tok), ptr(tlen), n, self.max_tokens, L, self.cls_id,
+                      self.sep_id, self.pad_id, ptr(ids), ptr(mask), stream_ptr(st))
+        cur.wait_stream(st)
+        for x in (ids, mask):
+            x.record_stream(cur)
+        for x in (b, o, tok, tlen):
+            x.record_stream(st)
+        return ids, mask

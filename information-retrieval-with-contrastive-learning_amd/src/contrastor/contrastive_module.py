@@ -21,6 +21,7 @@ tokenisation as bert_extract), so there is no separate frozen ``bert_model``
 momentum copy, and the loss / queue / enqueue tail is shared with the LSTM path.
 """
 import copy
+import os
 
 import torch
 import torch.nn as nn
@@ -32,6 +33,7 @@ from irc_amd.bert import BertModel
 from irc_amd.bert_train import BertEncoder, seq2vec_ids
 from irc_amd.lstm_head import LSTMHead, seq2vec as head_seq2vec
 from irc_amd.tokenizer import load_tokenizer
+from irc_amd.wordpiece import GpuWordPiece
 
 
 class RetrievalModelWrapper(nn.Module):
@@ -73,12 +75,12 @@ class RetrievalModelWrapper(nn.Module):
         self.bert_tokenizer = load_tokenizer(bc.get("vocab"), vocab_size)
         # data-parallel group for global in-batch negatives (None: single process)
         self.dist_group = None
+        self._gpu_tokenizers = {}  # device -> GpuWordPiece (built on first use)
 
     @torch.no_grad()
     def bert_extract(self, d1, d2, device):
-        t = self.bert_tokenizer(list(d1) + list(d2), padding=True, truncation=True,
-                                return_tensors="pt")
-        out = self.bert_model.encode(t["input_ids"].to(device), t["attention_mask"].to(device))
+        ids, mask = self.tokenize(list(d1) + list(d2), device)
+        out = self.bert_model.encode(ids, mask)
         return out[:len(d1)], out[len(d1):]
 
     @torch.no_grad()
@@ -143,6 +145,15 @@ class RetrievalModelWrapper(nn.Module):
             ops.enqueue(self.queue, keys.float().contiguous(), self.queue_ptr)
 
     def tokenize(self, texts, device):
+        """bert_tokenizer(texts, padding=True, truncation=True) as device tensors.
+        On a HIP device the WordPiece + joint padding run on the GPU
+        (irc_amd.wordpiece; IRC_TOKENIZER=host keeps the host tokenizer)."""
+        device = torch.device(device)
+        if device.type == "cuda" and os.environ.get("IRC_TOKENIZER", "gpu") != "host":
+            wp = self._gpu_tokenizers.get(device)
+            if wp is None:
+                wp = self._gpu_tokenizers[device] = GpuWordPiece(self.bert_tokenizer, device)
+            return wp(texts)
         t = self.bert_tokenizer(list(texts), padding=True, truncation=True, return_tensors="pt")
         return t["input_ids"].to(device), t["attention_mask"].to(device)
 

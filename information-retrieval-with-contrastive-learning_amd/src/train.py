@@ -201,11 +201,14 @@ def train(args):
                             positive_sample=positive_sample):
                         return model(anchor_sample, positive_sample, args.device,
                                      cluster_result, indexes)
-                _, stepped = st.micro_batch(len(indexes), fwd)
+                _, stepped = st.micro_batch(len(indexes), fwd, sync_loss=False)
                 if stepped:
                     pbar.update(1)
                     if st.step_sum % log_step == 0:
-                        loss_avg = float(np.mean(st.loss_record))
+                        # the per-micro-batch losses stay on the device until here (the
+                        # reference syncs loss.item() every micro-batch, train.py:148;
+                        # the logged mean is the same number)
+                        loss_avg = float(np.mean([float(x) for x in st.loss_record]))
                         st.loss_record = []
                         grad_norm = float(st.grad_norm[0].item())
                         st.check_faults()
