@@ -131,7 +131,9 @@ def c2_config():
     return cfg
 
 
-def run_train(args, rank, world, dev):
+def run_train(args, rank, world, dev, weights="bf16"):
+    """weights "fp8": config C5 -- the frozen encoder's nn.Linear layers on e4m3
+    (irc_gemm_fp8, per-channel weight / per-token input scales); same step."""
     from irc_amd import _lib
     from src.model import build_model, get_optimizer
     from src.train import TrainState
@@ -142,6 +144,8 @@ def run_train(args, rank, world, dev):
                             sample="uniform")
     torch.manual_seed(1337)
     model = build_model(ns).to(dev).train()
+    model.bert_model.set_weight_format(weights)
+    gname, gpeak = ("gemm_fp8", FP8_PEAK_TFS) if weights == "fp8" else ("gemm_bf16", BF16_PEAK_TFS)
     model.add_queue_to_loss = True  # steady state (step >= queue_start_steps)
     opt = get_optimizer(ns, model)
     st = TrainState(ns, model, opt)
@@ -178,7 +182,7 @@ def run_train(args, rank, world, dev):
     dt = time.perf_counter() - t0
     lib.irc_prof_enable(0)
     dt = _max_over_ranks(dt, dev, world)
-    live_s, live_n, live_flops = _prof(lib, "gemm_bf16")
+    live_s, live_n, live_flops = _prof(lib, gname)
     # Kernel efficiency: the same steps once more, serialised (BERT features and
     # every side-stream launch on the current stream, no prefetch), so concurrent
     # streams do not stretch the GEMM launches' event durations; the overlapped
@@ -195,7 +199,7 @@ def run_train(args, rank, world, dev):
                 *model.bert_extract_ids(ids, mask, TRAIN_B)), sync_loss=False)
         torch.cuda.synchronize()
     lib.irc_prof_enable(0)
-    g_s, g_n, g_flops = _prof(lib, "gemm_bf16")
+    g_s, g_n, g_flops = _prof(lib, gname)
     flops_pair = 2 * model.bert_model.flops_per_sequence(TRAIN_L) + _lstm_flops_per_pair(cfg)
     pairs = TRAIN_B * args.steps * world
     achieved = g_flops / g_s / 1e12 if g_s > 0 else None
@@ -206,13 +210,16 @@ def run_train(args, rank, world, dev):
         "loss_last": loss,
         "flops_per_pair": flops_pair,
         "step_tflops": pairs * flops_pair / dt / 1e12,
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS,
-                     "unit": "TFLOP/s", "frac": achieved / BF16_PEAK_TFS if achieved else None,
-                     "traffic": _pmc_traffic("gemm_bf16"),
-                     "traffic_source": _pmc_source("gemm_bf16"),
-                     "kernel": "bf16 GEMM kernels (gemm_big_kernel / gemm_pp_kernel / "
-                               "gemm_kernel; all GEMM launches of a single-stream pass of "
-                               "the same steps)",
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": gpeak,
+                     "unit": "TFLOP/s", "frac": achieved / gpeak if achieved else None,
+                     "traffic": _pmc_traffic(gname) if weights == "bf16" else None,
+                     "traffic_source": _pmc_source(gname) if weights == "bf16" else None,
+                     "kernel": ("bf16 GEMM kernels (gemm_big_kernel / gemm_pp_kernel / "
+                                "gemm_kernel; all GEMM launches of a single-stream pass of "
+                                "the same steps)") if weights == "bf16" else
+                               ("e4m3 GEMM (gemm_pp_kernel F8, v_mfma_scale_f32_16x16x128_"
+                                "f8f6f4) of the frozen encoder's linear layers, single-stream "
+                                "pass; the heads' bf16 GEMMs are not in this figure"),
                      "launches_per_step": g_n / args.steps,
                      "gemm_ms_per_step": g_s * 1e3 / args.steps,
                      "alg_flops_per_step": g_flops / args.steps,
@@ -539,7 +546,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--part", default="all", choices=["all", "train", "scan", "scan_c2", "bert"])
+    ap.add_argument("--part", default="all",
+                    choices=["all", "train", "train_fp8", "scan", "scan_c2", "bert"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -562,6 +570,10 @@ def main():
     model = None
     if args.part in ("all", "train"):
         model, train = run_train(args, rank, world, dev)
+    train8 = None
+    if args.part in ("all", "train_fp8"):
+        _, train8 = run_train(args, rank, world, dev, weights="fp8")
+        torch.cuda.empty_cache()
     bert = None
     if args.part in ("all", "bert"):
         bert = run_train_bert(args, rank, world, dev)
@@ -592,6 +604,10 @@ def main():
             head = {"value": train["pairs_per_s"], "unit": "pairs/s",
                     "ms_per_step": train["ms_per_step"], "roofline": train["roofline"],
                     "cpu_baseline": cpu_t}
+        elif train8 is not None:
+            head = {"value": train8["pairs_per_s"], "unit": "pairs/s",
+                    "ms_per_step": train8["ms_per_step"], "roofline": train8["roofline"],
+                    "cpu_baseline": None}
         elif bert is not None:
             head = {"value": bert["pairs_per_s"], "unit": "pairs/s",
                     "ms_per_step": bert["ms_per_step"], "roofline": bert["roofline"],
@@ -619,6 +635,10 @@ def main():
                                                    "flops_per_pair", "loss_last")}
         if bert is not None:
             line["train_bert"] = bert
+        if train8 is not None:
+            line["train_fp8"] = dict(train8, workload=(
+                "C5: fp8 (e4m3) frozen-encoder weights, d=768: the C2 step with every BERT-base "
+                "nn.Linear on irc_gemm_fp8 (per-channel weight / per-token input scales)"))
         if scan is not None:
             line["retrieval"] = scan
         if scan_c4 is not None:

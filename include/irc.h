@@ -287,6 +287,20 @@ int irc_colsum_batched(int dtype, const void* x, int64_t batch, int64_t R, int64
                        int64_t sx, float* out, int64_t so, int accumulate, float* partial,
                        int64_t partial_floats, irc_stream_t stream);
 
+/* ------------------------------------------------- fp8 encoder weights (csrc/fp8_linear.hip)
+ * BASELINE config C5 ("fp8 (CDNA4 MFMA) encoder weights"): the frozen BERT's
+ * nn.Linear layers (contrastive_module.py:36-41 -> HF modeling_bert) on e4m3.
+ * irc_quantize_rows_fp8: x bf16 (in_dtype 0) / fp32 (1) [M][ldx] -> out e4m3
+ *   [M][ldo], scale[m] = amax|x[m]| / 448 (1 for a zero row), out = e4m3(RNE(x /
+ *   scale)) saturated; used per output channel for weights, per token for inputs.
+ * irc_gemm_fp8: C bf16 [M][ldc] = (A8 [M][lda] . B8 [N][ldb]^T) * sa[m] * sb[n]
+ *   (+ bias) (epi 1) / -> GELU (2) / + residual R bf16 [M][ldr] (3); K % 128 == 0. */
+int irc_quantize_rows_fp8(int in_dtype, const void* x, int64_t ldx, int64_t M, int64_t K,
+                          void* out, int64_t ldo, float* scale, irc_stream_t stream);
+int irc_gemm_fp8(const void* A8, int64_t lda, const float* sa, const void* B8, int64_t ldb,
+                 const float* sb, int64_t M, int64_t N, int64_t K, const float* bias,
+                 const void* R, int64_t ldr, void* C, int64_t ldc, int epi, irc_stream_t stream);
+
 /* ------------------------------------------------- input pipeline (csrc/wordpiece.hip)
  * BERT WordPiece tokenisation + joint padding on the device: replaces the
  * reference's per-micro-batch host call bert_tokenizer(d1 + d2, padding=True,

@@ -28,6 +28,10 @@ struct PArgs {
   int qpad;
   int stride;
   uint32_t idx_base;
+  // fp8 linear layers (F8, non-scan epilogues): C = alpha * (A8 . B8^T) * sa[row]
+  // * sb[col] (+ bias ...): per-row dequantisation scales of both e4m3 operands
+  const float* sa;
+  const float* sb;
 };
 
 constexpr int EPI_SCAN = 7;
@@ -42,6 +46,9 @@ void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, in
 void run_scan(const PArgs& a, hipStream_t st, bool fp8 = false);
 // raw fp32 C = A . B^T of e4m3 operands (K, lda, ldb in 2-byte units; vec_c layout)
 void run_scores_fp8(const PArgs& a, hipStream_t st);
+// e4m3 linear layer: bf16 C = (A8 . B8^T) * sa[m] * sb[n] (+ bias / GELU / residual);
+// both operands K-major, K / lda / ldb in 2-byte units, vec_c layout required
+void run_fp8(int epi, const PArgs& a, hipStream_t st);
 
 }  // namespace gpp
 }  // namespace irc

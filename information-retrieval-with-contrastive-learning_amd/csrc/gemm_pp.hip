@@ -415,6 +415,23 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
       bv[j] = (!slab && has_bias(EPI) && col < g.N) ? bias[col] : 0.f;
     }
     const float alpha = slab ? 1.f : g.alpha;
+    // fp8 linear layers: per-row (A) and per-column (B) dequantisation scales
+    float sbv[4] = {1.f, 1.f, 1.f, 1.f};
+    float sav[8][4];
+    if constexpr (F8) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = cbase + 16 * j + (lane & 15);
+        sbv[j] = (g.sb != nullptr && col < g.N) ? g.sb[col] : 1.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = rbase0 + 16 * i + 4 * (lane >> 4) + e;
+          sav[i][e] = (g.sa != nullptr && row < g.M) ? g.sa[row] : 1.f;
+        }
+    }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {  // 32-row passes
 #pragma unroll
@@ -423,7 +440,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
         for (int j = 0; j < 4; ++j) {
           f32x2 v[2];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * alpha + bv[j];
+          for (int e = 0; e < 4; ++e) {
+            if constexpr (F8)
+              v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * (alpha * sav[2 * p + ii][e] * sbv[j]) +
+                                 bv[j];
+            else
+              v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * alpha + bv[j];
+          }
           if (!slab && EPI == EPI_BIAS_GELU) {
             v[0] = gelu_f2(v[0]);
             v[1] = gelu_f2(v[1]);
@@ -619,6 +642,20 @@ void run_scores_fp8(const PArgs& a, hipStream_t st) {
   const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
   hipLaunchKernelGGL((gemm_pp_kernel<true, true, float, EPI_NONE, true>), dim3((unsigned)tiles),
                      dim3(NT), 0, st, a);
+}
+
+void run_fp8(int epi, const PArgs& a, hipStream_t st) {
+  const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
+  const dim3 grid((unsigned)tiles);
+  switch (epi) {
+#define IRC_PP8(E)                                                                          \
+  case E:                                                                                   \
+    hipLaunchKernelGGL((gemm_pp_kernel<true, true, unsigned short, E, true>), grid, dim3(NT), \
+                       0, st, a);                                                           \
+    break;
+    IRC_PP8(0) IRC_PP8(1) IRC_PP8(2) IRC_PP8(3)
+#undef IRC_PP8
+  }
 }
 
 template <typename TO>

@@ -145,6 +145,9 @@ class BertModel(nn.Module):
         self.pooler = _Pooler(config.hidden_size)  # kept for checkpoint compatibility
         self._init_weights(seed)
         self._cache = {}
+        # "bf16" (default) or "fp8": e4m3 weights (per output channel scales) and
+        # per-token e4m3 inputs for every nn.Linear of the frozen encoder (config C5)
+        self.weight_format = os.environ.get("IRC_ENCODER_WEIGHTS", "bf16")
         self.eval()
 
     # HF _init_weights: normal(0, 0.02) for Linear/Embedding, padding row 0, LN (1, 0)
@@ -190,14 +193,27 @@ class BertModel(nn.Module):
         self._cache = {}
         return super().load_state_dict(*a, **k)
 
+    def set_weight_format(self, fmt: str):
+        if fmt not in ("bf16", "fp8"):
+            raise ValueError(f"weight format must be 'bf16' or 'fp8', got {fmt!r}")
+        self.weight_format = fmt
+        self._cache = {}
+
+    def _fp8_mode(self):
+        return self.weight_format == "fp8" and compute_dtype() == torch.bfloat16
+
     def _weights(self):
         dt = compute_dtype()
-        key = (dt, self.embeddings.word_embeddings.weight.device)
+        fp8 = self._fp8_mode()
+        key = (dt, fp8, self.embeddings.word_embeddings.weight.device)
         w = self._cache.get(key)
         if w is not None:
             return w
         cast = (lambda t: t.detach().to(dt).contiguous())
         f32 = (lambda t: t.detach().float().contiguous())
+        castw = cast
+        if fp8:  # linear weights: (e4m3 bytes, per-output-channel scales) of the fp32 weight
+            castw = (lambda t: ops.quantize_rows_fp8(t.detach().float().contiguous()))  # noqa: E731
         e = self.embeddings
         w = {"word": cast(e.word_embeddings.weight), "pos": cast(e.position_embeddings.weight),
              "type0": cast(e.token_type_embeddings.weight[0]), "ln_g": f32(e.LayerNorm.weight),
@@ -205,14 +221,14 @@ class BertModel(nn.Module):
         for lyr in self.encoder.layer:
             sa = lyr.attention.self
             w["layers"].append({
-                "wqkv": cast(torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0)),
+                "wqkv": castw(torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0)),
                 "bqkv": f32(torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0)),
-                "wo": cast(lyr.attention.output.dense.weight),
+                "wo": castw(lyr.attention.output.dense.weight),
                 "bo": f32(lyr.attention.output.dense.bias),
                 "ln1_g": f32(lyr.attention.output.LayerNorm.weight),
                 "ln1_b": f32(lyr.attention.output.LayerNorm.bias),
-                "w1": cast(lyr.intermediate.dense.weight), "b1": f32(lyr.intermediate.dense.bias),
-                "w2": cast(lyr.output.dense.weight), "b2": f32(lyr.output.dense.bias),
+                "w1": castw(lyr.intermediate.dense.weight), "b1": f32(lyr.intermediate.dense.bias),
+                "w2": castw(lyr.output.dense.weight), "b2": f32(lyr.output.dense.bias),
                 "ln2_g": f32(lyr.output.LayerNorm.weight), "ln2_b": f32(lyr.output.LayerNorm.bias),
             })
         self._cache = {key: w}
@@ -229,6 +245,8 @@ class BertModel(nn.Module):
             raise ValueError(f"sequence length {L} > max_position_embeddings")
         H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
         w = self._weights()
+        if self._fp8_mode():
+            return self._encode_fp8(ids, mask, w).view(B, L, H)
         x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
         for lw in w["layers"]:
             qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
@@ -239,6 +257,29 @@ class BertModel(nn.Module):
             x = ops.gemm(i, lw["w2"], bias=lw["b2"], residual=a, epilogue=ops.EPI_BIAS_RESID)
             x = ops.layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, out=x)
         return x.view(B, L, H)
+
+    def _encode_fp8(self, ids, mask, w):
+        """encode() with every nn.Linear on e4m3 (irc_gemm_fp8): the input rows are
+        quantised per token, the weights per output channel; embeddings, attention,
+        LayerNorm and the epilogues stay bf16 / fp32."""
+        c = self.config
+        B, L = ids.shape
+        H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
+        x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
+
+        def lin(inp, wq, bias, epi, residual=None):
+            aq, sa = ops.quantize_rows_fp8(inp)
+            return ops.gemm_fp8(aq, sa, wq[0], wq[1], bias=bias, epilogue=epi, residual=residual)
+
+        for lw in w["layers"]:
+            qkv = lin(x, lw["wqkv"], lw["bqkv"], ops.EPI_BIAS)
+            ctx = ops.attention(qkv, mask, B, L, H, heads)
+            a = lin(ctx, lw["wo"], lw["bo"], ops.EPI_BIAS_RESID, residual=x)
+            a = ops.layernorm(a, lw["ln1_g"], lw["ln1_b"], eps, out=a)
+            i = lin(a, lw["w1"], lw["b1"], ops.EPI_BIAS_GELU)
+            x = lin(i, lw["w2"], lw["b2"], ops.EPI_BIAS_RESID, residual=a)
+            x = ops.layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, out=x)
+        return x
 
     def forward(self, input_ids=None, attention_mask=None, **kw):
         if attention_mask is None:

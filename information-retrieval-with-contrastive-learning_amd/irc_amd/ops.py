@@ -463,3 +463,35 @@ def colsum_batched(x, out, out_stride, accumulate=True):
     ws = torch.empty((max(nws, 1),), dtype=F32, device=x.device)
     _lib.call("irc_colsum_batched", _code(x), ptr(x), nb, R, C, x.stride(1), x.stride(0), ptr(out),
               int(out_stride), 1 if accumulate else 0, ptr(ws), nws, stream_ptr(x.device))
+
+
+# ---- fp8 (e4m3) linear layers of the frozen encoder (csrc/fp8_linear.hip, config C5)
+def quantize_rows_fp8(x):
+    """x bf16 / fp32 [M, K] -> (e4m3 bytes uint8 [M, K], per-row fp32 scales [M]):
+    q = e4m3(RNE(x * 448 / amax_row)), scale = amax_row / 448."""
+    require_hip(x)
+    if x.dtype not in (BF16, F32):
+        raise TypeError(f"quantize_rows_fp8: bf16 or fp32 input, got {x.dtype}")
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    M, K = x.shape
+    q = torch.empty((M, K), dtype=torch.uint8, device=x.device)
+    s = torch.empty((M,), dtype=F32, device=x.device)
+    _lib.call("irc_quantize_rows_fp8", 0 if x.dtype == BF16 else 1, ptr(x), x.stride(0), M, K,
+              ptr(q), K, ptr(s), stream_ptr(x.device))
+    return q, s
+
+
+def gemm_fp8(aq, sa, bq, sb, bias=None, epilogue=EPI_NONE, residual=None):
+    """bf16 [M, N] = (aq . bq^T) * sa[:, None] * sb[None, :] (+ bias) (-> GELU)
+    (+ residual): aq [M, K], bq [N, K] e4m3 bytes with their row scales."""
+    require_hip(aq, sa, bq, sb, bias, residual)
+    M, K = aq.shape
+    N = bq.shape[0]
+    if bq.shape[1] != K:
+        raise ValueError(f"gemm_fp8 inner dims differ: {K} vs {bq.shape[1]}")
+    out = torch.empty((M, N), dtype=BF16, device=aq.device)
+    _lib.call("irc_gemm_fp8", ptr(aq), aq.stride(0), ptr(sa), ptr(bq), bq.stride(0), ptr(sb), M, N,
+              K, ptr(bias), ptr(residual), residual.stride(0) if residual is not None else 0,
+              ptr(out), out.stride(0), int(epilogue), stream_ptr(aq.device))
+    return out

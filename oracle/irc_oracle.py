@@ -146,6 +146,19 @@ def quantize_e4m3(x: np.ndarray, scale: float = 1.0) -> np.ndarray:
     return np.where(nan, np.uint8(0x7F), code).astype(np.uint8)
 
 
+def quantize_rows_e4m3(x: np.ndarray):
+    """Per-row e4m3 (BASELINE config C5 fp8 encoder weights; not in the reference,
+    which runs BERT in fp32): scale = amax|row| / 448 (1 for a zero row), codes =
+    RNE(row * (448 / amax)) in fp32 -- returns (codes uint8, scales float32)."""
+    x = np.asarray(x, dtype=F32)
+    amax = np.max(np.abs(x), axis=1).astype(F32)
+    inv = np.where(amax > 0, F32(448.0) / np.where(amax > 0, amax, F32(1)), F32(1)).astype(F32)
+    codes = np.stack([quantize_e4m3(x[i], inv[i]) for i in range(x.shape[0])]) if len(x) else \
+        np.zeros(x.shape, np.uint8)
+    scale = np.where(amax > 0, amax / F32(448.0), F32(1)).astype(F32)
+    return codes, scale
+
+
 def dequantize_e4m3(codes: np.ndarray) -> np.ndarray:
     return e4m3_decode_table()[np.asarray(codes, dtype=np.uint8)]
 
