@@ -37,6 +37,7 @@ import torch
 import torch.nn as nn
 
 from . import ops
+from ._torch import side_stream
 from .bert import BERT_BASE, PRESETS, BertConfig, BertModel
 from .precision import compute_dtype
 
@@ -105,6 +106,11 @@ class BertEncoder(nn.Module):
         self._shadow_t = None    # {name: bf16 transposed weight} (dX GEMM operands)
         self._shadow_ok = False
         self._shadow_t_ok = False
+        # data-parallel gradient reduction overlapped with the backward (set per
+        # micro-batch by TrainState.set_process_group's caller; None: no reduce)
+        self._reduce_group = None
+        self._reduce_works = []
+        self.reduce_bucket_layers = 4
         if init_from is not None:
             self.load_from_bert(init_from)
         else:
@@ -346,6 +352,17 @@ class BertEncoder(nn.Module):
         ds2s = torch.empty((nl, BL, H), dtype=dt, device=dev)
         dm = ops.l2norm_bwd(demb.float().contiguous(), emb, nrm)  # [B, H] fp32
         dy, bcast = dm, L  # top layer: the mean-pool backward folded into LN2's
+        # DP: buckets of reduce_bucket_layers layers, top bucket first; bucket_lo
+        # maps each bucket's lowest layer to its (exclusive) top
+        reduce_on = self._reduce_group is not None
+        nb = max(1, int(self.reduce_bucket_layers))
+        bucket_lo = {}
+        if reduce_on:
+            hi = nl
+            while hi > 0:
+                lo = max(0, hi - nb)
+                bucket_lo[lo] = hi
+                hi = lo
         for l in range(nl - 1, -1, -1):
             qkv, s1, u, s2 = layers[l]
             lw = w["layers"][l]
@@ -366,15 +383,11 @@ class BertEncoder(nn.Module):
             dqkv = ops.attention_bwd(qkv, mask, ctxs[l], dctx, B, L, H, heads, out=dqkvs[l])
             dy = self._dx_gemm(dqkv, lw["wqkv"], lw.get("wqkvT"), epilogue=ops.EPI_RESID,
                                residual=ds1)
-        # layer-batched weight / bias gradients
-        for dY, X, wname, bname in ((dqkvs, xs, "attention.self.query.weight",
-                                     "attention.self.query.bias"),
-                                    (ds1s, ctxs, "attention.output.dense.weight",
-                                     "attention.output.dense.bias"),
-                                    (dus, as_, "intermediate.dense.weight",
-                                     "intermediate.dense.bias"),
-                                    (ds2s, gs, "output.dense.weight", "output.dense.bias")):
-            self._wgrad_batched(dY, X, wname, bname)
+            if reduce_on and l in bucket_lo and l > 0:
+                self._bucket_wgrad_reduce(l, bucket_lo[l], acts, (dqkvs, ds1s, dus, ds2s))
+        # layer-batched weight / bias gradients (the layers not yet reduced)
+        lo_end = bucket_lo[0] if reduce_on else nl
+        self._wgrad_layers(0, lo_end, acts, (dqkvs, ds1s, dus, ds2s))
         # embeddings: LN backward on the rebuilt fp32 sum, then the table scatter
         e = ops.embed_sum(ids, w["word"], w["pos"], w["type0"])
         de = ops.layernorm_bwd(dy, e, w["ln_g"], self.view("embeddings.LayerNorm.weight", g),
@@ -383,6 +396,68 @@ class BertEncoder(nn.Module):
                       self.view("embeddings.position_embeddings.weight", g),
                       self.view("embeddings.token_type_embeddings.weight", g)[0],
                       c.pad_token_id)
+        if reduce_on:  # last bucket: embeddings + the bottom layers, on this stream
+            self._reduce_async(0, self._layer_start(lo_end))
+
+    # ---- data-parallel gradient all-reduce, bucketed and overlapped -------------
+    def set_grad_reduce(self, group):
+        """All-reduce (sum) flat_grad over ``group`` DURING the next backward, in
+        buckets of ``reduce_bucket_layers`` layers: once the dX chain has passed a
+        bucket's lowest layer, that bucket's weight gradients (one batched GEMM per
+        kind) and its RCCL all-reduce run on a side stream while the chain goes on
+        (the BERT-size gradient bucketed and overlapped with backward).
+        None: no reduction (a micro-batch that does not step)."""
+        self._reduce_group = group
+
+    def wait_grad_reduce(self):
+        """Make the current stream wait for the bucketed all-reduces."""
+        for work in self._reduce_works:
+            work.wait()
+        self._reduce_works = []
+
+    def _layer_start(self, l):
+        """Flat offset where layer l's parameters start (the end for l = nl)."""
+        c = self.config
+        if l >= c.num_hidden_layers:
+            return self.numel_flat
+        return self.offsets[f"encoder.layer.{l}.attention.self.query.weight"]
+
+    def _reduce_async(self, start, stop):
+        import torch.distributed as dist
+
+        self._reduce_works.append(dist.all_reduce(self.flat_grad.detach()[start:stop],
+                                                  op=dist.ReduceOp.SUM,
+                                                  group=self._reduce_group, async_op=True))
+
+    def _wgrad_layers(self, lo, hi, acts, grads):
+        xs, ctxs, as_, gs = acts
+        dqkvs, ds1s, dus, ds2s = grads
+        if hi <= lo:
+            return
+        for dY, X, wname, bname in ((dqkvs, xs, "attention.self.query.weight",
+                                     "attention.self.query.bias"),
+                                    (ds1s, ctxs, "attention.output.dense.weight",
+                                     "attention.output.dense.bias"),
+                                    (dus, as_, "intermediate.dense.weight",
+                                     "intermediate.dense.bias"),
+                                    (ds2s, gs, "output.dense.weight", "output.dense.bias")):
+            self._wgrad_batched(dY[lo:hi], X[lo:hi], wname, bname, first=lo)
+
+    def _bucket_wgrad_reduce(self, lo, hi, acts, grads):
+        """Layers [lo, hi): weight gradients + all-reduce of their flat slice (plus
+        everything above it for the top bucket) on the "grad_reduce" side stream."""
+        cur = torch.cuda.current_stream(self.flat_grad.device)
+        side = side_stream(self.flat_grad.device, "grad_reduce")
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self._wgrad_layers(lo, hi, acts, grads)
+            top = hi >= self.config.num_hidden_layers
+            self._reduce_async(self._layer_start(lo),
+                               self.numel_flat if top else self._layer_start(hi))
+        for t in list(acts) + list(grads):
+            t.record_stream(side)
+        # no join here: the dX chain goes on; wait_grad_reduce() joins through the
+        # all-reduce works (each enqueued behind its bucket's GEMMs on `side`)
 
     def _layer_stride(self, name):
         c = self.config
@@ -394,13 +469,14 @@ class BertEncoder(nn.Module):
                 self.offsets[f"encoder.layer.{l - 1}.{name}"] == st
         return st
 
-    def _wgrad_batched(self, dY, X, wname, bname):
-        """dW[l] += dY[l]^T X[l] and db[l] += colsum(dY[l]) for every layer l."""
+    def _wgrad_batched(self, dY, X, wname, bname, first=0):
+        """dW[l] += dY[l]^T X[l] and db[l] += colsum(dY[l]) for the layers
+        first .. first + len(dY) - 1."""
         g = self.flat_grad.detach()
         nl, BL, out_n = dY.shape
         in_n = X.shape[2]
-        ow = self.offsets[f"encoder.layer.0.{wname}"]
-        ob = self.offsets[f"encoder.layer.0.{bname}"]
+        ow = self.offsets[f"encoder.layer.{first}.{wname}"]
+        ob = self.offsets[f"encoder.layer.{first}.{bname}"]
         sw, sb = self._layer_stride(wname), self._layer_stride(bname)
         ops.gemm_strided(dY, X, g[ow:], M=out_n, N=in_n, K=BL, batch=nl, lda=out_n,
                          sA=BL * out_n, ldb=in_n, sB=BL * in_n, ldc=in_n, sC=sw, trans_a=True,

@@ -19,7 +19,8 @@ from . import _lib
 from ._torch import contig, ptr, require_hip, stream_ptr, workspace
 
 
-def scan_topk(queries: torch.Tensor, docs: torch.Tensor, k: int, doc_offset: int = 0):
+def scan_topk(queries: torch.Tensor, docs: torch.Tensor, k: int, doc_offset: int = 0,
+              ws_tag: str = "scan"):
     """Exact top-k of queries @ docs.T (bf16 inputs, fp32 scores).
 
     queries [Q, D], docs [N, D] on the same HIP device.  Returns
@@ -36,7 +37,7 @@ def scan_topk(queries: torch.Tensor, docs: torch.Tensor, k: int, doc_offset: int
     out_s = torch.empty((Q, k), dtype=torch.float32, device=q.device)
     out_i = torch.empty((Q, k), dtype=torch.int64, device=q.device)
     nbytes = int(_lib.fn("irc_scan_topk_workspace")(Q, N, D, k))
-    ws = workspace(nbytes, q.device, "scan")
+    ws = workspace(nbytes, q.device, ws_tag)
     _lib.call("irc_scan_topk", ptr(q), ptr(d), Q, N, D, k, doc_offset, ptr(ws), ws.numel(),
               ptr(out_s), ptr(out_i), stream_ptr(q.device))
     return out_s, out_i
@@ -83,7 +84,7 @@ def _fp8_operands(queries, docs):
 
 
 def scan_topk_fp8(queries: torch.Tensor, docs: torch.Tensor, k: int, doc_offset: int = 0,
-                  score_scale: float = 1.0):
+                  score_scale: float = 1.0, ws_tag: str = "scan"):
     """Exact top-k over e4m3 queries [Q, D] and docs [N, D] (uint8 bytes); the
     returned scores are the fp32 dot products of the quantised values times
     score_scale (a power of two)."""
@@ -93,7 +94,7 @@ def scan_topk_fp8(queries: torch.Tensor, docs: torch.Tensor, k: int, doc_offset:
     out_s = torch.empty((Q, k), dtype=torch.float32, device=q.device)
     out_i = torch.empty((Q, k), dtype=torch.int64, device=q.device)
     nbytes = int(_lib.fn("irc_scan_topk_fp8_workspace")(Q, N, D, k))
-    ws = workspace(nbytes, q.device, "scan")
+    ws = workspace(nbytes, q.device, ws_tag)
     _lib.call("irc_scan_topk_fp8", ptr(q), ptr(d), Q, N, D, k, doc_offset, float(score_scale),
               ptr(ws), ws.numel(), ptr(out_s), ptr(out_i), stream_ptr(q.device))
     return out_s, out_i
@@ -205,38 +206,126 @@ class ShardedDenseIndex:
 
     # The two device steps are methods so the collective orchestration can be
     # exercised on CPU (gloo) with a test double in tests/test_dist_cpu.py.
-    def _local_topk(self, queries, k):
+    def _local_topk(self, queries, k, ws_tag="scan"):
         if self.dtype == "fp8":
             q8 = quantize_fp8(queries, self.fp8_scale)
             return scan_topk_fp8(q8, self.docs, k, self.doc_offset,
-                                 1.0 / (self.fp8_scale * self.fp8_scale))
-        return scan_topk(queries, self.docs, k, self.doc_offset)
+                                 1.0 / (self.fp8_scale * self.fp8_scale), ws_tag=ws_tag)
+        return scan_topk(queries, self.docs, k, self.doc_offset, ws_tag=ws_tag)
 
     def _merge(self, scores, idx, k):
         return topk_merge(scores, idx, k)
 
-    def search(self, queries: torch.Tensor, k: int):
+    def search(self, queries: torch.Tensor, k: int, equal_counts: bool = False,
+               ws_tag: str = "scan"):
+        """Global top-k of the gathered queries.  ``equal_counts``: every rank
+        passes the same number of queries, so the ragged-count exchange (a host
+        sync) is skipped and the whole search stays stream-ordered."""
         import torch.distributed as dist
 
         if self.group is None or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
-            return self._local_topk(queries, k)
+            return self._local_topk(queries, k, ws_tag)
         world = dist.get_world_size(self.group)
         # (1) all-gather query embeddings (ragged: exchange counts first)
-        n_local = torch.tensor([queries.shape[0]], dtype=torch.int64, device=queries.device)
-        counts = [torch.zeros_like(n_local) for _ in range(world)]
-        dist.all_gather(counts, n_local, group=self.group)
-        counts = [int(c.item()) for c in counts]
+        if equal_counts:
+            counts = [queries.shape[0]] * world
+        else:
+            n_local = torch.tensor([queries.shape[0]], dtype=torch.int64, device=queries.device)
+            cnt = [torch.zeros_like(n_local) for _ in range(world)]
+            dist.all_gather(cnt, n_local, group=self.group)
+            counts = [int(c.item()) for c in cnt]
         qmax = max(counts)
-        qpad = torch.zeros((qmax, queries.shape[1]), dtype=queries.dtype, device=queries.device)
-        qpad[: queries.shape[0]] = queries
+        if qmax == queries.shape[0]:
+            qpad = queries.contiguous()
+        else:
+            qpad = torch.zeros((qmax, queries.shape[1]), dtype=queries.dtype,
+                               device=queries.device)
+            qpad[: queries.shape[0]] = queries
         gathered = [torch.empty_like(qpad) for _ in range(world)]
         dist.all_gather(gathered, qpad, group=self.group)
         allq = torch.cat([g[:c] for g, c in zip(gathered, counts)], dim=0)
         # (2) local exact top-k over this shard (global indices)
-        s, i = self._local_topk(allq, k)
+        s, i = self._local_topk(allq, k, ws_tag)
         # (3) exchange per-shard lists and merge (every rank gets the result)
         ss = [torch.empty_like(s) for _ in range(world)]
         ii = [torch.empty_like(i) for _ in range(world)]
         dist.all_gather(ss, s.contiguous(), group=self.group)
         dist.all_gather(ii, i.contiguous(), group=self.group)
         return self._merge(torch.stack(ss), torch.stack(ii), k)
+
+    def search_many(self, batches, k: int, depth: int = 2, equal_counts: bool = False,
+                    graphs: bool | None = None):
+        """search() over a sequence of query batches with up to ``depth`` batches
+        in flight on as many HIP streams (each with its own scan workspace): one
+        batch's latency-bound selects overlap the next batch's HBM-bound filter.
+        ``graphs`` (default: single process and every batch of one shape): each
+        stream replays a HIP graph of the whole local search captured once, so the
+        host issues a copy, a replay and two result copies per batch instead of
+        the call's individual launches.  Results are identical to calling
+        search() per batch; returned in order, usable on the current stream."""
+        import torch.distributed as dist
+
+        batches = list(batches)
+        dev = self.docs.device
+        cur = torch.cuda.current_stream(dev)
+        streams = _search_streams(dev, depth)
+        single = self.group is None or not dist.is_initialized() or \
+            dist.get_world_size(self.group) == 1
+        if graphs is None:
+            graphs = single and len({tuple(b.shape) for b in batches}) <= 1
+        if graphs and not single:
+            raise ValueError("graphed search_many needs a single-process index")
+        slots = self._graph_slots(batches[0], k, depth, streams) if (graphs and batches) else None
+        out = []
+        for n, q in enumerate(batches):
+            st = streams[n % depth]
+            st.wait_stream(cur)  # the batch's inputs were produced on `cur`
+            with torch.cuda.stream(st):
+                if slots is not None:
+                    g, qin, so, io = slots[n % depth]
+                    qin.copy_(q)
+                    g.replay()
+                    res = (so.clone(), io.clone())
+                else:
+                    res = self.search(q, k, equal_counts=equal_counts, ws_tag=f"scan{n % depth}")
+            q.record_stream(st)
+            out.append(res)
+        for st in streams:
+            cur.wait_stream(st)
+        for s, i in out:
+            s.record_stream(cur)
+            i.record_stream(cur)
+        return out
+
+    def _graph_slots(self, q0, k, depth, streams):
+        """Per stream: (graph, static query buffer, static scores, static ids) of the
+        local search for q0's shape, captured once and cached on the index."""
+        key = (tuple(q0.shape), q0.dtype, int(k), depth)
+        cache = self.__dict__.setdefault("_graphs", {})
+        if key in cache:
+            return cache[key]
+        slots = []
+        for j, st in enumerate(streams):
+            qin = torch.empty_like(q0)
+            qin.copy_(q0)
+            tag = f"gscan{j}"
+            with torch.cuda.stream(st):
+                self._local_topk(qin, k, tag)  # warm-up: workspace sized outside the graph
+            st.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                so, io = self._local_topk(qin, k, tag)
+            slots.append((g, qin, so, io))
+        cache[key] = slots
+        return slots
+
+
+_SEARCH_STREAMS = {}
+
+
+def _search_streams(dev, depth):
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), depth)
+    st = _SEARCH_STREAMS.get(key)
+    if st is None:
+        st = _SEARCH_STREAMS[key] = [torch.cuda.Stream(dev) for _ in range(depth)]
+    return st

@@ -98,6 +98,15 @@ class TrainState:
     def micro_batch(self, n_pairs, forward_fn, sync_loss=True):
         """forward_fn() -> loss tensor of this micro-batch (model(...) call)."""
         self._maybe_enable_queue()
+        will_step = self.batch_size + n_pairs == self.acml or n_pairs != self.bsz
+        enc = self.model.encoder_q
+        # --model BERT under DP: the 110M-float gradient is all-reduced in buckets
+        # DURING the encoder backward (overlapped); only when this micro-batch
+        # steps and the encoder runs backward once (keys from the momentum encoder)
+        overlap = self.process_group is not None and hasattr(enc, "set_grad_reduce") and \
+            self.model.use_momentum and self.world > 1
+        if overlap:
+            enc.set_grad_reduce(self.process_group if will_step else None)
         self.batch_size += n_pairs
         # data parallel: the loss is the GLOBAL micro-batch's (gathered negatives),
         # so it is divided by the global accumulation size acml * world, as one
@@ -111,7 +120,10 @@ class TrainState:
             self.loss_sum = self.loss_sum + loss.detach()
         stepped = False
         if self.batch_size == self.acml or n_pairs != self.bsz:
-            if self.process_group is not None:
+            if overlap:
+                enc.wait_grad_reduce()
+                enc.set_grad_reduce(None)
+            elif self.process_group is not None:
                 from irc_amd.dist import all_reduce_sum_
 
                 all_reduce_sum_(self.model.encoder_q.flat_grad, self.process_group)

@@ -64,7 +64,7 @@ def _index_worker(rank, port, out_dir):
         def __init__(self, docs, doc_offset, group):
             self.docs, self.doc_offset, self.group = docs, doc_offset, group
 
-        def _local_topk(self, queries, k):
+        def _local_topk(self, queries, k, ws_tag=None):
             i, s = O.scan_topk(queries.numpy(), self.docs.numpy(), k, self.doc_offset)
             return torch.from_numpy(s), torch.from_numpy(i)
 

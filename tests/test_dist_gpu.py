@@ -27,7 +27,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _args(b):
+def _args(b, model="LSTM"):
     import yaml
 
     from conftest import PKG
@@ -38,9 +38,12 @@ def _args(b):
         "vocab_size": 500, "hidden_size": 128, "num_hidden_layers": 2, "num_attention_heads": 2,
         "intermediate_size": 256, "max_position_embeddings": 64}}
     cfg["model"]["LSTM"].update(input_size=128, hidden_size=256, num_layers=2, output_size=64)
+    cfg["model"]["BERT"] = {"name": "tiny", "seed": 5, "config": {
+        "vocab_size": 500, "hidden_size": 64, "num_hidden_layers": 5, "num_attention_heads": 2,
+        "intermediate_size": 128, "max_position_embeddings": 64}}
     cfg["loss"]["InfoNCE"].update(queue_size=256, queue_start_steps=1)
     cfg["train"].update(batch_size=b, acml_batch_size=b)
-    return argparse.Namespace(config=cfg, loss="InfoNCE", model="LSTM", opt="adam",
+    return argparse.Namespace(config=cfg, loss="InfoNCE", model=model, opt="adam",
                               sample="uniform")
 
 
@@ -55,16 +58,18 @@ def _batches():
     return out
 
 
-def _run(rank, world, dev, out_dir):
+def _run(rank, world, dev, out_dir, model_kind="LSTM"):
     from irc_amd.precision import set_precision
     from src.model import build_model, get_optimizer
     from src.train import TrainState
 
     set_precision("fp32")
     b = B // world
-    args = _args(b)
+    args = _args(b, model_kind)
     torch.manual_seed(1337)
     model = build_model(args).to(dev).train()
+    if model_kind == "BERT":
+        model.encoder_q.reduce_bucket_layers = 2  # 3 buckets over 5 layers
     st = TrainState(args, model, get_optimizer(args, model))
     if world > 1:
         st.set_process_group(dist.group.WORLD)
@@ -74,32 +79,40 @@ def _run(rank, world, dev, out_dir):
         p = slice(B + rank * b, B + (rank + 1) * b)
         ids_r = torch.cat([ids[a], ids[p]]).to(dev)
         mask_r = torch.cat([mask[a], mask[p]]).to(dev)
-        loss, stepped = st.micro_batch(
-            b, lambda: model.forward_features(*model.bert_extract_ids(ids_r, mask_r, b)))
+        if model_kind == "BERT":
+            fwd = lambda: model.forward_ids(ids_r, mask_r, b)  # noqa: E731
+        else:
+            fwd = lambda: model.forward_features(*model.bert_extract_ids(ids_r, mask_r, b))  # noqa: E731
+        loss, stepped = st.micro_batch(b, fwd)
         assert stepped
         losses.append(loss.item())
     sd = {k: v.cpu().numpy() for k, v in model.state_dict().items()
           if k.startswith(("encoder_q", "encoder_k", "queue"))}
-    np.savez(os.path.join(out_dir, f"r{rank}_w{world}.npz"), losses=np.array(losses), **sd)
+    np.savez(os.path.join(out_dir, f"{model_kind}_r{rank}_w{world}.npz"),
+             losses=np.array(losses), **sd)
 
 
-def _worker(rank, port, out_dir):
+def _worker(rank, port, out_dir, model_kind):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
-        _run(rank, WORLD, torch.device("cuda:0"), out_dir)
+        _run(rank, WORLD, torch.device("cuda:0"), out_dir, model_kind)
     finally:
         dist.destroy_process_group()
 
 
-def test_dp_two_ranks_match_single_process(gpu, tmp_path):
-    mp.start_processes(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True,
-                       start_method="spawn")
-    _run(0, 1, gpu, str(tmp_path))
-    ref = np.load(tmp_path / "r0_w1.npz")
+@pytest.mark.parametrize("model_kind", ["LSTM", "BERT"])
+def test_dp_two_ranks_match_single_process(gpu, tmp_path, model_kind):
+    """LSTM: frozen BERT + BiLSTM heads (one all-reduce after backward).  BERT: the
+    trainable encoder, whose gradient is all-reduced in 3 buckets DURING its
+    backward (BertEncoder.set_grad_reduce) -- same numbers either way."""
+    mp.start_processes(_worker, args=(_free_port(), str(tmp_path), model_kind), nprocs=WORLD,
+                       join=True, start_method="spawn")
+    _run(0, 1, gpu, str(tmp_path), model_kind)
+    ref = np.load(tmp_path / f"{model_kind}_r0_w1.npz")
     for r in range(WORLD):
-        got = np.load(tmp_path / f"r{r}_w{WORLD}.npz")
+        got = np.load(tmp_path / f"{model_kind}_r{r}_w{WORLD}.npz")
         # global batch loss on every rank = single-process loss (same logits rows)
         np.testing.assert_allclose(got["losses"], ref["losses"], rtol=2e-5)
         # parameters after STEPS Adam steps: Adam normalises each coordinate (g /
@@ -109,7 +122,8 @@ def test_dp_two_ranks_match_single_process(gpu, tmp_path):
             if k != "losses":
                 np.testing.assert_allclose(got[k], ref[k], rtol=1e-4, atol=1.25e-4 * STEPS,
                                            err_msg=k)
-    a, b = np.load(tmp_path / "r0_w2.npz"), np.load(tmp_path / "r1_w2.npz")
+    a = np.load(tmp_path / f"{model_kind}_r0_w2.npz")
+    b = np.load(tmp_path / f"{model_kind}_r1_w2.npz")
     for k in a.files:  # replicas stay bit-identical across ranks
         if k != "losses":
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)

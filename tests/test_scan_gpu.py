@@ -171,3 +171,34 @@ def test_full_c2_size_properties(gpu):
     # idempotence: a second call returns the same bits
     s2, i2 = retrieval.scan_topk(q, d, k)
     assert torch.equal(i, i2) and torch.equal(s, s2)
+
+
+def test_search_many_equals_serial_search(gpu):
+    """Pipelined batches (search_many, 2 streams, own workspaces) return exactly
+    what serial search() calls return."""
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(8)
+    d = _dev(_grid(rng, (30000, 256), 3), gpu)
+    index = retrieval.ShardedDenseIndex(d)
+    batches = [_dev(_grid(rng, (q, 256), 3), gpu) for q in (256, 1, 300, 64, 256)]
+    many = index.search_many(batches, 50, depth=2)
+    for q, (s, i) in zip(batches, many):
+        s0, i0 = index.search(q, 50)
+        assert torch.equal(s, s0) and torch.equal(i, i0)
+
+
+def test_graphed_search_many_equals_serial_search(gpu):
+    """HIP-graph replays of the whole local search (one graph per stream) return
+    exactly what serial search() calls return, for bf16 and fp8 shards."""
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(9)
+    d = _dev(_grid(rng, (20000, 256), 3), gpu)
+    for dtype in ("bf16", "fp8"):
+        index = retrieval.ShardedDenseIndex(d, doc_offset=5, dtype=dtype)
+        batches = [_dev(_grid(rng, (256, 256), 3), gpu) for _ in range(5)]
+        many = index.search_many(batches, 40, depth=2, graphs=True)
+        for q, (s, i) in zip(batches, many):
+            s0, i0 = index.search(q, 40)
+            assert torch.equal(s, s0) and torch.equal(i, i0), dtype
