@@ -93,7 +93,7 @@ __device__ __forceinline__ void sweep(F addr, unsigned epoch, unsigned (&v)[N], 
       v[k] = (unsigned)x;
       ok &= (unsigned)(x >> 32) == epoch;
     }
-    if (__all(ok)) return;
+    if (__all(ok) && spin_max) return;  // spin_max 0: forced timeout (debug)
     if (++spins > spin_max) {
       if ((threadIdx.x & 63) == 0) {
         __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -138,7 +138,7 @@ __device__ __forceinline__ void poll_flags(unsigned* flags, unsigned epoch, unsi
       if (lane < P)
         ok = __hip_atomic_load((gu32*)(flags + lane), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT) >= epoch;
-      if (__all(ok)) break;
+      if (__all(ok) && spin_max) break;
       if (++spins > spin_max) {
         if (lane == 0) {
           __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -163,7 +163,7 @@ __device__ __forceinline__ void poll_sentinels(const unsigned long long* const* 
     for (unsigned spins = 0;;) {
       bool ok = true;
       if (lane < P) ok = (unsigned)(ld_sc1(sent[lane]) >> 32) == epoch;
-      if (__all(ok)) break;
+      if (__all(ok) && spin_max) break;
       if (++spins > spin_max) {
         if (lane == 0) {
           __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -585,8 +585,8 @@ extern "C" int irc_lstm_coop_pack(const float* whh, int64_t H, int64_t ndir, voi
 }
 
 // Spin bound of the cross-CU hand-off (IRC_LSTM_COOP_SPIN_MAX overrides; a
-// debug knob: 0 makes every wait that is not satisfied at once time out, which
-// the fault-path tests use).  ~1.6e9 cycles by default -- a true deadlock only.
+// debug knob: 0 makes the first cross-CU wait of every workgroup time out, ready
+// or not, which the fault-path tests use).  ~1.6e9 cycles by default -- a true deadlock only.
 static unsigned coop_spin_max() {
   const char* e = getenv("IRC_LSTM_COOP_SPIN_MAX");
   return e ? (unsigned)strtoul(e, nullptr, 10) : lstmc::SPIN_MAX;

@@ -109,7 +109,13 @@ def test_dp_two_ranks_match_single_process(gpu, tmp_path, model_kind):
     backward (BertEncoder.set_grad_reduce) -- same numbers either way."""
     mp.start_processes(_worker, args=(_free_port(), str(tmp_path), model_kind), nprocs=WORLD,
                        join=True, start_method="spawn")
-    _run(0, 1, gpu, str(tmp_path), model_kind)
+    from irc_amd.precision import get_precision, set_precision
+
+    old = get_precision()
+    try:
+        _run(0, 1, gpu, str(tmp_path), model_kind)
+    finally:
+        set_precision(old)
     ref = np.load(tmp_path / f"{model_kind}_r0_w1.npz")
     for r in range(WORLD):
         got = np.load(tmp_path / f"{model_kind}_r{r}_w{WORLD}.npz")

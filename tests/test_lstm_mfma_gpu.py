@@ -152,9 +152,9 @@ def test_coop_matches_single_cu_and_no_timeout(gpu, B, L):
 
 @pytest.fixture
 def forced_coop_timeout():
-    """IRC_LSTM_COOP_SPIN_MAX=0 (read per call by the library): every cross-CU
-    wait that is not satisfied at once times out -- the debug path that must
-    never yield numbers."""
+    """IRC_LSTM_COOP_SPIN_MAX=0 (read per call by the library): the first cross-CU
+    wait of every workgroup times out, whether its data has arrived or not -- the
+    debug path that must never yield numbers."""
     import os
 
     os.environ["IRC_LSTM_COOP_SPIN_MAX"] = "0"
@@ -162,7 +162,7 @@ def forced_coop_timeout():
     del os.environ["IRC_LSTM_COOP_SPIN_MAX"]
 
 
-def test_coop_forced_timeout_poisons_outputs(gpu, forced_coop_timeout):
+def test_coop_forced_timeout_poisons_outputs(gpu, forced_coop_timeout, bf16_mode):
     """A timed-out cluster call NaN-poisons its own output on the device and sets
     the sticky fault word -- whatever the caller does with the sync word."""
     from irc_amd import ops
@@ -183,7 +183,7 @@ def test_coop_forced_timeout_poisons_outputs(gpu, forced_coop_timeout):
     assert bool(torch.isnan(dg.float()).all())
 
 
-def test_coop_forced_timeout_raises_in_train_step(gpu, forced_coop_timeout):
+def test_coop_forced_timeout_raises_in_train_step(gpu, forced_coop_timeout, bf16_mode):
     """The production step (H = 256 BiLSTM head on the cluster recurrence) raises
     at its next sync point instead of training on stale state."""
     import argparse
