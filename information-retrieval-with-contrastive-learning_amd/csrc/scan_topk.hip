@@ -28,6 +28,12 @@
 #ifndef IRC_SCAN_AUX
 #define IRC_SCAN_AUX 0  // cache policy of the corpus stream (0: default)
 #endif
+#ifndef IRC_SCAN_SEL_STOP
+#define IRC_SCAN_SEL_STOP -1  // diagnostic builds: the final select returns at stage N
+#endif
+#ifndef IRC_SCAN_GENERAL_SELECT
+#define IRC_SCAN_GENERAL_SELECT 0  // A/B builds: 1 = region selects without select_fast
+#endif
 
 namespace irc {
 namespace scan {
@@ -74,7 +80,13 @@ struct Geo {
 // keeps only the largest key of the JPW docs it finishes per tile -- the k-th
 // largest of these group maxima is still a lower bound of the true k-th key
 // (k distinct docs reach it), with 8-16x fewer keys to store and select.
-enum Mode { KEYS = 0, SCORES = 1, GMAX = 2 };
+// LTOP (single pass, no threshold): each lane keeps the 4 largest keys of the
+// docs it finishes (its "list": one (worker, query, slice)), in registers, and
+// writes them densely at the end; select_dense then finds the k-th key of all
+// lists and rescans, exactly, the workers whose truncated lists could hide a
+// winner.
+enum Mode { KEYS = 0, SCORES = 1, GMAX = 2, LTOP = 3 };
+constexpr int LT_M = 4;  // keys per LTOP list
 
 // Opaque copy: stops LICM from hoisting per-lane address math out of the tile
 // loop (keeping 12+ 64-bit DMA addresses live costs more VGPRs than recomputing).
@@ -186,6 +198,14 @@ void scan_tile_kernel(
       bq[c] = v;
     }
   }
+  // LTOP list (descending; 0 = empty slot: real keys are >= 1) and the float
+  // prefilter of its last slot
+  uint64_t lt0 = 0, lt1 = 0, lt2 = 0, lt3 = 0;
+#ifdef IRC_LTOP_NOCAND  // diagnostic: the LTOP kernel with no candidate ever
+  float ltf = __builtin_huge_valf();
+#else
+  float ltf = q < Q ? -__builtin_huge_valf() : __builtin_huge_valf();
+#endif
   const uint64_t qthr = (MODE == KEYS && thr != nullptr && q < Q) ? thr[q] : 0ull;
   const uint32_t qthr_hi = (uint32_t)(qthr >> 32);
   const float qtf = q >= Q ? __builtin_huge_valf()
@@ -339,6 +359,40 @@ void scan_tile_kernel(
         bs = better ? s : bs;
       }
       push(bs >= 0, make_key(bv, idx_base + (uint32_t)bs * (uint32_t)stride));
+    } else if (MODE == LTOP) {
+      // candidates: scores >= the list's last score; one per lane per round
+      // (rounds = the wave's largest candidate count; after the first tiles
+      // mostly 0-2).  Measured alternatives that ran slower on MI355X: one
+      // insertion step per slot with any candidate (the select chain saved, more
+      // steps at Q >= 16), a select tree + position-compare insertion (more
+      // instructions), a floor shared with the h-partner lane (select_dense
+      // slower).
+      uint32_t pm = 0;
+#pragma unroll
+      for (int jj = 0; jj < JPW; ++jj) pm |= (uint32_t)(!(fin[jj] < ltf)) << jj;
+      while (__ballot(pm != 0)) {
+#ifdef IRC_SCAN_STAMPS  // diagnostic: LTOP rounds (wave 0 of blocks < 256)
+        if (wave == 0 && lane == 0 && blockIdx.x < 256)
+          atomicAdd((unsigned long long*)&dbg_stamps[3][28], 1ull);
+#endif
+        const int b = pm != 0 ? __builtin_ctz(pm) : 0;
+        const bool cand = pm != 0;
+        pm &= pm - 1;
+        float v = fin[0];
+#pragma unroll
+        for (int jj = 1; jj < JPW; ++jj) v = b == jj ? fin[jj] : v;
+        const int j = b + joff;
+        const int s = s0row + (j & 3) + 8 * (j >> 2) + 4 * h;
+        const uint64_t key = make_key(v, idx_base + (uint32_t)s * (uint32_t)stride);
+        if (cand && s < NS && key > lt3) {
+          lt3 = key;
+          uint64_t t;
+          if (lt3 > lt2) { t = lt2; lt2 = lt3; lt3 = t; }
+          if (lt2 > lt1) { t = lt1; lt1 = lt2; lt2 = t; }
+          if (lt1 > lt0) { t = lt0; lt0 = lt1; lt1 = t; }
+          ltf = lt3 != 0 ? unorderable_f32((uint32_t)(lt3 >> 32)) : -__builtin_huge_valf();
+        }
+      }
     } else {
       // Float prefilter (key >= thr implies score >= qtf for non-NaN scores; NaN
       // passes it and fails the exact test): a branch-free pass mask, and the
@@ -370,6 +424,19 @@ void scan_tile_kernel(
     wg_barrier();  // all reads of this buffer (and of xbuf) done before reuse
   }
 
+  if (MODE == LTOP) {
+    // dense lists: keys[((q * G_total + worker) * 2KS + slice) * 4 + i], cap = lists
+    // per query (G_total * 2KS); every list written, empty slots 0
+    if (q < Q) {
+      typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+      u64x2* dst = reinterpret_cast<u64x2*>(
+          keys + (((int64_t)q * cap + (int64_t)worker * (2 * KS) + slice) * LT_M));
+      dst[0] = (u64x2){lt0, lt1};
+      dst[1] = (u64x2){lt2, lt3};
+    }
+    STAMP(3, 1);
+    return;
+  }
   if (MODE != SCORES) {  // flush the shift buffer (newest first; order is irrelevant)
     if (sbn > 0) myreg[nsurv] = sb0;
     if (sbn > 1) myreg[nsurv + 1] = sb1;
@@ -383,31 +450,45 @@ void scan_tile_kernel(
 
 // ----------------------------------------------------------------- selection
 // Key sources for the select kernel.
+// NSL (slices per region group) is a power of two (1, 2 or 4) and the slice
+// capacity is precomputed: region addressing is shifts and one multiply (a
+// run-time integer division costs ~40 VALU instructions, 64-bit ~100, and the
+// selects address every candidate this way).
 struct RegionSource {  // scan workspace: G regions per query, NSL slices each
   const uint64_t* keys;
   const uint32_t* counts;
   int G;
   int Qpad;
   int64_t cap;
-  int NSL;
+  int lnsl;           // log2(NSL)
+  int64_t slice_cap;  // cap / NSL
   static constexpr bool kRegions = true;
-  __device__ __forceinline__ int nregions() const { return NSL * G; }
+  __device__ __forceinline__ int nregions() const { return G << lnsl; }
+  __device__ __forceinline__ int64_t group(int q, int r) const {
+    return (int64_t)(r >> lnsl) * Qpad + q;
+  }
   __device__ __forceinline__ uint32_t count(int q, int r) const {
-    return counts[((int64_t)(r / NSL) * Qpad + q) * NSL + (r % NSL)];
+    return counts[(group(q, r) << lnsl) + (r & ((1 << lnsl) - 1))];
   }
   __device__ __forceinline__ const uint64_t* region(int q, int r) const {
-    return keys + ((int64_t)(r / NSL) * Qpad + q) * cap + (r % NSL) * (cap / NSL);
+    return keys + group(q, r) * cap + (r & ((1 << lnsl) - 1)) * slice_cap;
   }
   template <class F>
   __device__ __forceinline__ void for_each(int q, int tid, int nt, F&& f) const {
-    for (int gs = tid; gs < NSL * G; gs += nt) {
-      const int g = gs / NSL, sl = gs % NSL;
-      const uint32_t n = counts[((int64_t)g * Qpad + q) * NSL + sl];
-      const uint64_t* p = keys + ((int64_t)g * Qpad + q) * cap + sl * (cap / NSL);
+    for (int r = tid; r < nregions(); r += nt) {
+      const uint32_t n = count(q, r);
+      const uint64_t* p = region(q, r);
       for (uint32_t j = 0; j < n; ++j) f(p[j]);
     }
   }
 };
+
+static RegionSource region_source(const uint64_t* keys, const uint32_t* counts, int G, int Qpad,
+                                  int64_t cap, int nsl) {
+  int l = 0;
+  while ((1 << l) < nsl) ++l;
+  return RegionSource{keys, counts, G, Qpad, cap, l, cap >> l};
+}
 
 struct ListSource {  // merge input: [P][Q][kin] scores + global idx (-1 = empty)
   const float* score;
@@ -421,12 +502,19 @@ struct ListSource {  // merge input: [P][Q][kin] scores + global idx (-1 = empty
   __device__ __forceinline__ const uint64_t* region(int, int) const { return nullptr; }
   template <class F>
   __device__ __forceinline__ void for_each(int q, int tid, int nt, F&& f) const {
-    const int64_t M = (int64_t)P * kin;
-    for (int64_t i = tid; i < M; i += nt) {
-      const int p = (int)(i / kin), j = (int)(i % kin);
+    // (p, j) stepped incrementally: no run-time division per element
+    int p = tid / kin, j = tid - p * kin;
+    const int dp = nt / kin, dj = nt - dp * kin;
+    for (; p < P;) {
       const int64_t off = ((int64_t)p * Q + q) * kin + j;
       const int64_t id = idx[off];
       if (id >= 0) f(make_key(score[off], (uint32_t)id));
+      p += dp;
+      j += dj;
+      if (j >= kin) {
+        j -= kin;
+        ++p;
+      }
     }
   }
 };
@@ -527,6 +615,180 @@ __device__ __forceinline__ void sort_and_emit(const uint64_t* cand, int cnt, int
   }
 }
 
+// Fast path of select_body for region sources whose candidates fit the stage
+// (M <= SEL_STAGE: the scan's threshold and final selects on any input short of
+// adversarial skew).  Round-1 phase stamps of select_body on MI355X (C2, k = 100,
+// M ~ 1.8k): 12.5 us per final select, of which 3.4 us in two radix passes that
+// re-read the staged keys from LDS, 1.2 us collecting, 2.3 us in wave 0's sort.
+// Here thread t's keys (i = t + 256 u of the region-id map) stay in registers
+// for every pass; the histogram is double-buffered (waves 1-3 clear the next
+// pass's copy while wave 0 scans), so a pass costs two barriers; the winners are
+// collected with one LDS atomic per wave and placed by rank (each counts the
+// winners above it over broadcast LDS reads) -- no sort.  Same keys, same k-th
+// key, same outputs as the general path.
+template <class Src, bool BIGK>
+__device__ __forceinline__ void select_fast(const Src& src, int q, int k, int mode, uint32_t M,
+                                            const uint16_t* rid, const uint32_t* roff,
+                                            uint32_t* hbuf, uint64_t* cand, uint64_t* s_mm,
+                                            uint32_t* s_misc, uint32_t* s_coll,
+                                            uint64_t* __restrict__ thr_out,
+                                            float* __restrict__ out_score,
+                                            int64_t* __restrict__ out_idx, float smul) {
+  constexpr int U = SEL_STAGE / SEL_NT;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  uint64_t v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t i = tid + u * SEL_NT;
+    v[u] = 0;
+    if (i < M) {
+      const int r = rid[i];
+      v[u] = src.region(q, r)[i - roff[r]];
+    }
+  }
+  uint32_t* h0 = hbuf;
+  uint32_t* h1 = hbuf + SEL_NW * 256;
+  for (int i = tid; i < SEL_NW * 256; i += SEL_NT) h0[i] = 0;
+  uint64_t mn = ~0ull, mx = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (tid + u * SEL_NT < M) {
+      mn = v[u] < mn ? v[u] : mn;
+      mx = v[u] > mx ? v[u] : mx;
+    }
+  }
+  mn = wave_min_u64(mn);
+  mx = wave_max_u64(mx);
+  if (lane == 0) {
+    s_mm[wave] = mn;
+    s_mm[SEL_NW + wave] = mx;
+  }
+  __syncthreads();
+  STAMP(mode, 2);
+  if (IRC_SCAN_SEL_STOP == 2 && mode == SEL_FINAL) return;
+
+  uint64_t kth = 0;  // 0 = keep everything
+  if (M > (uint32_t)k) {
+    mn = s_mm[0];
+    mx = s_mm[SEL_NW];
+#pragma unroll
+    for (int w = 1; w < SEL_NW; ++w) {
+      mn = s_mm[w] < mn ? s_mm[w] : mn;
+      mx = s_mm[SEL_NW + w] > mx ? s_mm[SEL_NW + w] : mx;
+    }
+    const int top = 63 - __builtin_clzll((mn ^ mx) | 1ull);
+    uint64_t pmask = top >= 63 ? 0ull : (~0ull << (top + 1));
+    uint64_t prefix = mn & pmask;
+    uint32_t kr = (uint32_t)k;
+    int hi = top;
+    for (int pass = 0;; ++pass) {
+      uint32_t* h = (pass & 1) ? h1 : h0;
+      uint32_t* hn = (pass & 1) ? h0 : h1;
+      const int lo = hi >= 7 ? hi - 7 : 0;
+      const uint32_t dm = (2u << (hi - lo)) - 1u;
+      uint32_t* hw = h + wave * 256;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (tid + u * SEL_NT < M && (v[u] & pmask) == prefix)
+          atomicAdd(&hw[(uint32_t)(v[u] >> lo) & dm], 1u);
+      __syncthreads();
+      if (wave == 0) {
+        uint32_t bb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint32_t t = 0;
+#pragma unroll
+          for (int w = 0; w < SEL_NW; ++w) t += h[w * 256 + 4 * lane + j];
+          bb[j] = t;
+        }
+        const uint32_t cnt4 = bb[0] + bb[1] + bb[2] + bb[3];
+        uint32_t suf = cnt4;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t t = __shfl_down(suf, o, 64);
+          if (lane + o < 64) suf += t;
+        }
+        const uint32_t above = suf - cnt4;
+        if (suf >= kr && above < kr) {
+          uint32_t acc = above;
+          int sel = 4 * lane, selc = 0;
+          for (int j = 3; j >= 0; --j) {
+            if (acc + bb[j] >= kr) {
+              sel = 4 * lane + j;
+              selc = (int)bb[j];
+              break;
+            }
+            acc += bb[j];
+          }
+          s_misc[2] = (uint32_t)sel;
+          s_misc[1] = kr - acc;
+          s_misc[3] = (uint32_t)selc == kr - acc;
+        }
+      } else {
+        for (int i = tid - 64; i < SEL_NW * 256; i += SEL_NT - 64) hn[i] = 0;
+      }
+      __syncthreads();
+      prefix |= (uint64_t)s_misc[2] << lo;
+      pmask |= (uint64_t)dm << lo;
+      kr = s_misc[1];
+      STAMP(mode, 4 + pass);
+      if (s_misc[3] || lo == 0 || (mode == SEL_THRESHOLD && pass == 1)) break;
+      hi = lo - 1;  // s_misc is rewritten only after the next pass's first barrier
+    }
+    kth = prefix;
+  }
+  if (mode == SEL_THRESHOLD) {
+    if (tid == 0) thr_out[q] = kth;
+    return;
+  }
+  STAMP(mode, 12);
+  if (IRC_SCAN_SEL_STOP == 3 && mode == SEL_FINAL) return;
+  // collect the exactly min(M, k) keys >= kth: one LDS atomic per wave and slot
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const bool take = tid + u * SEL_NT < M && v[u] >= kth;
+    const uint64_t bal = __ballot(take);
+    if (bal != 0) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(s_coll, (uint32_t)__popcll(bal));
+      base = __shfl(base, 0, 64);
+      if (take) cand[base + __popcll(bal & ((1ull << lane) - 1))] = v[u];
+    }
+  }
+  __syncthreads();
+  STAMP(mode, 13);
+  if (IRC_SCAN_SEL_STOP == 4 && mode == SEL_FINAL) return;
+  const int cnt = (int)(M < (uint32_t)k ? M : (uint32_t)k);
+  if (cnt <= SEL_NT) {
+    // winner tid goes to its rank (keys are distinct); slots past cnt are empty
+    for (int i = tid; i < k; i += SEL_NT) {
+      float sc = -__builtin_huge_valf();
+      int64_t id = -1;
+      int pos = i;
+      if (i < cnt) {
+        const uint64_t key = cand[i];
+        int rank = 0;
+        int j = 0;
+        for (; j + 4 <= cnt; j += 4)
+          rank += (int)(cand[j] > key) + (int)(cand[j + 1] > key) + (int)(cand[j + 2] > key) +
+                  (int)(cand[j + 3] > key);
+        for (; j < cnt; ++j) rank += (int)(cand[j] > key);
+        pos = rank;
+        sc = unorderable_f32((uint32_t)(key >> 32)) * smul;
+        id = (int64_t)(uint32_t)(~(uint32_t)key);
+      }
+      out_score[(int64_t)q * k + pos] = sc;
+      out_idx[(int64_t)q * k + pos] = id;
+    }
+  } else if (wave == 0) {
+    if (cnt <= 512 || !BIGK) sort_and_emit<8>(cand, cnt, k, q, lane, smul, out_score, out_idx);
+    else sort_and_emit<16>(cand, cnt, k, q, lane, smul, out_score, out_idx);
+  }
+  STAMP(mode, 14);
+}
+
 // One workgroup per query: the exact k-th largest distinct key among the
 // query's candidates by radix select, then the winners sorted.
 //  * Region sources: all region counts are loaded at once (each thread owns up
@@ -565,8 +827,13 @@ __device__ __forceinline__ void select_body(Src src, int k, int mode,
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = tid & 63;
+#define SEL_STOP(n)                                                     \
+  do {                                                                  \
+    if (IRC_SCAN_SEL_STOP == (n) && mode == SEL_FINAL) return;          \
+  } while (0)
 
   STAMP(mode, 0);
+  SEL_STOP(0);
   if (tid == 0) {
     s_misc[0] = 0;
     s_misc[3] = 0;
@@ -624,6 +891,15 @@ __device__ __forceinline__ void select_body(Src src, int k, int mode,
   const bool staged = M <= (uint32_t)SEL_STAGE;
   __syncthreads();
   STAMP(mode, 1);
+  SEL_STOP(1);
+  if constexpr (Src::kRegions) {
+    if (table && staged && !IRC_SCAN_GENERAL_SELECT) {
+      select_fast<Src, BIGK>(src, q, k, mode, M, rid, roff,
+                             reinterpret_cast<uint32_t*>(stage), cand, &s_mm[0][0], s_misc,
+                             &s_coll, thr_out, out_score, out_idx, smul);
+      return;
+    }
+  }
   uint64_t mn = ~0ull, mx = 0;
   if (staged) {
     if (table) {
@@ -1005,6 +1281,383 @@ __global__ __launch_bounds__(64 * SWQ) void select_wave_kernel(RegionSource src,
   }
 }
 
+// ------------------------------------------------------------- select_dense
+// Final select of the single-pass LTOP scan (no sample pass, no threshold
+// select).  Per query: LS lists of LT_M keys (one per (worker, slice)), dense.
+//  1. kth = the exact k-th largest nonzero key of all lists -- a LOWER bound of
+//     the true k-th key (a subset's k-th key is never larger).
+//  2. A list whose last slot holds a key >= kth may have dropped a winner: its
+//     worker is rescanned -- every doc of the worker's tiles scored again with
+//     the filter's own MFMA sequence (same operands, same k order, same two
+//     k-slice partial sums added), so the keys are bit-identical -- and the
+//     worker's lists are replaced by its keys >= the running bound.  The
+//     rescanned keys are held in LDS; when the buffer fills, the union is cut to
+//     its k-th key (a new, higher bound) and the scan goes on.
+//  3. The exact top-k of the union, ranked as in select_fast.
+// On random data a rescan is rare (each list holds ~0.1 winners on average at
+// C2); a corpus sorted or clustered by score triggers it, at a cost, never a
+// wrong result.
+struct DenseArgs {
+  const uint64_t* lists;          // [Q][LS][LT_M]
+  const unsigned char* queries;   // [Q][D] elements of EB bytes
+  const unsigned char* docs;      // [NS][D]
+  int LS;                         // lists per query (workers * 2KS), LS * LT_M <= SEL_STAGE
+  int NS;
+  int tpw;                        // tiles (of TD docs) per worker
+  uint32_t idx_base;
+  int k;
+  float smul;
+  float* out_score;
+  int64_t* out_idx;
+};
+constexpr int SD_XCAP = 2048;  // rescanned keys held at once (>= SEL_MAXK + 4 * TD)
+constexpr int SD_DCAP = 2048;  // docs listed per rescan phase (64 tiles x 32 rows)
+
+// Exact k-th largest nonzero key of v[] (registers, slot i = tid + 256 u) and
+// xk[0, xn) (LDS); 0 when there are <= k of them.  Block-wide, every thread
+// returns it.  *total = the number of nonzero keys.
+template <int U>
+__device__ uint64_t dense_kth(const uint64_t (&v)[U], const uint64_t* xk, uint32_t xn, int k,
+                              uint32_t* hbuf, uint64_t* s_mm, uint32_t* s_cnt, uint32_t* s_misc,
+                              uint32_t* total) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  uint32_t c = 0;
+  uint64_t mn = ~0ull, mx = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (v[u] != 0) {
+      ++c;
+      mn = v[u] < mn ? v[u] : mn;
+      mx = v[u] > mx ? v[u] : mx;
+    }
+  for (uint32_t i = tid; i < xn; i += SEL_NT) {
+    const uint64_t x = xk[i];
+    ++c;
+    mn = x < mn ? x : mn;
+    mx = x > mx ? x : mx;
+  }
+  uint32_t* h0 = hbuf;
+  uint32_t* h1 = hbuf + SEL_NW * 256;
+  for (int i = tid; i < SEL_NW * 256; i += SEL_NT) h0[i] = 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  mn = wave_min_u64(mn);
+  mx = wave_max_u64(mx);
+  if (lane == 0) {
+    s_mm[wave] = mn;
+    s_mm[SEL_NW + wave] = mx;
+    s_cnt[wave] = c;
+  }
+  __syncthreads();
+  uint32_t M = 0;
+  mn = s_mm[0];
+  mx = s_mm[SEL_NW];
+#pragma unroll
+  for (int w = 0; w < SEL_NW; ++w) {
+    M += s_cnt[w];
+    mn = s_mm[w] < mn ? s_mm[w] : mn;
+    mx = s_mm[SEL_NW + w] > mx ? s_mm[SEL_NW + w] : mx;
+  }
+  *total = M;
+  if (M <= (uint32_t)k) return 0;
+  const int top = 63 - __builtin_clzll((mn ^ mx) | 1ull);
+  uint64_t pmask = top >= 63 ? 0ull : (~0ull << (top + 1));
+  uint64_t prefix = mn & pmask;
+  uint32_t kr = (uint32_t)k;
+  int hi = top;
+  for (int pass = 0;; ++pass) {
+    uint32_t* h = (pass & 1) ? h1 : h0;
+    uint32_t* hn = (pass & 1) ? h0 : h1;
+    const int lo = hi >= 7 ? hi - 7 : 0;
+    const uint32_t dm = (2u << (hi - lo)) - 1u;
+    uint32_t* hw = h + wave * 256;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (v[u] != 0 && (v[u] & pmask) == prefix) atomicAdd(&hw[(uint32_t)(v[u] >> lo) & dm], 1u);
+    for (uint32_t i = tid; i < xn; i += SEL_NT) {
+      const uint64_t x = xk[i];
+      if ((x & pmask) == prefix) atomicAdd(&hw[(uint32_t)(x >> lo) & dm], 1u);
+    }
+    __syncthreads();
+    if (wave == 0) {
+      uint32_t bb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < SEL_NW; ++w) t += h[w * 256 + 4 * lane + j];
+        bb[j] = t;
+      }
+      const uint32_t cnt4 = bb[0] + bb[1] + bb[2] + bb[3];
+      uint32_t suf = cnt4;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_down(suf, o, 64);
+        if (lane + o < 64) suf += t;
+      }
+      const uint32_t above = suf - cnt4;
+      if (suf >= kr && above < kr) {
+        uint32_t acc = above;
+        int sel = 4 * lane, selc = 0;
+        for (int j = 3; j >= 0; --j) {
+          if (acc + bb[j] >= kr) {
+            sel = 4 * lane + j;
+            selc = (int)bb[j];
+            break;
+          }
+          acc += bb[j];
+        }
+        s_misc[2] = (uint32_t)sel;
+        s_misc[1] = kr - acc;
+        s_misc[3] = (uint32_t)selc == kr - acc;
+      }
+    } else {
+      for (int i = tid - 64; i < SEL_NW * 256; i += SEL_NT - 64) hn[i] = 0;
+    }
+    __syncthreads();
+    prefix |= (uint64_t)s_misc[2] << lo;
+    pmask |= (uint64_t)dm << lo;
+    kr = s_misc[1];
+    const bool done = s_misc[3] || lo == 0;
+    __syncthreads();  // s_misc is rewritten by the next pass (or the next call)
+    if (done) break;
+    hi = lo - 1;
+  }
+  return prefix;
+}
+
+// Scores of up to TD docs (ids dl[0, n)) against query q, as scan_tile_kernel
+// computes them: the same MFMA sequence over the same operand bytes, the two
+// k-slice partial sums added -- bit-identical (an MFMA row's result does not
+// depend on the other rows).  Lane (r32, h) returns rows (j & 3) + 8 (j >> 2) + 4 h
+// of column 0 in acc[j] (lanes 0 and 32 hold the query's column).
+template <int D, int EB>
+__device__ __forceinline__ f32x16 rescore_docs(const unsigned char* qlds,
+                                               const unsigned char* __restrict__ docs,
+                                               const uint32_t* dl, int n, int lane) {
+  using G = Geo<D, EB>;
+  constexpr int KS = G::KS;
+  constexpr int NCW = (G::KK / KS) * EB / 2;
+  const int r32 = lane & 31, h = lane >> 5;
+  const bool live = r32 < n;
+  const unsigned char* dr = docs + (int64_t)(live ? dl[r32] : 0u) * D * EB + 16 * h;
+  const unsigned char* qr = qlds + 16 * h;
+  f32x16 tot = (f32x16)0.0f;
+#pragma unroll
+  for (int kh = 0; kh < KS; ++kh) {
+    f32x16 acc = (f32x16)0.0f;
+    u16x8 af[NCW];  // the k-slice's A fragments, all in flight at once
+#pragma unroll
+    for (int c = 0; c < NCW; ++c)
+      af[c] = live ? *reinterpret_cast<const u16x8*>(dr + kh * (D * EB / KS) + c * 32) : (u16x8)0;
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) {
+      const int off = kh * (D * EB / KS) + c * 32;
+      const u16x8 av = af[c];
+      u16x8 bv = *reinterpret_cast<const u16x8*>(qr + off);
+      if (r32 != 0) bv = (u16x8)0;
+      if constexpr (EB == 2) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av),
+                                                      __builtin_bit_cast(bf16x8, bv), acc, 0, 0, 0);
+      } else {
+        typedef long l2 __attribute__((ext_vector_type(2)));
+        const l2 a2 = __builtin_bit_cast(l2, av), b2 = __builtin_bit_cast(l2, bv);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a2[0], b2[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a2[1], b2[1], acc, 0, 0, 0);
+      }
+    }
+    if (kh == 0) tot = acc;
+    else tot += acc;  // the filter's exchange: fl(half 0 + half 1), commutative
+  }
+  return tot;
+}
+
+template <int D, int EB>
+__global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
+  using G = Geo<D, EB>;
+  constexpr int NSL = 2 * G::KS;
+  constexpr int U = SEL_STAGE / SEL_NT;
+  constexpr int MAXW = SEL_STAGE / (LT_M * 2);  // workers (NSL >= 2)
+  __shared__ uint32_t hbuf[2 * SEL_NW * 256];
+  __shared__ uint64_t cand[SEL_MAXK];
+  __shared__ uint64_t xk[SD_XCAP];
+  __shared__ uint64_t s_mm[2 * SEL_NW];
+  __shared__ uint32_t s_cnt[SEL_NW];
+  __shared__ uint32_t s_misc[4];
+  __shared__ uint32_t s_xn, s_coll, s_nv;
+  __shared__ uint32_t vflag[MAXW];  // per worker: tile rows of its truncated lists
+  __shared__ uint16_t vw[MAXW];
+  __shared__ __attribute__((aligned(16))) unsigned char qlds[D * EB];
+  __shared__ uint32_t dl[SD_DCAP];  // docs to rescore
+  __shared__ uint32_t s_nd;
+  const int q = blockIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int M4 = a.LS * LT_M;
+  const uint64_t* L = a.lists + (int64_t)q * M4;
+  uint64_t v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = tid + u * SEL_NT;
+    v[u] = i < M4 ? L[i] : 0ull;
+  }
+  const int nworkers = a.LS / NSL;
+  for (int w = tid; w < nworkers; w += SEL_NT) vflag[w] = 0;
+  if (tid == 0) {
+    s_xn = 0;
+    s_coll = 0;
+    s_nv = 0;
+  }
+  uint32_t M = 0;
+  uint64_t kth = dense_kth<U>(v, xk, 0, a.k, hbuf, s_mm, s_cnt, s_misc, &M);
+  // lists whose last slot could have pushed out a winner -> the tile rows they
+  // cover (slice kh * 2 + h: rows (j & 3) + 8 (j >> 2) + 4 h, j in kh's half)
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = tid + u * SEL_NT;
+    if ((i & (LT_M - 1)) == LT_M - 1 && i < M4 && v[u] != 0 && v[u] >= kth) {
+      const int sl = (i / LT_M) % NSL, kh = sl >> 1, hh = sl & 1;
+      constexpr int JPW = 16 / G::KS;
+      uint32_t rows = 0;
+      for (int j = kh * JPW; j < (kh + 1) * JPW; ++j) rows |= 1u << ((j & 3) + 8 * (j >> 2) + 4 * hh);
+      atomicOr(&vflag[(i / LT_M) / NSL], rows);
+    }
+  }
+  __syncthreads();
+  for (int w = tid; w < nworkers; w += SEL_NT)
+    if (vflag[w]) vw[atomicAdd(&s_nv, 1u)] = (uint16_t)w;
+  __syncthreads();
+  const int nv = (int)s_nv;
+#ifdef IRC_SCAN_STAMPS  // diagnostic: rescanned workers, queries with a rescan
+  if (tid == 0) {
+    atomicAdd((unsigned long long*)&dbg_stamps[3][30], (unsigned long long)nv);
+    atomicAdd((unsigned long long*)&dbg_stamps[3][31], (unsigned long long)(nv > 0));
+  }
+#endif
+  if (nv > 0) {  // block-uniform
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // truncated lists: replaced by the rescan of their rows
+      const int i = tid + u * SEL_NT;
+      if (i < M4 && vflag[(i / LT_M) / NSL] != 0) {
+        const int sl = (i / LT_M) % NSL, kh = sl >> 1, hh = sl & 1;
+        constexpr int JPW = 16 / G::KS;
+        const int j0 = kh * JPW;  // any row of the slice identifies it
+        if ((vflag[(i / LT_M) / NSL] >> ((j0 & 3) + 8 * (j0 >> 2) + 4 * hh)) & 1u) v[u] = 0;
+      }
+    }
+    uint64_t thr = kth;
+    const int ntiles = (a.NS + TD - 1) / TD;
+    const int units = nv * a.tpw;  // (violated worker, tile) pairs
+    {  // the query row, read by every rescan from LDS
+      const unsigned char* qrow = a.queries + (int64_t)q * D * EB;
+      for (int i = tid; i < D * EB / 16; i += SEL_NT)
+        reinterpret_cast<u16x8*>(qlds)[i] = reinterpret_cast<const u16x8*>(qrow)[i];
+    }
+    // phases of <= SD_DCAP / TD units: list the docs of the truncated lists' rows,
+    // then score them in dense 32-doc MFMA tiles, SEL_NW tiles per round
+    for (int u0 = 0; u0 < units; u0 += SD_DCAP / TD) {
+      if (tid == 0) s_nd = 0;
+      __syncthreads();
+      const int u1 = u0 + SD_DCAP / TD < units ? u0 + SD_DCAP / TD : units;
+      for (int u = u0 + tid; u < u1; u += SEL_NT) {
+        const int w = vw[u / a.tpw];
+        const int tile = w * a.tpw + u % a.tpw;
+        if (tile >= ntiles) continue;
+        uint32_t rows = vflag[w];
+        const int rem = a.NS - tile * TD;
+        if (rem < TD) rows &= (1u << rem) - 1u;
+        uint32_t o = atomicAdd(&s_nd, (uint32_t)__popc(rows));
+        while (rows) {
+          const int r = __builtin_ctz(rows);
+          rows &= rows - 1u;
+          dl[o++] = (uint32_t)(tile * TD + r);
+        }
+      }
+      __syncthreads();
+      const int nd = (int)s_nd;
+      for (int c0 = 0; c0 < nd; c0 += SEL_NW * TD) {
+        if (s_xn + SEL_NW * TD > (uint32_t)SD_XCAP) {
+          // cut the union to its k-th key: a higher bound, at most k keys kept in xk
+          uint32_t tot;
+          const uint64_t kc = dense_kth<U>(v, xk, s_xn, a.k, hbuf, s_mm, s_cnt, s_misc, &tot);
+          thr = kc > thr ? kc : thr;
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (v[u] < thr) v[u] = 0;
+          const uint32_t xn0 = s_xn;
+          for (uint32_t i = tid; i < xn0; i += SEL_NT)
+            if (xk[i] >= thr) cand[atomicAdd(&s_coll, 1u)] = xk[i];
+          __syncthreads();
+          const uint32_t nk = s_coll;
+          for (uint32_t i = tid; i < nk; i += SEL_NT) xk[i] = cand[i];
+          __syncthreads();
+          if (tid == 0) {
+            s_xn = nk;
+            s_coll = 0;
+          }
+          __syncthreads();
+        }
+        const int c = c0 + wave * TD;
+        if (c < nd) {
+          const int n = nd - c < TD ? nd - c : TD;
+          const f32x16 sc = rescore_docs<D, EB>(qlds, a.docs, dl + c, n, lane);
+          if ((lane & 31) == 0) {
+            const int h = lane >> 5;
+            uint64_t kk[16];
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              const int r = (j & 3) + 8 * (j >> 2) + 4 * h;
+              kk[j] = r < n ? make_key(sc[j], a.idx_base + dl[c + r]) : 0ull;
+              cnt += (int)(kk[j] != 0 && kk[j] >= thr);
+            }
+            uint32_t o = cnt ? atomicAdd(&s_xn, (uint32_t)cnt) : 0u;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+              if (kk[j] != 0 && kk[j] >= thr) xk[o++] = kk[j];
+          }
+        }
+        __syncthreads();
+      }
+    }
+    kth = dense_kth<U>(v, xk, s_xn, a.k, hbuf, s_mm, s_cnt, s_misc, &M);
+  }
+  // collect the exactly min(M, k) keys >= kth, then place them by rank
+  const uint32_t xn = s_xn;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const bool take = v[u] != 0 && v[u] >= kth;
+    const uint64_t bal = __ballot(take);
+    if (bal != 0) {
+      uint32_t b0 = 0;
+      if (lane == 0) b0 = atomicAdd(&s_coll, (uint32_t)__popcll(bal));
+      b0 = __shfl(b0, 0, 64);
+      if (take) cand[b0 + __popcll(bal & ((1ull << lane) - 1))] = v[u];
+    }
+  }
+  for (uint32_t i = tid; i < xn; i += SEL_NT)
+    if (xk[i] >= kth) cand[atomicAdd(&s_coll, 1u)] = xk[i];
+  __syncthreads();
+  const int k = a.k;  // <= SEL_NT (make_plan): one winner per thread at most
+  const int cnt = (int)(M < (uint32_t)k ? M : (uint32_t)k);
+  {
+    for (int i = tid; i < k; i += SEL_NT) {
+      float sc = -__builtin_huge_valf();
+      int64_t id = -1;
+      int pos = i;
+      if (i < cnt) {
+        const uint64_t key = cand[i];
+        int rank = 0;
+        for (int j = 0; j < cnt; ++j) rank += (int)(cand[j] > key);
+        pos = rank;
+        sc = unorderable_f32((uint32_t)(key >> 32)) * a.smul;
+        id = (int64_t)(uint32_t)(~(uint32_t)key);
+      }
+      a.out_score[(int64_t)q * k + pos] = sc;
+      a.out_idx[(int64_t)q * k + pos] = id;
+    }
+  }
+}
+
 // The 256-thread select_kernel is the default: measured on MI355X (100k x 768,
 // k=100) the wave-per-query variant made the whole call 40 us slower at Q=1 and
 // 35 us slower at Q=256 (one wave walks every region and every radix pass alone).
@@ -1045,6 +1698,9 @@ struct Plan {
   int64_t cap_s;
   int g_f, tpw_f;
   int64_t cap_f;
+  // single-pass LTOP scan + select_dense (no sample, no threshold select)
+  bool ltop;
+  int ls;  // lists per query
   // filter pass on the ping-pong GEMM (Q >= pp_min_q): regions = 256-doc tiles
   bool pp;
   int pp_G, pp_qpad;
@@ -1070,6 +1726,28 @@ static int pp_min_q() {
     if (e && e[0] == '0') return 1 << 30;
     const char* m = getenv("IRC_SCAN_PP_MINQ");
     return m ? atoi(m) : 192;
+  }();
+  return v;
+}
+
+// IRC_SCAN_LTOP=0 keeps the sampled-threshold pipeline where LTOP would apply.
+static bool ltop_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("IRC_SCAN_LTOP");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// LTOP up to IRC_SCAN_LTOP_MAXQ queries (default 64).  C2 corpus (100k x 768) on
+// MI355X, whole call: Q = 1 / 16 / 32 / 64: 51.4 / 56.5 / 58.4 / 61.9 us against
+// 60.0 / 64.9 / 67.3 / 71.5 with the sampled threshold; at Q = 128 the list
+// insertions (+10 us in the filter) and an occasional rescan (~1 query of 128 on
+// Gaussian data, ~12 us) cancel the gain (84.6 vs 83.1).
+static int ltop_max_q() {
+  static const int v = [] {
+    const char* e = getenv("IRC_SCAN_LTOP_MAXQ");
+    return e ? atoi(e) : 64;
   }();
   return v;
 }
@@ -1181,6 +1859,15 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
     if (pc > cnt_bytes) cnt_bytes = pc;
     if (pp_keys > key_bytes) key_bytes = pp_keys;
   }
+  // LTOP where the GEMM filter does not run and all lists fit one select stage
+  p.ls = p.g_f * 2 * p.ks;
+  p.ltop = !p.pp && ltop_enabled() && Q <= ltop_max_q() && (int64_t)p.ls * LT_M <= SEL_STAGE &&
+           k <= SEL_NT;
+  if (p.ltop) {
+    p.two_phase = false;
+    const size_t lb = (size_t)p.qpad * p.ls * LT_M * 8;
+    if (lb > key_bytes) key_bytes = lb;
+  }
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const int qthr = p.pp && p.pp_qpad > p.qpad ? p.pp_qpad : p.qpad;
   p.off_thr = 0;
@@ -1248,6 +1935,28 @@ static int dispatch_tile(int eb, int64_t D, const Plan& p, int g, const void* qs
                                    counts, cap, scores, st);
 }
 
+template <int EB>
+static void launch_dense_eb(int64_t D, int Q, const DenseArgs& a, hipStream_t st) {
+#define IRC_DENSE_CASE(DD)                                                                 \
+  case DD:                                                                                 \
+    hipLaunchKernelGGL((select_dense_kernel<DD, EB>), dim3((unsigned)Q), dim3(SEL_NT), 0, st, a); \
+    break;
+  switch (D) {
+    IRC_DENSE_CASE(64)
+    IRC_DENSE_CASE(128)
+    IRC_DENSE_CASE(256)
+    IRC_DENSE_CASE(384)
+    IRC_DENSE_CASE(512)
+    IRC_DENSE_CASE(768)
+    default: IRC_DENSE_CASE(1024)
+  }
+#undef IRC_DENSE_CASE
+}
+static void launch_dense(int eb, int64_t D, int Q, const DenseArgs& a, hipStream_t st) {
+  if (eb == 1) launch_dense_eb<1>(D, Q, a, st);
+  else launch_dense_eb<2>(D, Q, a, st);
+}
+
 static bool supported_d(int64_t D) {
   return D == 64 || D == 128 || D == 256 || D == 384 || D == 512 || D == 768 || D == 1024;
 }
@@ -1290,11 +1999,23 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
   const uint32_t base = (uint32_t)doc_offset;
   const double alg_bytes = (double)N * D * eb + (double)Q * D * eb;
   int rc;
+  if (p.ltop) {
+    prof_begin(st);
+    rc = dispatch_tile<LTOP>(eb, D, p, p.g_f, queries, docs, (int)Q, N, 1, p.tpw_f, base, nullptr,
+                             keys, cnt, p.ls, nullptr, st);
+    prof_end("scan_filter", st, alg_bytes);
+    if (rc) return rc;
+    DenseArgs da{keys, static_cast<const unsigned char*>(queries),
+                 static_cast<const unsigned char*>(docs), p.ls, (int)N, p.tpw_f, base, (int)k, smul,
+                 out_score, out_idx};
+    launch_dense(eb, D, (int)Q, da, st);
+    return check_launch("select_dense_kernel");
+  }
   if (p.two_phase) {
     rc = dispatch_tile<GMAX>(eb, D, p, p.g_s, queries, docs, (int)Q, p.S, p.stride, p.tpw_s,
                              base, nullptr, keys, cnt, p.cap_s, nullptr, st);
     if (rc) return rc;
-    RegionSource s1{keys, cnt, p.g_s, p.qpad, p.cap_s, 2 * p.ks};
+    const RegionSource s1 = region_source(keys, cnt, p.g_s, p.qpad, p.cap_s, 2 * p.ks);
     launch_select(s1, (int)Q, (int)k, SEL_THRESHOLD, thr, nullptr, nullptr, 1.0f, st);
     if ((rc = check_launch("select_kernel(threshold)"))) return rc;
   }
@@ -1322,8 +2043,11 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
     gpp::run_scan(a, st, eb == 1);
     prof_end("scan_filter", st, alg_bytes);
     if ((rc = check_launch("gemm_pp_kernel(scan)"))) return rc;
-    RegionSource s2{keys, cnt, p.pp_G, p.pp_qpad, p.pp_cap, 1};
+    const RegionSource s2 = region_source(keys, cnt, p.pp_G, p.pp_qpad, p.pp_cap, 1);
     launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
+#ifdef IRC_SCAN_DOUBLE_SELECT  // diagnostic: the same (idempotent) select again, I-cache warm
+    launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
+#endif
     return check_launch("select_kernel(final)");
   }
   prof_begin(st);
@@ -1331,8 +2055,11 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
                            p.two_phase ? thr : nullptr, keys, cnt, p.cap_f, nullptr, st);
   prof_end("scan_filter", st, alg_bytes);  // algorithmic bytes
   if (rc) return rc;
-  RegionSource s2{keys, cnt, p.g_f, p.qpad, p.cap_f, 2 * p.ks};
+  const RegionSource s2 = region_source(keys, cnt, p.g_f, p.qpad, p.cap_f, 2 * p.ks);
   launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
+#ifdef IRC_SCAN_DOUBLE_SELECT
+  launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
+#endif
   return check_launch("select_kernel(final)");
 }
 

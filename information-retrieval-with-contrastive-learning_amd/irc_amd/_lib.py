@@ -13,7 +13,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libirc_hip.so")
 # IRC_LIB_PATH: load a differently built copy (A/B experiments of kernel variants)
-LIB_PATH = os.environ.get("IRC_LIB_PATH", LIB_PATH)
+LIB_PATH = os.environ.get("IRC_LIB_PATH") or LIB_PATH
 
 _c = ctypes
 P = _c.c_void_p

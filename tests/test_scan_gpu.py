@@ -173,6 +173,42 @@ def test_full_c2_size_properties(gpu):
     assert torch.equal(i, i2) and torch.equal(s, s2)
 
 
+@pytest.mark.parametrize("Q,D,fp8", [(1, 768, False), (16, 768, False), (64, 256, False),
+                                      (40, 768, True)])
+def test_clustered_corpus_rescan_properties(gpu, Q, D, fp8):
+    """A block of 600 consecutive docs aligned with the queries: ~25 winners per
+    worker there, so the single-pass scan's 4-key lists overflow and
+    select_dense must rescan those workers.  Scores bit-exact with the scan's
+    own MFMA scores, complete, sorted, ties to the lower index."""
+    from irc_amd import retrieval
+
+    g = torch.Generator().manual_seed(7)
+    N, k = 40_000, 100
+    unit = lambda x: torch.nn.functional.normalize(x, dim=-1)  # noqa: E731
+    base = unit(torch.randn(D, generator=g))
+    q = unit(base + 0.5 * unit(torch.randn(Q, D, generator=g)))
+    d = unit(torch.randn(N, D, generator=g))
+    d[17_000:17_600] = unit(base + 0.5 * unit(torch.randn(600, D, generator=g)))
+    if fp8:
+        qq = retrieval.quantize_fp8(q.to(gpu))
+        dd = retrieval.quantize_fp8(d.to(gpu))
+        s, i = retrieval.scan_topk_fp8(qq, dd, k, 0, 1.0 / 256)
+        full = retrieval.scan_scores_fp8(qq, dd) * (1.0 / 256)
+    else:
+        qq, dd = q.bfloat16().to(gpu), d.bfloat16().to(gpu)
+        s, i = retrieval.scan_topk(qq, dd, k)
+        full = retrieval.scan_scores(qq, dd)
+    assert bool((i >= 0).all()) and bool((i < N).all())
+    assert bool(((i >= 17_000) & (i < 17_600)).all())  # the block wins
+    assert torch.equal(s, torch.gather(full, 1, i))
+    assert bool((s[:, 1:] <= s[:, :-1]).all())
+    tie = s[:, 1:] == s[:, :-1]
+    assert bool((i[:, 1:][tie] > i[:, :-1][tie]).all())
+    masked = full.clone()
+    masked.scatter_(1, i, float("-inf"))
+    assert bool((masked.max(dim=1).values <= s[:, -1]).all())
+
+
 def test_search_many_equals_serial_search(gpu):
     """Pipelined batches (search_many, 2 streams, own workspaces) return exactly
     what serial search() calls return."""
