@@ -1807,6 +1807,18 @@ static void plan_workers(int64_t ntiles, int gy, int64_t D, int eb, int nw, int*
 // and 98 / 115 / 296 at 32, tools/g4.sh).
 // Any value keeps the result exact (the threshold is the 2*KS-th group maximum of real
 // scores); it trades the sample pass against the filter's survivor count.
+// Minimum tiles per sample worker (IRC_SCAN_SAMPLE_TPW, default 1 = plan_workers'
+// choice).  Fewer, longer workers amortise each workgroup's query-fragment loads
+// but lose parallelism: C2 whole call at Q = 256 92.5 / 93.5 / 96.1 / 102.1 us for
+// 1 / 3 / 5 / 8 (MI355X).
+static int sample_min_tpw() {
+  static const int v = [] {
+    const char* e = getenv("IRC_SCAN_SAMPLE_TPW");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 static int64_t sample_div() {
   static const int64_t v = [] {
     const char* e = getenv("IRC_SCAN_SAMPLE_DIV");
@@ -1839,6 +1851,11 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   p.two_phase = p.stride > 1;
   p.S = p.two_phase ? (N + p.stride - 1) / p.stride : N;
   plan_workers((p.S + TD - 1) / TD, p.gy, D, eb, p.nw, &p.g_s, &p.tpw_s);
+  if (p.tpw_s < sample_min_tpw()) {  // fewer, longer sample workers (query loads amortised)
+    const int64_t st = (p.S + TD - 1) / TD;
+    p.tpw_s = sample_min_tpw();
+    p.g_s = (int)(((st + p.tpw_s - 1) / p.tpw_s + 7) / 8 * 8);
+  }
   p.cap_s = (int64_t)p.tpw_s * TD;
   plan_workers((N + TD - 1) / TD, p.gy, D, eb, p.nw, &p.g_f, &p.tpw_f);
   p.cap_f = (int64_t)p.tpw_f * TD;
