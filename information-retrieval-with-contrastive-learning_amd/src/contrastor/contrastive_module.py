@@ -90,27 +90,46 @@ class RetrievalModelWrapper(nn.Module):
         return out[:n_anchor], out[n_anchor:]
 
     @torch.no_grad()
-    def bert_extract_async(self, input_ids, attention_mask, n_anchor):
+    def bert_extract_async(self, input_ids, attention_mask, n_anchor, inputs_ready=False):
         """bert_extract_ids issued on the "bert_prefetch" side stream.
 
         BERT is frozen (contrastive_module.py:34-36: no_grad, eval, never in the
         optimizer), so the features of micro-batch t+1 do not depend on the heads'
         update of micro-batch t: issuing them here, before the heads' step of
         micro-batch t is enqueued, lets the BERT GEMMs fill the CUs the
-        latency-bound BiLSTM recurrences leave idle.  The side stream first waits
-        for the work already on the current stream (the inputs' producers).
-        Returns a handle for features_ready()."""
+        latency-bound BiLSTM recurrences leave idle.
+
+        inputs_ready=False (default): the inputs may have just been produced on the
+        current stream, so the side stream first waits for everything queued there
+        -- including the previous micro-batch's backward, which serialises BERT
+        behind it (on MI355X the side stream then idled ~2.5 ms of a 10 ms C2 step).
+        inputs_ready=True: the inputs are already complete (resident, or produced on
+        the side stream as in bert_extract_texts_async): no wait.  Returns a handle
+        for features_ready()."""
         dev = input_ids.device
         cur = torch.cuda.current_stream(dev)
         side = side_stream(dev, "bert_prefetch")
-        side.wait_stream(cur)
+        if not inputs_ready:
+            side.wait_stream(cur)
         with torch.cuda.stream(side):
             out = self.bert_model.encode(input_ids, attention_mask)
             done = torch.cuda.Event()
             done.record(side)
-        input_ids.record_stream(side)
-        attention_mask.record_stream(side)
+        if side != cur:
+            input_ids.record_stream(side)
+            attention_mask.record_stream(side)
         return out, int(n_anchor), done
+
+    @torch.no_grad()
+    def bert_extract_texts_async(self, anchors, positives, device):
+        """Tokenise (GPU WordPiece + joint padding) AND encode on the "bert_prefetch"
+        side stream: the features of the next micro-batch depend on nothing the
+        current stream is doing.  Returns a handle for features_ready()."""
+        dev = torch.device(device)
+        side = side_stream(dev, "bert_prefetch")
+        with torch.cuda.stream(side):
+            ids, mask = self.tokenize(list(anchors) + list(positives), dev)
+        return self.bert_extract_async(ids, mask, len(anchors), inputs_ready=True)
 
     @staticmethod
     def features_ready(handle):

@@ -188,8 +188,7 @@ def train(args):
 
     def _issue(b):
         idx, a, p = b
-        ids, mask = model.tokenize(list(a) + list(p), args.device)
-        return idx, model.bert_extract_async(ids, mask, len(a))
+        return idx, model.bert_extract_texts_async(a, p, args.device)
 
     while st.step_sum < total_steps:
         it = iter(train_loader)

@@ -83,7 +83,11 @@ def _replay(gpu, precision, pipelined=False, fixture="train_traj.npz"):
                 handle = pending
                 if i + 1 < n_mb:
                     nb1, ids1, mask1 = batch(i + 1)
-                    pending = model.bert_extract_async(ids1, mask1, nb1)
+                    if pipelined == "ready":  # resident inputs: no wait on the heads' work
+                        torch.cuda.current_stream(gpu).synchronize()
+                        pending = model.bert_extract_async(ids1, mask1, nb1, inputs_ready=True)
+                    else:
+                        pending = model.bert_extract_async(ids1, mask1, nb1)
                 loss, _ = st.micro_batch(
                     nb, lambda: model.forward_features(*model.features_ready(handle)))
             else:
@@ -125,12 +129,13 @@ def test_train_trajectory_bf16(gpu):
     np.testing.assert_allclose(losses, fx["mb_loss"], rtol=5e-3)
 
 
-def test_train_pipelined_bert_prefetch_matches_sequential(gpu):
+@pytest.mark.parametrize("mode", [True, "ready"])
+def test_train_pipelined_bert_prefetch_matches_sequential(gpu, mode):
     """bert_extract_async (the next micro-batch's frozen-BERT features on a side
     stream, as src/train.py and bench.py run it) changes only the overlap, never
     the numbers: losses and final parameters bit-identical to the sequential loop."""
     fx, seq_losses, seq_model = _replay(gpu, "bf16")
-    _, pipe_losses, pipe_model = _replay(gpu, "bf16", pipelined=True)
+    _, pipe_losses, pipe_model = _replay(gpu, "bf16", pipelined=mode)
     np.testing.assert_array_equal(pipe_losses, seq_losses)
     a, b = seq_model.state_dict(), pipe_model.state_dict()
     for k in a:

@@ -1,4 +1,11 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
-L=$GRAFT_REPO_ROOT/information-retrieval-with-contrastive-learning_amd/irc_amd/lib/variants/stamps.so
-IRC_LIB_PATH=$L timeout -k 10 120 python tools/dense_stats.py --q 1 16 64 2>&1 | grep -v amdgpu.ids || exit 1
-timeout -k 10 120 python3 tools/scan_bench.py --reps 100 --q 1 16 32 64 2>&1 | grep -v amdgpu.ids || exit 1
+mkdir -p gpurun_out
+for i in 1 2; do
+  timeout -k 10 200 python bench.py --part scan --no-cpu-baseline > gpurun_out/bs$i.log 2>&1 || exit 1
+  python - "$i" <<'PY'
+import json, sys
+d = json.loads(open(f"gpurun_out/bs{sys.argv[1]}.log").read().strip().splitlines()[-1])
+r = d["retrieval"]["call_level"]
+print(r["serial_us_per_call"], r["pipelined_us_per_batch"])
+PY
+done
