@@ -19,7 +19,13 @@ import bench  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--prio", action="store_true",
+                    help="heads (and their side streams) on high-priority streams")
     a = ap.parse_args()
+    if a.prio:
+        from irc_amd import _torch as T
+
+        T.HIGH_PRIORITY_TAGS = ("key_encoder", "lstm_wgrad", "heads")
     from src.model import build_model, get_optimizer
     from src.train import TrainState
 
@@ -34,11 +40,17 @@ def main():
     ids, mask = ids.to(dev), mask.to(dev)
     pending = [model.bert_extract_async(ids, mask, bench.TRAIN_B)]
 
+    from irc_amd._torch import side_stream
+
+    hs = side_stream(dev, "heads") if a.prio else torch.cuda.current_stream(dev)
+
     def step():
         handle = pending[0]
         pending[0] = model.bert_extract_async(ids, mask, bench.TRAIN_B, inputs_ready=True)
-        st.micro_batch(bench.TRAIN_B, lambda: model.forward_features(*model.features_ready(handle)),
-                       sync_loss=False)
+        with torch.cuda.stream(hs):
+            st.micro_batch(bench.TRAIN_B,
+                           lambda: model.forward_features(*model.features_ready(handle)),
+                           sync_loss=False)
 
     def timed(fn, n):
         for _ in range(3):
@@ -56,6 +68,38 @@ def main():
     h_ms = timed(lambda: st.micro_batch(bench.TRAIN_B, lambda: model.forward_features(*feats),
                                         sync_loss=False), 10)
     print(f"BERT forward alone {b_ms:.2f} ms, heads step alone {h_ms:.2f} ms")
+    # BERT side-stream spans: an event before each encode and its done event
+    spans = []
+    from irc_amd._torch import side_stream as _ss
+
+    bside = _ss(dev, "bert_prefetch")
+
+    def step_ev():
+        handle = pending[0]
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(bside)
+        pending[0] = model.bert_extract_async(ids, mask, bench.TRAIN_B, inputs_ready=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(bside)
+        spans.append((e0, e1))
+        with torch.cuda.stream(hs):
+            st.micro_batch(bench.TRAIN_B,
+                           lambda: model.forward_features(*model.features_ready(handle)),
+                           sync_loss=False)
+
+    for _ in range(5):
+        step_ev()
+    torch.cuda.synchronize()
+    spans.clear()
+    tw = time.perf_counter()
+    for _ in range(a.steps):
+        step_ev()
+    torch.cuda.synchronize()
+    wall_ev = (time.perf_counter() - tw) / a.steps * 1e3
+    busy = [s0.elapsed_time(s1) for s0, s1 in spans]
+    gaps = [spans[i][1].elapsed_time(spans[i + 1][0]) for i in range(len(spans) - 1)]
+    print(f"with side-stream events: wall {wall_ev:.2f} ms/step; BERT encode span "
+          f"{sum(busy) / len(busy):.2f} ms, gap between encodes {sum(gaps) / len(gaps):.3f} ms")
     for _ in range(5):
         step()
     torch.cuda.synchronize()
