@@ -394,10 +394,13 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
   }
 }
 
-// C[b][m][n] (=|+=) alpha * sum_s P[b][s][m][n]  (s ascending: deterministic)
+// C[b][m][n] (=|+=) alpha * sum_s P[b][s][m][n] (+ bias[b][n])  (s ascending:
+// deterministic; the bias is the EPI_BIAS epilogue of an fp32 GEMM that was split)
 __global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restrict__ C, int M,
                                      int N, int S, int64_t ldc, int64_t sC, int batch,
-                                     float alpha, int accumulate) {
+                                     float alpha, int accumulate,
+                                     const float* __restrict__ bias = nullptr,
+                                     int64_t sBias = 0) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t mn = (int64_t)M * N;
   if (e >= mn * batch) return;
@@ -406,21 +409,26 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restr
   const float* p = P + (int64_t)b * S * mn + r;
   float s = 0.f;
   for (int k = 0; k < S; ++k) s += p[k * mn];
+  float v = alpha * s;
+  if (bias) v += bias[b * sBias + (r % N)];
   float* dst = C + b * sC + (r / N) * ldc + (r % N);
-  *dst = accumulate ? *dst + alpha * s : alpha * s;
+  *dst = accumulate ? *dst + v : v;
 }
 
 // Split-K count: only when the output tile grid cannot fill the chip and each
-// slice keeps >= 512 of K.  Restricted to fp32 C with no fused epilogue.
+// slice keeps >= 512 of K (bf16) / >= 128 of K (fp32: the exact-fp32 MFMA runs at
+// 1/16 of the bf16 rate, so a 128-deep slice is already 8 K-steps of real work --
+// the InfoNCE / scaling-layer GEMMs of the heads' step ran on 2-4 workgroups for
+// 50-100 us each before).  Restricted to fp32 C with no fused epilogue.
 inline int split_count(int TIbytes, int out_f32, int epi, int64_t M, int64_t N, int64_t K,
                        int64_t batch) {
-  if (!out_f32 || epi != EPI_NONE) return 1;
+  if (!out_f32 || !(epi == EPI_NONE || (epi == EPI_BIAS && TIbytes == 4))) return 1;
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch;
   const int bk = TIbytes == 2 ? TT<unsigned short>::BK : TT<float>::BK;
   int64_t s = (512 + tiles - 1) / tiles;
-  const int64_t smax = K / 512;
+  const int64_t smax = K / (TIbytes == 2 ? 512 : 128);
   if (s > smax) s = smax;
-  if (s > 32) s = 32;
+  if (s > (TIbytes == 2 ? 32 : 64)) s = TIbytes == 2 ? 32 : 64;
   if (s < 2) return 1;
   // equalise slices on BK boundaries; drop empty trailing slices
   const int64_t chunk = ((K + s - 1) / s + bk - 1) / bk * bk;
@@ -714,7 +722,7 @@ static int launch(const Args& g0, int batch, int splits, hipStream_t st) {
     const int64_t n = (int64_t)g.M * g.N * batch;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                        g.P, reinterpret_cast<float*>(g.C), g.M, g.N, splits, g.ldc, g.sC, batch,
-                       g.alpha, g.accumulate);
+                       g.alpha, g.accumulate, EPI == EPI_BIAS ? g.bias : nullptr, g.sBias);
   }
   prof_end(sizeof(TI) == 2 ? "gemm_bf16" : "gemm_f32", st, 2.0 * g.M * g.N * g.K * batch);
   return check_launch("gemm_kernel");
@@ -724,7 +732,8 @@ template <typename TI, typename TO, int LA, int LB>
 static int by_epi(int epi, const Args& g, int batch, int splits, hipStream_t st) {
   switch (epi) {
     case EPI_NONE: return launch<TI, TO, LA, LB, EPI_NONE>(g, batch, splits, st);
-    case EPI_BIAS: return launch<TI, TO, LA, LB, EPI_BIAS>(g, batch, 1, st);
+    case EPI_BIAS:  // split only for fp32 operands (split_count); the reduce adds the bias
+      return launch<TI, TO, LA, LB, EPI_BIAS>(g, batch, sizeof(TI) == 4 ? splits : 1, st);
     case EPI_BIAS_GELU: return launch<TI, TO, LA, LB, EPI_BIAS_GELU>(g, batch, 1, st);
     case EPI_BIAS_RESID: return launch<TI, TO, LA, LB, EPI_BIAS_RESID>(g, batch, 1, st);
     case EPI_RESID: return launch<TI, TO, LA, LB, EPI_RESID>(g, batch, 1, st);
