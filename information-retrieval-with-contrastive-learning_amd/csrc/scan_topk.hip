@@ -362,11 +362,13 @@ void scan_tile_kernel(
     } else if (MODE == LTOP) {
       // candidates: scores >= the list's last score; one per lane per round
       // (rounds = the wave's largest candidate count; after the first tiles
-      // mostly 0-2).  Measured alternatives that ran slower on MI355X: one
-      // insertion step per slot with any candidate (the select chain saved, more
-      // steps at Q >= 16), a select tree + position-compare insertion (more
-      // instructions), a floor shared with the h-partner lane (select_dense
-      // slower).
+      // mostly 0-2).  Measured alternatives on MI355X: one insertion step per slot
+      // with any candidate (the select chain saved, more steps at Q >= 16), a
+      // select tree + position-compare insertion (more instructions) and a floor
+      // shared with the h-partner lane (select_dense slower) were slower; a fixed
+      // merge network (sorted 4-runs + top-4 merges) for tiles where some lane has
+      // 3+ candidates gave C2 calls of 55.3 / 55.8 / 56.5 / 59.6 us at Q = 1 / 16 /
+      // 32 / 64 against 51.4 / 56.5 / 58.4 / 61.9 with rounds only -- not kept.
       uint32_t pm = 0;
 #pragma unroll
       for (int jj = 0; jj < JPW; ++jj) pm |= (uint32_t)(!(fin[jj] < ltf)) << jj;
