@@ -101,6 +101,16 @@ def _prof(lib, name):
     return tot.value / 1e3, cnt.value, work.value  # seconds, launches, work
 
 
+def _alg_bytes(lib, traffic):
+    """Algorithmic HBM bytes per bf16 GEMM launch of the last profiled pass (operands
+    read once, C written once, residual read once: gemm.hip gemm_alg_bytes) and the
+    PMC traffic's ratio to them (same dispatch set: the bench part's GEMM launches)."""
+    _, n, b = _prof(lib, "gemm_bf16_bytes")
+    per = b / n if n else None
+    return {"alg_bytes_per_launch": per,
+            "traffic_over_alg": (traffic / per) if (traffic and per) else None}
+
+
 def _max_over_ranks(x, dev, world):
     if world == 1:
         return x
@@ -214,6 +224,7 @@ def run_train(args, rank, world, dev, weights="bf16"):
         torch.cuda.synchronize()
     lib.irc_prof_enable(0)
     g_s, g_n, g_flops = _prof(lib, gname)
+    g_bytes = _alg_bytes(lib, _pmc_traffic(gname) if weights == "bf16" else None)
     flops_pair = 2 * model.bert_model.flops_per_sequence(TRAIN_L) + _lstm_flops_per_pair(cfg)
     pairs = TRAIN_B * args.steps * world
     achieved = g_flops / g_s / 1e12 if g_s > 0 else None
@@ -237,6 +248,7 @@ def run_train(args, rank, world, dev, weights="bf16"):
                      "launches_per_step": g_n / args.steps,
                      "gemm_ms_per_step": g_s * 1e3 / args.steps,
                      "alg_flops_per_step": g_flops / args.steps,
+                     **(g_bytes if weights == "bf16" else {}),
                      "live_overlapped": {
                          "achieved": live_flops / live_s / 1e12 if live_s > 0 else None,
                          "note": "timed region itself: BERT GEMMs share the chip with the "
@@ -297,6 +309,7 @@ def run_train_bert(args, rank, world, dev):
         torch.cuda.synchronize()
     lib.irc_prof_enable(0)
     g_s, g_n, g_flops = _prof(lib, "gemm_bf16")
+    g_bytes = _alg_bytes(lib, _pmc_traffic("gemm_bf16_bert"))
     enc = model.encoder_q
     D, K = enc.config.hidden_size, cfg["loss"]["InfoNCE"]["queue_size"]
     loss_flops = 3 * (2 * (2 * TRAIN_B) ** 2 * D + 2 * TRAIN_B * D * K) / TRAIN_B
@@ -321,6 +334,7 @@ def run_train_bert(args, rank, world, dev):
                      "launches_per_step": g_n / args.steps,
                      "gemm_ms_per_step": g_s * 1e3 / args.steps,
                      "alg_flops_per_step": g_flops / args.steps,
+                     **g_bytes,
                      "live_overlapped": {
                          "achieved": live_flops / live_s / 1e12 if live_s > 0 else None}},
     }

@@ -113,6 +113,14 @@ int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilog
  * gradients, K = B*L); passing a smaller/NULL workspace disables it. */
 int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M, int64_t N,
                            int64_t K, int64_t batch);
+/* Persistent tile loop of the 256x256 bf16 GEMM, for launches of more output tiles
+ * than CUs (batch 1, no split-K, aligned C): mode 0 = one workgroup per tile (the
+ * default); 1 = each workgroup takes tiles from a tile counter and DMAs the next
+ * tile's first K-tile while this tile's epilogue runs; 2 = static waves of tiles
+ * with that prestage; 3 = static waves without it.  Same arithmetic per tile, so
+ * the results are bit-identical in every mode (env IRC_GEMM_PERSIST sets the
+ * initial mode).  Returns the previous mode. */
+int irc_gemm_set_persistent(int mode);
 
 /* ------------------------------------------------------------- BERT encoder
  * Frozen BERT forward pieces (contrastive_module.py:36-41 -> HF BertModel):

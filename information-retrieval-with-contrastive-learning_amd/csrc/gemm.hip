@@ -448,6 +448,17 @@ inline int split_count(int TIbytes, int out_f32, int epi, int64_t M, int64_t N, 
 // free -- applied on the SOURCE address, since the DMA destination is
 // lane-linear.  Rows past M / N load a clamped valid row and are never stored.
 // Requires K % 64 == 0, lda/ldb % 8 == 0 and 16-byte aligned bases.
+// Algorithmic HBM bytes of one bf16 GEMM launch: both operands read once, C written
+// once (read too when accumulating), the residual / saved pre-activation read (or,
+// for the GELU-save epilogue, written) once; bias vectors ignored.
+inline double gemm_alg_bytes(int out_f32, int epi, int accumulate, int64_t M, int64_t N,
+                             int64_t K, int64_t batch) {
+  const double ob = out_f32 ? 4.0 : 2.0;
+  double b = 2.0 * (double)(M + N) * K + ob * (double)M * N * (accumulate ? 2 : 1);
+  if (epi >= 3) b += ob * (double)M * N;
+  return b * batch;
+}
+
 namespace big {
 constexpr int BM = 256, BK = 64, NW = 8, NT = NW * 64;
 constexpr int ROW_BYTES = BK * 2;  // 128
@@ -700,6 +711,8 @@ static int launch_big(const Args& g, int batch, int wnb, hipStream_t st) {
   else
     hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 2>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
   prof_end("gemm_bf16", st, 2.0 * g.M * g.N * g.K * batch);
+  prof_work("gemm_bf16_bytes", gemm_alg_bytes(sizeof(TO) == 4, EPI, g.accumulate, g.M, g.N, g.K,
+                                               batch));
   return check_launch("gemm_big_kernel");
 }
 
@@ -725,6 +738,9 @@ static int launch(const Args& g0, int batch, int splits, hipStream_t st) {
                        g.alpha, g.accumulate, EPI == EPI_BIAS ? g.bias : nullptr, g.sBias);
   }
   prof_end(sizeof(TI) == 2 ? "gemm_bf16" : "gemm_f32", st, 2.0 * g.M * g.N * g.K * batch);
+  if (sizeof(TI) == 2)
+    prof_work("gemm_bf16_bytes", gemm_alg_bytes(sizeof(TO) == 4, EPI, g.accumulate, g.M, g.N, g.K,
+                                                 batch));
   return check_launch("gemm_kernel");
 }
 
@@ -836,6 +852,8 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
                            nb, alpha, accumulate);
       }
       prof_end("gemm_bf16", st, 2.0 * M * N * K * batch);
+      prof_work("gemm_bf16_bytes",
+                gemm::gemm_alg_bytes(out_dtype, epilogue, accumulate, M, N, K, batch));
       return check_launch("gemm_pp_kernel");
     }
   }

@@ -32,6 +32,10 @@
 //    or raw fp32 split-K slabs reduced afterwards in a fixed order.
 #include "gemm_pp.h"
 
+#include <atomic>
+#include <cstdlib>
+#include <mutex>
+
 namespace irc {
 namespace gemm {
 // shared with gemm.hip
@@ -207,67 +211,51 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int row0, int s, int lan
 // fragments take the same bytes of the row, so the k order is consistent.
 typedef int v8i32 __attribute__((ext_vector_type(8)));
 
-template <bool AK, bool BK_, typename TO, int EPI, bool F8 = false>
-__global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
-  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
-  const int tiles_m = (g.M + BM - 1) / BM;
-  const int tiles_n = (g.N + BN - 1) / BN;
-  const int ntiles = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {  // XCD-aware bijective remap: blocks sharing an XCD walk consecutive tiles
-    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-  }
-  // EPI_SCAN: query tiles fastest, so the blocks of one doc tile run back to back
-  // on one XCD and read it from that XCD's L2 (C4: 2048 queries = 8 query tiles)
-  const int tm = EPI == EPI_SCAN ? bid % tiles_m : bid / tiles_n;
-  const int tn = EPI == EPI_SCAN ? bid / tiles_m : bid % tiles_n;
-  const int batch = blockIdx.y;
-  const int kbeg = blockIdx.z * g.kchunk;
-  const int kend = min(g.K, kbeg + g.kchunk);
-  const int nk = (kend - kbeg) / BK;
-  const unsigned short* A = g.A + batch * g.sA;
-  const unsigned short* B = g.B + batch * g.sB;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = wave >> 2, wq = wave & 3;  // group = row half; wq = wave within group
-  const int wn = wq;                          // 64-column slab of the tile
+// One 64-deep K-tile of both operands into the LDS image at `base`: group g stages
+// A rows/cols [128g, +128) and B rows/cols [128g, +128).
+template <bool AK, bool BK_>
+__device__ __forceinline__ void stage_tile(const PArgs& g, const unsigned short* A,
+                                           const unsigned short* B, int m0, int n0, int k0,
+                                           char* base, int grp, int wq, int lane) {
+  constexpr int SA = slot_bytes(AK), SB = slot_bytes(BK_);
+  stage_half<AK>(A, g.lda, m0 + 128 * grp, g.M, k0, base + grp * SA, wq, lane);
+  stage_half<BK_>(B, g.ldb, n0 + 128 * grp, g.N, k0, base + 2 * SA + grp * SB, wq, lane);
+}
+
+// The ping-pong K loop of one 256x256 output tile over nk K-tiles from kbeg.
+// K-tile kt lives in LDS buffer (kt + par) & 1, the buffers `pitch` bytes apart.
+// staged: K-tile 0's DMA was already issued by the caller.  pub != null: thread 0
+// stores pub_val there before its last barrier, so every wave reads it after the
+// loop.  On return every wave of the CALLER's group is past its last MFMA and every
+// wave of both groups past its last fragment read; group 1 may still be in its last
+// MFMAs when group 0 returns (registers only: LDS is free for the epilogue).
+template <bool AK, bool BK_, bool F8>
+__device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A,
+                                         const unsigned short* B, int m0, int n0, int kbeg,
+                                         int nk, char* lds, int pitch, int par, bool staged,
+                                         f32x4 (&acc)[8][4], int grp, int wq, int lane, int* pub,
+                                         int pub_val) {
+  constexpr int SA = slot_bytes(AK), SB = slot_bytes(BK_);
+  const int wn = wq;  // 64-column slab of the tile
   const int bh = wn >> 1, bcol = 64 * (wn & 1);
-
-  // group g stages A rows/cols [128g, +128) and B rows/cols [128g, +128)
-  constexpr int SA = slot_bytes(AK), SB = slot_bytes(BK_), BUF = buf_bytes(AK, BK_);
-  auto stage = [&](int kt, int buf) {
-    char* base = lds + buf * BUF;
-    const int k0 = kbeg + kt * BK;
-    if constexpr (AK)
-      stage_half<true>(A, g.lda, m0 + 128 * grp, g.M, k0, base + grp * SA, wq, lane);
-    else
-      stage_half<false>(A, g.lda, m0 + 128 * grp, g.M, k0, base + grp * SA, wq, lane);
-    if constexpr (BK_)
-      stage_half<true>(B, g.ldb, n0 + 128 * grp, g.N, k0, base + 2 * SA + grp * SB, wq, lane);
-    else
-      stage_half<false>(B, g.ldb, n0 + 128 * grp, g.N, k0, base + 2 * SA + grp * SB, wq, lane);
-  };
-
-  if (EPI == EPI_SCAN) PSTAMP(0);
-  f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4)0.0f;
 
   if (nk > 0) {
-    stage(0, 0);
+    if (!staged) stage_tile<AK, BK_>(g, A, B, m0, n0, kbeg, lds + par * pitch, grp, wq, lane);
     wait_vmcnt<0>();
     wg_barrier();
     if (grp == 1) wg_barrier();  // group 1 runs one section behind
     for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
+      const int cur = (kt + par) & 1;
       // ---- L section: next tile's DMA, this tile's fragments
-      if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-      const char* la = lds + cur * BUF + grp * SA;
-      const char* lb = lds + cur * BUF + 2 * SA + bh * SB;
+      if (kt + 1 < nk)
+        stage_tile<AK, BK_>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch, grp,
+                            wq, lane);
+      const char* la = lds + cur * pitch + grp * SA;
+      const char* lb = lds + cur * pitch + 2 * SA + bh * SB;
       bf16x8 fa[8][2], fb[4][2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -303,107 +291,38 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
                                                                   0, 0, 0);
       }
       __builtin_amdgcn_s_setprio(0);
-      if (grp == 0) wait_vmcnt<0>();
+      if (grp == 0) {
+        wait_vmcnt<0>();
+        if (kt == nk - 1 && pub != nullptr && threadIdx.x == 0) {
+          *pub = pub_val;
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        }
+      }
+      // Group 1's last M section ends without a barrier, and group 0 does not wait
+      // for it after the loop: group 0's last barrier above already follows group
+      // 1's last fragment reads, so group 0 starts its epilogue while group 1's last
+      // 64 MFMAs run (one barrier fewer for each group keeps the counts matched).
+#ifdef IRC_PP_LAST_BARRIER  // A/B build: both groups meet after the last M section
       wg_barrier();
     }
     if (grp == 0) wg_barrier();
+#else
+      if (!(grp == 1 && kt == nk - 1)) wg_barrier();
+    }
+#endif
   }
+}
 
-  // ---------------------------------------------------------------- epilogue
-  // acc[i][j] element e -> row 128 grp + 16 i + 4 (lane >> 4) + e, col 64 wn + 16 j + (lane & 15)
+// Vectorised epilogue of one 256x256 tile (16-byte aligned C / R rows, or raw fp32
+// split-K slabs): per wave, four 32-row passes through its LDS staging rows (the
+// first 8 * 32 * EP_PITCH floats of LDS), fused bias / GELU / GELU' / residual /
+// pre-activation save / fp32 accumulate, then coalesced 16-byte stores.
+template <typename TO, int EPI, bool F8>
+__device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[8][4], char* lds,
+                                             int m0, int n0, int batch, int grp, int wn, int wave,
+                                             int lane) {
   const int rbase0 = m0 + 128 * grp;
   const int cbase = n0 + 64 * wn;
-  if constexpr (EPI == EPI_SCAN) {
-    // rows = queries, cols = docs.  LDS is free (every wave is past its last
-    // fragment read): per-query survivor counters + thresholds (key and its float
-    // prefilter: key >= thr implies score >= float(thr >> 32) for non-NaN scores).
-    PSTAMP(1);
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
-    uint64_t* thk = reinterpret_cast<uint64_t*>(lds + 1024);
-    float* thf = reinterpret_cast<float*>(lds + 3072);
-    if (threadIdx.x < 256) {
-      const int q = m0 + threadIdx.x;
-      const uint64_t t = (g.thr != nullptr && q < g.M) ? g.thr[q] : 0ull;
-      cnt[threadIdx.x] = 0;
-      thk[threadIdx.x] = t;
-      const uint32_t hi = (uint32_t)(t >> 32);
-      // padded query rows never pass; no threshold (hi == 0) admits everything
-#ifdef IRC_PP_SCAN_NOPASS  // diagnostic build: nothing passes
-      thf[threadIdx.x] = __builtin_huge_valf();
-      if (true) {} else
-#endif
-      thf[threadIdx.x] = q >= g.M ? __builtin_huge_valf()
-                                  : (hi == 0 ? -__builtin_huge_valf() : unorderable_f32(hi));
-    }
-    __syncthreads();
-#ifdef IRC_PP_SCAN_NOEPI  // diagnostic build: main loop + counters only
-    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
-      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = acc[0][0][0] == 12345.f ? 1u : 0u;
-    return;
-#endif
-    // Pass test of the lane's 128 scores (bit 16 i + 4 j + e) as a branch-free
-    // mask; then per half (i < 4, i >= 4) the lane's 64 accumulators are staged in
-    // its private LDS slot (16 x 16-byte writes, unconditional) and only the set
-    // bits (a few per lane: the threshold admits ~16k of N per query) read their
-    // score back by a dynamic LDS index for the exact-key / slot / store path.
-    // The slot's 16-byte chunk c sits at position c ^ (lane & 15): lanes' slots are
-    // 256 B apart, so unswizzled every lane of a ds_write_b128 would hit the same
-    // 4 banks (16-way conflicts on the 2 x 16 staging writes).
-    float* slotv = reinterpret_cast<float*>(lds + 4096) + threadIdx.x * 64;
-    const int sw = lane & 15;
-    uint64_t pm[2] = {0, 0};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const f32x4 tf = *reinterpret_cast<const f32x4*>(&thf[128 * grp + 16 * i + 4 * (lane >> 4)]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int bit = 16 * i + 4 * j + e;
-          pm[bit >> 6] |= (uint64_t)(!(acc[i][j][e] < tf[e])) << (bit & 63);
-        }
-    }
-    PSTAMP(2);
-#ifdef IRC_PP_SCAN_MASKONLY  // diagnostic build: mask, no exact path
-    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
-      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = __popcll(pm[0] | pm[1]) == 999 ? 1u : 0u;
-    return;
-#endif
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      if (__ballot(pm[hh] != 0) == 0) continue;  // wave-uniform
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          *reinterpret_cast<f32x4*>(slotv + 4 * ((4 * i + j) ^ sw)) = acc[4 * hh + i][j];
-      uint64_t bits = pm[hh];
-      while (__ballot(bits != 0) != 0) {
-        if (bits != 0) {
-          const int b = __builtin_ctzll(bits);
-          bits &= bits - 1;
-          const float v = slotv[4 * ((b >> 2) ^ sw) + (b & 3)];
-          const int bit = 64 * hh + b;
-          const int ql = 128 * grp + 16 * (bit >> 4) + 4 * (lane >> 4) + (bit & 3);
-          const int q = m0 + ql;
-          const int d = cbase + 16 * ((bit >> 2) & 3) + (lane & 15);
-          if (q < g.M && d < g.N) {
-            const uint64_t key = make_key(v, g.idx_base + (uint32_t)d * (uint32_t)g.stride);
-            if (key >= thk[ql]) {
-              const uint32_t slot = atomicAdd(&cnt[ql], 1u);
-              g.keys[((int64_t)tn * g.qpad + q) * g.cap + slot] = key;
-            }
-          }
-        }
-      }
-    }
-    PSTAMP(3);
-    __syncthreads();
-    PSTAMP(4);
-    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
-      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = cnt[threadIdx.x];
-    return;
-  }
   float* st = reinterpret_cast<float*>(lds) + wave * (32 * EP_PITCH);
   const bool slab = g.P != nullptr;
   if (slab || g.vec_c) {
@@ -549,6 +468,139 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
     }
     return;
   }
+}
+
+template <bool AK, bool BK_, typename TO, int EPI, bool F8 = false>
+__global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
+  const int tiles_m = (g.M + BM - 1) / BM;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {  // XCD-aware bijective remap: blocks sharing an XCD walk consecutive tiles
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  // EPI_SCAN: query tiles fastest, so the blocks of one doc tile run back to back
+  // on one XCD and read it from that XCD's L2 (C4: 2048 queries = 8 query tiles)
+  const int tm = EPI == EPI_SCAN ? bid % tiles_m : bid / tiles_n;
+  const int tn = EPI == EPI_SCAN ? bid / tiles_m : bid % tiles_n;
+  const int batch = blockIdx.y;
+  const int kbeg = blockIdx.z * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const int nk = (kend - kbeg) / BK;
+  const unsigned short* A = g.A + batch * g.sA;
+  const unsigned short* B = g.B + batch * g.sB;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wave >> 2, wq = wave & 3;  // group = row half; wq = wave within group
+  const int wn = wq;                          // 64-column slab of the tile
+
+  if (EPI == EPI_SCAN) PSTAMP(0);
+  f32x4 acc[8][4];
+  mainloop<AK, BK_, F8>(g, A, B, m0, n0, kbeg, nk, lds, buf_bytes(AK, BK_), 0, false, acc, grp,
+                        wq, lane, nullptr, 0);
+
+  // ---------------------------------------------------------------- epilogue
+  // acc[i][j] element e -> row 128 grp + 16 i + 4 (lane >> 4) + e, col 64 wn + 16 j + (lane & 15)
+  const int rbase0 = m0 + 128 * grp;
+  const int cbase = n0 + 64 * wn;
+  if constexpr (EPI == EPI_SCAN) {
+    // rows = queries, cols = docs.  LDS is free (every wave is past its last
+    // fragment read): per-query survivor counters + thresholds (key and its float
+    // prefilter: key >= thr implies score >= float(thr >> 32) for non-NaN scores).
+    PSTAMP(1);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
+    uint64_t* thk = reinterpret_cast<uint64_t*>(lds + 1024);
+    float* thf = reinterpret_cast<float*>(lds + 3072);
+    if (threadIdx.x < 256) {
+      const int q = m0 + threadIdx.x;
+      const uint64_t t = (g.thr != nullptr && q < g.M) ? g.thr[q] : 0ull;
+      cnt[threadIdx.x] = 0;
+      thk[threadIdx.x] = t;
+      const uint32_t hi = (uint32_t)(t >> 32);
+      // padded query rows never pass; no threshold (hi == 0) admits everything
+#ifdef IRC_PP_SCAN_NOPASS  // diagnostic build: nothing passes
+      thf[threadIdx.x] = __builtin_huge_valf();
+      if (true) {} else
+#endif
+      thf[threadIdx.x] = q >= g.M ? __builtin_huge_valf()
+                                  : (hi == 0 ? -__builtin_huge_valf() : unorderable_f32(hi));
+    }
+    __syncthreads();
+#ifdef IRC_PP_SCAN_NOEPI  // diagnostic build: main loop + counters only
+    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
+      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = acc[0][0][0] == 12345.f ? 1u : 0u;
+    return;
+#endif
+    // Pass test of the lane's 128 scores (bit 16 i + 4 j + e) as a branch-free
+    // mask; then per half (i < 4, i >= 4) the lane's 64 accumulators are staged in
+    // its private LDS slot (16 x 16-byte writes, unconditional) and only the set
+    // bits (a few per lane: the threshold admits ~16k of N per query) read their
+    // score back by a dynamic LDS index for the exact-key / slot / store path.
+    // The slot's 16-byte chunk c sits at position c ^ (lane & 15): lanes' slots are
+    // 256 B apart, so unswizzled every lane of a ds_write_b128 would hit the same
+    // 4 banks (16-way conflicts on the 2 x 16 staging writes).
+    float* slotv = reinterpret_cast<float*>(lds + 4096) + threadIdx.x * 64;
+    const int sw = lane & 15;
+    uint64_t pm[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 tf = *reinterpret_cast<const f32x4*>(&thf[128 * grp + 16 * i + 4 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int bit = 16 * i + 4 * j + e;
+          pm[bit >> 6] |= (uint64_t)(!(acc[i][j][e] < tf[e])) << (bit & 63);
+        }
+    }
+    PSTAMP(2);
+#ifdef IRC_PP_SCAN_MASKONLY  // diagnostic build: mask, no exact path
+    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
+      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = __popcll(pm[0] | pm[1]) == 999 ? 1u : 0u;
+    return;
+#endif
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      if (__ballot(pm[hh] != 0) == 0) continue;  // wave-uniform
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4*>(slotv + 4 * ((4 * i + j) ^ sw)) = acc[4 * hh + i][j];
+      uint64_t bits = pm[hh];
+      while (__ballot(bits != 0) != 0) {
+        if (bits != 0) {
+          const int b = __builtin_ctzll(bits);
+          bits &= bits - 1;
+          const float v = slotv[4 * ((b >> 2) ^ sw) + (b & 3)];
+          const int bit = 64 * hh + b;
+          const int ql = 128 * grp + 16 * (bit >> 4) + 4 * (lane >> 4) + (bit & 3);
+          const int q = m0 + ql;
+          const int d = cbase + 16 * ((bit >> 2) & 3) + (lane & 15);
+          if (q < g.M && d < g.N) {
+            const uint64_t key = make_key(v, g.idx_base + (uint32_t)d * (uint32_t)g.stride);
+            if (key >= thk[ql]) {
+              const uint32_t slot = atomicAdd(&cnt[ql], 1u);
+              g.keys[((int64_t)tn * g.qpad + q) * g.cap + slot] = key;
+            }
+          }
+        }
+      }
+    }
+    PSTAMP(3);
+    __syncthreads();
+    PSTAMP(4);
+    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
+      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = cnt[threadIdx.x];
+    return;
+  }
+  if (g.P != nullptr || g.vec_c) {
+    epilogue_vec<TO, EPI, F8>(g, acc, lds, m0, n0, batch, grp, wn, wave, lane);
+    return;
+  }
   // scalar epilogue (unaligned C / R)
   const float* bias = g.bias ? g.bias + batch * g.sBias : nullptr;
   const TO* R = reinterpret_cast<const TO*>(g.R) + (g.R ? batch * g.sR : 0);
@@ -592,6 +644,78 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
             *reinterpret_cast<float*>(dst) = v;
         }
       }
+  }
+}
+
+// Persistent form of the same tile (batch 1, no split-K, vectorised epilogue), for
+// launches of more tiles than CUs.  Each workgroup runs tiles until none is left:
+// its first tile by the XCD-aware map of blockIdx over the first G tiles, every
+// later one fetched from a per-launch tile counter (dynamic, so workgroups that
+// start late -- CUs held by kernels of other streams, e.g. the heads' cluster
+// recurrences beside the BERT prefetch -- take fewer tiles instead of stretching the
+// launch).  Between two tiles, the next tile's first K-tile is DMA'd into LDS
+// buffer 1 while this tile's epilogue stages through buffer 0 (buffers PBUF apart,
+// PBUF = the 8 waves' staging rows), and the counter fetch for the tile after
+// that is in flight meanwhile, so neither the prologue DMA nor the fetch is exposed.
+// ctr[0] = tiles handed out past G, ctr[1] = finished workgroups; the last one to
+// finish zeroes both for the next launch that uses this counter slot.
+constexpr int PBUF = 8 * 32 * EP_PITCH * 4;  // 69,632 B
+static_assert(PBUF >= buf_bytes(false, false) && 2 * PBUF <= LDS_BYTES, "persistent LDS plan");
+
+template <bool AK, bool BK_, typename TO, int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_pp_pers_kernel(PArgs g, uint32_t* ctr, int mode) {
+  // mode 1: dynamic tiles + prestage; 2: static waves of G tiles + prestage;
+  // 3: static, no prestage (A/B of what each part buys)
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
+  __shared__ int s_next;
+  const int tiles_n = (g.N + BN - 1) / BN;
+  const int ntiles = ((g.M + BM - 1) / BM) * tiles_n;
+  const int G = gridDim.x;  // <= ntiles
+  int slot;
+  {
+    const int q = G / 8, r = G % 8, x = blockIdx.x % 8;
+    slot = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
+  }
+  int tile = slot;
+  const bool dyn = mode == 1, pre = mode != 3;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = wave >> 2, wq = wave & 3;
+  const int nk = g.K / BK;
+  int pending = G + slot;  // the tile after the next one (thread 0 when dynamic)
+  if (dyn && threadIdx.x == 0) pending = G + (int)atomicAdd(ctr, 1u);
+  if (pre)
+    stage_tile<AK, BK_>(g, g.A, g.B, (tile / tiles_n) * BM, (tile % tiles_n) * BN, 0, lds + PBUF,
+                        grp, wq, lane);
+  f32x4 acc[8][4];
+  while (true) {
+    // a lane index the compiler must re-derive per tile: otherwise it hoists the
+    // epilogue's and the DMA's per-lane addresses out of this loop, keeps them live
+    // through the K loop and spills
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
+    mainloop<AK, BK_, false>(g, g.A, g.B, m0, n0, 0, nk, lds, PBUF, 1, pre, acc, grp, wq, ln,
+                             dyn ? &s_next : nullptr, pending);
+    int next;
+    if (dyn) {
+      // published before the loop's last barrier (uniform: keep it in an SGPR)
+      next = __builtin_amdgcn_readfirstlane(s_next);
+      if (next < ntiles && threadIdx.x == 0) pending = G + (int)atomicAdd(ctr, 1u);
+    } else {
+      next = tile + G;
+    }
+    if (pre && next < ntiles)
+      stage_tile<AK, BK_>(g, g.A, g.B, (next / tiles_n) * BM, (next % tiles_n) * BN, 0,
+                          lds + PBUF, grp, wq, ln);
+    epilogue_vec<TO, EPI, false>(g, acc, lds, m0, n0, 0, grp, wq, wave, ln);
+    if (next >= ntiles) break;
+    tile = next;
+    if (!pre) wg_barrier();  // every wave's epilogue is done with buffer 0
+  }
+  if (dyn && threadIdx.x == 0 && atomicAdd(ctr + 1, 1u) == (uint32_t)G - 1) {
+    atomicExch(ctr, 0u);
+    atomicExch(ctr + 1, 0u);
   }
 }
 
@@ -709,9 +833,86 @@ bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, i
   return tiles * batch * splits >= 32;
 }
 
+// IRC_GEMM_PERSIST=0 turns the persistent form off (A/B experiments; read on first
+// use); irc_gemm_set_persistent switches it at run time (the tests compare both forms).
+static std::atomic<int>& pers_mode() {
+  static std::atomic<int> on{[] {
+    const char* e = getenv("IRC_GEMM_PERSIST");
+    return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
+  }()};
+  return on;
+}
+static bool pers_enabled() { return pers_mode().load(std::memory_order_relaxed) != 0; }
+
+static int cu_count() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = -1;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// Tile-counter slots of the persistent launches, one 64-byte slot per launch in
+// rotation (so launches on concurrent streams never share one); zeroed once, and
+// each launch leaves its slot zeroed again.
+constexpr int PERS_SLOTS = 1024;
+static uint32_t* pers_counter() {
+  static std::mutex mu;
+  static uint32_t* base[64] = {};
+  static std::atomic<uint32_t> next{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (base[dev] == nullptr) {
+      void* p = nullptr;
+      if (hipMalloc(&p, PERS_SLOTS * 64) != hipSuccess) return nullptr;
+      if (hipMemset(p, 0, PERS_SLOTS * 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+      }
+      base[dev] = static_cast<uint32_t*>(p);
+    }
+  }
+  return base[dev] + (next.fetch_add(1) % PERS_SLOTS) * 16;
+}
+
+template <bool AK, bool BKM, typename TO>
+static void launch_pers(int epi, const PArgs& a, unsigned grid, uint32_t* ctr, hipStream_t st) {
+  const int mode = pers_mode().load(std::memory_order_relaxed);
+  switch (epi) {
+#define IRC_PPP(E)                                                                       \
+  case E:                                                                                \
+    hipLaunchKernelGGL((gemm_pp_pers_kernel<AK, BKM, TO, E>), dim3(grid), dim3(NT), 0, st, a, \
+                       ctr, mode);                                                           \
+    break;
+    IRC_PPP(0) IRC_PPP(1) IRC_PPP(2) IRC_PPP(3) IRC_PPP(4) IRC_PPP(5) IRC_PPP(6)
+#undef IRC_PPP
+  }
+}
+
 void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, int splits,
          hipStream_t st) {
   const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
+  // persistent form: one launch-wide pass over more tiles than CUs, A K-major
+  if (splits == 1 && batch == 1 && a.vec_c && la == 0 && pers_enabled()) {
+    const int ncu = cu_count();
+    uint32_t* ctr = (ncu > 0 && tiles > ncu) ? pers_counter() : nullptr;
+    if (ctr != nullptr) {
+      if (out_f32) {
+        if (lb == 0) launch_pers<true, true, float>(epi, a, (unsigned)ncu, ctr, st);
+        else launch_pers<true, false, float>(epi, a, (unsigned)ncu, ctr, st);
+      } else {
+        if (lb == 0) launch_pers<true, true, unsigned short>(epi, a, (unsigned)ncu, ctr, st);
+        else launch_pers<true, false, unsigned short>(epi, a, (unsigned)ncu, ctr, st);
+      }
+      return;
+    }
+  }
   const dim3 grid((unsigned)tiles, (unsigned)batch, (unsigned)splits);
   if (splits > 1)  // raw fp32 slabs, no epilogue (reduced afterwards)
     launch_layout<float>(la, lb, 0, a, grid, st);
@@ -723,3 +924,8 @@ void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, in
 
 }  // namespace gpp
 }  // namespace irc
+
+// Persistent tile loop mode of the 256x256 GEMM (0 off, 1-3 see irc.h); returns the previous one.
+extern "C" int irc_gemm_set_persistent(int mode) {
+  return irc::gpp::pers_mode().exchange(mode < 0 ? 0 : mode > 3 ? 1 : mode);
+}

@@ -32,6 +32,7 @@ int check_launch(const char* what);
 bool prof_on();
 void prof_begin(hipStream_t st);
 void prof_end(const char* name, hipStream_t st, double work = 0.0);
+void prof_work(const char* name, double work);
 
 static inline hipStream_t as_stream(irc_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -72,6 +72,16 @@ void prof_end(const char* name, hipStream_t st, double work) {
   g_open_ev = nullptr;
 }
 
+// A work tally without timing (count += 1, work += work), e.g. the algorithmic
+// bytes of the launches a timed record of another name covers.
+void prof_work(const char* name, double work) {
+  if (!g_prof) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  ProfRec& r = g_prof_tab[name];
+  r.count += 1;
+  r.work += work;
+}
+
 }  // namespace irc
 
 extern "C" int irc_prof_enable(int on) {

@@ -25,6 +25,14 @@ def _code(t: torch.Tensor) -> int:
         raise TypeError(f"irc kernels take bf16 or fp32, got {t.dtype}") from None
 
 
+def gemm_set_persistent(mode) -> int:
+    """Persistent tile loop of the 256x256 bf16 GEMM (irc_gemm_set_persistent): 0 off
+    (the default), 1 / True dynamic tiles with the next tile's first K-tile prestaged
+    during the epilogue, 2 static waves + prestage, 3 static.  Returns the previous
+    mode.  Results are bit-identical in every mode."""
+    return int(_lib.load().irc_gemm_set_persistent(int(mode)))
+
+
 def gemm(a, b, *, trans_a=False, b_is_nk=True, bias=None, epilogue=EPI_NONE, residual=None,
          alpha=1.0, out=None, out_dtype=None, accumulate=False):
     """out[M, N] = alpha * op(a) @ op(b) (+ bias) (-> gelu) (+ residual).

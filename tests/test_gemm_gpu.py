@@ -249,3 +249,86 @@ def test_pp_splitk_accumulate(gpu, M, N, K, batch):
     ref = base.cpu() + torch.einsum("bkm,bkn->bmn", a.float().cpu(), b.float().cpu())
     err = (outs[0].cpu() - ref).abs().max().item()
     assert err <= 1e-3 * ref.abs().max().item()
+
+
+# ---- persistent form of the 256x256 path: launches of more tiles than CUs
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("odt", [torch.bfloat16, torch.float32])
+def test_pp_persistent_bitwise(gpu, epi, odt):
+    """17 x 17 = 289 ragged output tiles (> 256 CUs): the persistent tile loop
+    (dynamic tile counter, next tile's first K-tile DMA'd during the epilogue) gives
+    the same bits as one workgroup per tile, for every epilogue, and matches the
+    fp32 reference within the bf16 tolerance of test_pp_epilogues."""
+    from irc_amd import ops
+
+    M, N, K = 4100, 4200, 192
+    g = torch.Generator().manual_seed(300 + epi)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    b = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g) if epi in (1, 2, 3, 6) else None
+    res = torch.randn(M, N, generator=g).to(odt) if epi in (3, 4, 5, 6) else None
+    outs = []
+    prev = ops.gemm_set_persistent(True)
+    try:
+        # modes: 1 dynamic tiles (twice: the tile counter resets), 0 one workgroup per
+        # tile, 2 static waves + prestage, 3 static without prestage
+        for pers in (1, 0, 1, 2, 3):
+            ops.gemm_set_persistent(pers)
+            r = None if res is None else res.to(gpu)
+            out = ops.gemm(a.to(gpu), b.to(gpu), bias=None if bias is None else bias.to(gpu),
+                           epilogue=epi, residual=r, out_dtype=odt, alpha=0.5)
+            torch.cuda.synchronize()
+            outs.append((out.cpu(), None if r is None else r.cpu()))
+    finally:
+        ops.gemm_set_persistent(prev)
+    for o, r in outs[1:]:
+        assert torch.equal(o, outs[0][0])
+        if epi == 6:  # pre-activation written to R
+            assert torch.equal(r, outs[0][1])
+    y = 0.5 * (a.float() @ b.float().T)
+    if bias is not None:
+        y = y + bias
+    if epi in (2, 6):
+        ref = torch.nn.functional.gelu(y)
+    elif epi in (3, 4):
+        ref = y + res.float()
+    elif epi == 5:
+        ur = res.float().requires_grad_(True)
+        torch.nn.functional.gelu(ur).backward(y)
+        ref = ur.grad
+    else:
+        ref = y
+    tol = 1e-2 if odt == torch.bfloat16 else 1e-3
+    assert (outs[0][0].float() - ref).abs().max().item() <= tol * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("b_is_nk", [True, False])
+def test_pp_persistent_bert_shapes(gpu, b_is_nk):
+    """The BERT-base layer shapes at C2 (M = 32768 rows) through the persistent form,
+    B K-major (forward) and K-outer (the trainable encoder's dX): bit-identical to one
+    workgroup per tile, several launches back to back on two streams (distinct tile
+    counter slots)."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(11)
+    M, N, K = 32768, 3072, 768
+    a = torch.randn(M, K, generator=g).bfloat16().to(gpu)
+    b = (torch.randn(N, K, generator=g) if b_is_nk else torch.randn(K, N, generator=g))
+    b = b.bfloat16().to(gpu)
+    bias = torch.randn(N, generator=g).to(gpu)
+    prev = ops.gemm_set_persistent(False)
+    try:
+        ref = ops.gemm(a, b, b_is_nk=b_is_nk, bias=bias, epilogue=2)
+        torch.cuda.synchronize()
+        ops.gemm_set_persistent(True)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        outs = []
+        for st in (s1, s2, s1, s2):
+            st.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(st):
+                outs.append(ops.gemm(a, b, b_is_nk=b_is_nk, bias=bias, epilogue=2))
+        torch.cuda.synchronize()
+    finally:
+        ops.gemm_set_persistent(prev)
+    for o in outs:
+        assert torch.equal(o, ref)
