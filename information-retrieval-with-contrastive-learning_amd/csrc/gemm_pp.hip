@@ -470,6 +470,108 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
   }
 }
 
+// Threshold epilogue of the scan filter (EPI_SCAN) for one 256-query x 256-doc
+// tile: rows = queries, cols = docs.  Needs LDS [0, 4096 + 512 * 128) = [0, PBUF)
+// only, so a persistent caller can DMA into buffer 1 meanwhile; `after_init` runs
+// right after the first barrier (once the threshold loads are consumed, so the
+// compiler's waits for them do not also wait for DMA issued there).
+template <typename Fn>
+__device__ __forceinline__ void epilogue_scan(const PArgs& g, const f32x4 (&acc)[8][4], char* lds,
+                                              int m0, int n0, int tn, int grp, int wn, int lane,
+                                              Fn after_init) {
+  const int cbase = n0 + 64 * wn;
+  // per-query survivor counters + thresholds (key and its float prefilter: key >=
+  // thr implies score >= float(thr >> 32) for non-NaN scores).
+  PSTAMP(1);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
+  uint64_t* thk = reinterpret_cast<uint64_t*>(lds + 1024);
+  float* thf = reinterpret_cast<float*>(lds + 3072);
+  if (threadIdx.x < 256) {
+    const int q = m0 + threadIdx.x;
+    const uint64_t t = (g.thr != nullptr && q < g.M) ? g.thr[q] : 0ull;
+    cnt[threadIdx.x] = 0;
+    thk[threadIdx.x] = t;
+    const uint32_t hi = (uint32_t)(t >> 32);
+    // padded query rows never pass; no threshold (hi == 0) admits everything
+#ifdef IRC_PP_SCAN_NOPASS  // diagnostic build: nothing passes
+    thf[threadIdx.x] = __builtin_huge_valf();
+    if (true) {} else
+#endif
+    thf[threadIdx.x] = q >= g.M ? __builtin_huge_valf()
+                                : (hi == 0 ? -__builtin_huge_valf() : unorderable_f32(hi));
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  wg_barrier();
+  after_init();
+#ifdef IRC_PP_SCAN_NOEPI  // diagnostic build: main loop + counters only
+  if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
+    g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = acc[0][0][0] == 12345.f ? 1u : 0u;
+  return;
+#endif
+  // Pass test of the lane's 128 scores (bit 16 i + 4 j + e) as a branch-free
+  // mask; then per quarter (i = 2 qq, 2 qq + 1) the lane's 32 accumulators are
+  // staged in its private 128-B LDS slot (8 x 16-byte writes, unconditional) and
+  // only the set bits (a few per lane: the threshold admits ~16k of N per query)
+  // read their score back by a dynamic LDS index for the exact-key / slot / store
+  // path.  The slot's 16-byte chunk c sits at position c ^ ((lane >> 1) & 7): the
+  // 16 lanes of one ds_write_b128 group then cover all 64 banks (slots 128 B apart).
+  float* slotv = reinterpret_cast<float*>(lds + 4096) + threadIdx.x * 32;
+  const int sw = (lane >> 1) & 7;
+  uint64_t pm[2] = {0, 0};
+  const float* thq = thf + 128 * grp + 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f32x4 tf = *reinterpret_cast<const f32x4*>(&thq[16 * i]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int bit = 16 * i + 4 * j + e;
+        pm[bit >> 6] |= (uint64_t)(!(acc[i][j][e] < tf[e])) << (bit & 63);
+      }
+  }
+  PSTAMP(2);
+#ifdef IRC_PP_SCAN_MASKONLY  // diagnostic build: mask, no exact path
+  if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
+    g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = __popcll(pm[0] | pm[1]) == 999 ? 1u : 0u;
+  return;
+#endif
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    uint32_t bits = (uint32_t)(pm[qq >> 1] >> (32 * (qq & 1)));
+    if (__ballot(bits != 0) == 0) continue;  // wave-uniform
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<f32x4*>(slotv + 4 * ((4 * i + j) ^ sw)) = acc[2 * qq + i][j];
+    while (__ballot(bits != 0) != 0) {
+      if (bits != 0) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const float v = slotv[4 * ((b >> 2) ^ sw) + (b & 3)];
+        const int bit = 32 * qq + b;
+        const int ql = 128 * grp + 16 * (bit >> 4) + 4 * (lane >> 4) + (bit & 3);
+        const int q = m0 + ql;
+        const int d = cbase + 16 * ((bit >> 2) & 3) + (lane & 15);
+        if (q < g.M && d < g.N) {
+          const uint64_t key = make_key(v, g.idx_base + (uint32_t)d * (uint32_t)g.stride);
+          if (key >= thk[ql]) {
+            const uint32_t slot = atomicAdd(&cnt[ql], 1u);
+            g.keys[((int64_t)tn * g.qpad + q) * g.cap + slot] = key;
+          }
+        }
+      }
+    }
+  }
+  PSTAMP(3);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  wg_barrier();
+  PSTAMP(4);
+  if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
+    g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = cnt[threadIdx.x];
+}
+
 template <bool AK, bool BK_, typename TO, int EPI, bool F8 = false>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
@@ -507,94 +609,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   const int rbase0 = m0 + 128 * grp;
   const int cbase = n0 + 64 * wn;
   if constexpr (EPI == EPI_SCAN) {
-    // rows = queries, cols = docs.  LDS is free (every wave is past its last
-    // fragment read): per-query survivor counters + thresholds (key and its float
-    // prefilter: key >= thr implies score >= float(thr >> 32) for non-NaN scores).
-    PSTAMP(1);
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
-    uint64_t* thk = reinterpret_cast<uint64_t*>(lds + 1024);
-    float* thf = reinterpret_cast<float*>(lds + 3072);
-    if (threadIdx.x < 256) {
-      const int q = m0 + threadIdx.x;
-      const uint64_t t = (g.thr != nullptr && q < g.M) ? g.thr[q] : 0ull;
-      cnt[threadIdx.x] = 0;
-      thk[threadIdx.x] = t;
-      const uint32_t hi = (uint32_t)(t >> 32);
-      // padded query rows never pass; no threshold (hi == 0) admits everything
-#ifdef IRC_PP_SCAN_NOPASS  // diagnostic build: nothing passes
-      thf[threadIdx.x] = __builtin_huge_valf();
-      if (true) {} else
-#endif
-      thf[threadIdx.x] = q >= g.M ? __builtin_huge_valf()
-                                  : (hi == 0 ? -__builtin_huge_valf() : unorderable_f32(hi));
-    }
-    __syncthreads();
-#ifdef IRC_PP_SCAN_NOEPI  // diagnostic build: main loop + counters only
-    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
-      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = acc[0][0][0] == 12345.f ? 1u : 0u;
-    return;
-#endif
-    // Pass test of the lane's 128 scores (bit 16 i + 4 j + e) as a branch-free
-    // mask; then per half (i < 4, i >= 4) the lane's 64 accumulators are staged in
-    // its private LDS slot (16 x 16-byte writes, unconditional) and only the set
-    // bits (a few per lane: the threshold admits ~16k of N per query) read their
-    // score back by a dynamic LDS index for the exact-key / slot / store path.
-    // The slot's 16-byte chunk c sits at position c ^ (lane & 15): lanes' slots are
-    // 256 B apart, so unswizzled every lane of a ds_write_b128 would hit the same
-    // 4 banks (16-way conflicts on the 2 x 16 staging writes).
-    float* slotv = reinterpret_cast<float*>(lds + 4096) + threadIdx.x * 64;
-    const int sw = lane & 15;
-    uint64_t pm[2] = {0, 0};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const f32x4 tf = *reinterpret_cast<const f32x4*>(&thf[128 * grp + 16 * i + 4 * (lane >> 4)]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int bit = 16 * i + 4 * j + e;
-          pm[bit >> 6] |= (uint64_t)(!(acc[i][j][e] < tf[e])) << (bit & 63);
-        }
-    }
-    PSTAMP(2);
-#ifdef IRC_PP_SCAN_MASKONLY  // diagnostic build: mask, no exact path
-    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
-      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = __popcll(pm[0] | pm[1]) == 999 ? 1u : 0u;
-    return;
-#endif
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      if (__ballot(pm[hh] != 0) == 0) continue;  // wave-uniform
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          *reinterpret_cast<f32x4*>(slotv + 4 * ((4 * i + j) ^ sw)) = acc[4 * hh + i][j];
-      uint64_t bits = pm[hh];
-      while (__ballot(bits != 0) != 0) {
-        if (bits != 0) {
-          const int b = __builtin_ctzll(bits);
-          bits &= bits - 1;
-          const float v = slotv[4 * ((b >> 2) ^ sw) + (b & 3)];
-          const int bit = 64 * hh + b;
-          const int ql = 128 * grp + 16 * (bit >> 4) + 4 * (lane >> 4) + (bit & 3);
-          const int q = m0 + ql;
-          const int d = cbase + 16 * ((bit >> 2) & 3) + (lane & 15);
-          if (q < g.M && d < g.N) {
-            const uint64_t key = make_key(v, g.idx_base + (uint32_t)d * (uint32_t)g.stride);
-            if (key >= thk[ql]) {
-              const uint32_t slot = atomicAdd(&cnt[ql], 1u);
-              g.keys[((int64_t)tn * g.qpad + q) * g.cap + slot] = key;
-            }
-          }
-        }
-      }
-    }
-    PSTAMP(3);
-    __syncthreads();
-    PSTAMP(4);
-    if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
-      g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = cnt[threadIdx.x];
+    epilogue_scan(g, acc, lds, m0, n0, tn, grp, wn, lane, [] {});
     return;
   }
   if (g.P != nullptr || g.vec_c) {
@@ -662,14 +677,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
 constexpr int PBUF = 8 * 32 * EP_PITCH * 4;  // 69,632 B
 static_assert(PBUF >= buf_bytes(false, false) && 2 * PBUF <= LDS_BYTES, "persistent LDS plan");
 
-template <bool AK, bool BK_, typename TO, int EPI>
+template <bool AK, bool BK_, typename TO, int EPI, bool F8 = false>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_pers_kernel(PArgs g, uint32_t* ctr, int mode) {
   // mode 1: dynamic tiles + prestage; 2: static waves of G tiles + prestage;
   // 3: static, no prestage (A/B of what each part buys)
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
   __shared__ int s_next;
-  const int tiles_n = (g.N + BN - 1) / BN;
-  const int ntiles = ((g.M + BM - 1) / BM) * tiles_n;
+  const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  // tile -> (row tile, col tile) as gemm_pp_kernel: EPI_SCAN walks query tiles fastest
+  auto tile_m = [&](int t) { return EPI == EPI_SCAN ? t % tiles_m : t / tiles_n; };
+  auto tile_n = [&](int t) { return EPI == EPI_SCAN ? t / tiles_m : t % tiles_n; };
   const int G = gridDim.x;  // <= ntiles
   int slot;
   {
@@ -685,8 +703,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_pers_kernel(PArgs g, uint32_t* 
   int pending = G + slot;  // the tile after the next one (thread 0 when dynamic)
   if (dyn && threadIdx.x == 0) pending = G + (int)atomicAdd(ctr, 1u);
   if (pre)
-    stage_tile<AK, BK_>(g, g.A, g.B, (tile / tiles_n) * BM, (tile % tiles_n) * BN, 0, lds + PBUF,
-                        grp, wq, lane);
+    stage_tile<AK, BK_>(g, g.A, g.B, tile_m(tile) * BM, tile_n(tile) * BN, 0, lds + PBUF, grp, wq,
+                        lane);
   f32x4 acc[8][4];
   while (true) {
     // a lane index the compiler must re-derive per tile: otherwise it hoists the
@@ -694,9 +712,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_pers_kernel(PArgs g, uint32_t* 
     // through the K loop and spills
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
-    mainloop<AK, BK_, false>(g, g.A, g.B, m0, n0, 0, nk, lds, PBUF, 1, pre, acc, grp, wq, ln,
-                             dyn ? &s_next : nullptr, pending);
+    const int tn = tile_n(tile);
+    const int m0 = tile_m(tile) * BM, n0 = tn * BN;
+    mainloop<AK, BK_, F8>(g, g.A, g.B, m0, n0, 0, nk, lds, PBUF, 1, pre, acc, grp, wq, ln,
+                          dyn ? &s_next : nullptr, pending);
     int next;
     if (dyn) {
       // published before the loop's last barrier (uniform: keep it in an SGPR)
@@ -705,10 +724,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_pers_kernel(PArgs g, uint32_t* 
     } else {
       next = tile + G;
     }
-    if (pre && next < ntiles)
-      stage_tile<AK, BK_>(g, g.A, g.B, (next / tiles_n) * BM, (next % tiles_n) * BN, 0,
-                          lds + PBUF, grp, wq, ln);
-    epilogue_vec<TO, EPI, false>(g, acc, lds, m0, n0, 0, grp, wq, wave, ln);
+    auto prestage = [&] {
+      if (pre && next < ntiles)
+        stage_tile<AK, BK_>(g, g.A, g.B, tile_m(next) * BM, tile_n(next) * BN, 0, lds + PBUF, grp,
+                            wq, ln);
+    };
+    if constexpr (EPI == EPI_SCAN) {
+      epilogue_scan(g, acc, lds, m0, n0, tn, grp, wq, ln, prestage);
+    } else {
+      prestage();
+      epilogue_vec<TO, EPI, F8>(g, acc, lds, m0, n0, 0, grp, wq, wave, ln);
+    }
     if (next >= ntiles) break;
     tile = next;
     if (!pre) wg_barrier();  // every wave's epilogue is done with buffer 0
@@ -752,8 +778,70 @@ extern "C" int irc_pp_dbg_stamps(uint64_t* out /* [16] */) {
 #endif
 }
 
+// IRC_GEMM_PERSIST=0 turns the persistent form off (A/B experiments; read on first
+// use); irc_gemm_set_persistent switches it at run time (the tests compare both forms).
+static std::atomic<int>& pers_mode() {
+  static std::atomic<int> on{[] {
+    const char* e = getenv("IRC_GEMM_PERSIST");
+    return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
+  }()};
+  return on;
+}
+static bool pers_enabled() { return pers_mode().load(std::memory_order_relaxed) != 0; }
+
+static int cu_count() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = -1;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// Tile-counter slots of the persistent launches, one 64-byte slot per launch in
+// rotation (so launches on concurrent streams never share one); zeroed once, and
+// each launch leaves its slot zeroed again.
+constexpr int PERS_SLOTS = 1024;
+static uint32_t* pers_counter() {
+  static std::mutex mu;
+  static uint32_t* base[64] = {};
+  static std::atomic<uint32_t> next{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (base[dev] == nullptr) {
+      void* p = nullptr;
+      if (hipMalloc(&p, PERS_SLOTS * 64) != hipSuccess) return nullptr;
+      if (hipMemset(p, 0, PERS_SLOTS * 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+      }
+      base[dev] = static_cast<uint32_t*>(p);
+    }
+  }
+  return base[dev] + (next.fetch_add(1) % PERS_SLOTS) * 16;
+}
+
 void run_scan(const PArgs& a, hipStream_t st, bool fp8) {
   const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
+  if (pers_enabled()) {
+    const int ncu = cu_count();
+    uint32_t* ctr = (ncu > 0 && tiles > ncu) ? pers_counter() : nullptr;
+    if (ctr != nullptr) {
+      const int mode = pers_mode().load(std::memory_order_relaxed);
+      if (fp8)
+        hipLaunchKernelGGL((gemm_pp_pers_kernel<true, true, float, EPI_SCAN, true>), dim3(ncu),
+                           dim3(NT), 0, st, a, ctr, mode);
+      else
+        hipLaunchKernelGGL((gemm_pp_pers_kernel<true, true, float, EPI_SCAN>), dim3(ncu), dim3(NT),
+                           0, st, a, ctr, mode);
+      return;
+    }
+  }
   if (fp8)
     hipLaunchKernelGGL((gemm_pp_kernel<true, true, float, EPI_SCAN, true>), dim3((unsigned)tiles),
                        dim3(NT), 0, st, a);
@@ -831,54 +919,6 @@ bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, i
   if (lb == 1 && N % 8) return false;
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   return tiles * batch * splits >= 32;
-}
-
-// IRC_GEMM_PERSIST=0 turns the persistent form off (A/B experiments; read on first
-// use); irc_gemm_set_persistent switches it at run time (the tests compare both forms).
-static std::atomic<int>& pers_mode() {
-  static std::atomic<int> on{[] {
-    const char* e = getenv("IRC_GEMM_PERSIST");
-    return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
-  }()};
-  return on;
-}
-static bool pers_enabled() { return pers_mode().load(std::memory_order_relaxed) != 0; }
-
-static int cu_count() {
-  static int cus[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (cus[dev] == 0) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = -1;
-    cus[dev] = n;
-  }
-  return cus[dev];
-}
-
-// Tile-counter slots of the persistent launches, one 64-byte slot per launch in
-// rotation (so launches on concurrent streams never share one); zeroed once, and
-// each launch leaves its slot zeroed again.
-constexpr int PERS_SLOTS = 1024;
-static uint32_t* pers_counter() {
-  static std::mutex mu;
-  static uint32_t* base[64] = {};
-  static std::atomic<uint32_t> next{0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    if (base[dev] == nullptr) {
-      void* p = nullptr;
-      if (hipMalloc(&p, PERS_SLOTS * 64) != hipSuccess) return nullptr;
-      if (hipMemset(p, 0, PERS_SLOTS * 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-        (void)hipFree(p);
-        return nullptr;
-      }
-      base[dev] = static_cast<uint32_t*>(p);
-    }
-  }
-  return base[dev] + (next.fetch_add(1) % PERS_SLOTS) * 16;
 }
 
 template <bool AK, bool BKM, typename TO>
