@@ -111,6 +111,7 @@ struct Args {
   int vec_c;         // C (and R) rows 16-byte aligned and N % 8 == 0: vector epilogue
   int kchunk;        // split-K: K range of one blockIdx.z slice (multiple of BK)
   float* P;          // split-K partials [batch][split][M][N] (raw sums), or null
+  int group_m;       // big-tile kernel: grouped tile order (irc_common.h); 0 = row-major
 };
 
 // bf16 K-outer (COL / KN) slabs are kept k-major in LDS: [BK=32 k][128 rows]
@@ -497,7 +498,8 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
     const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  int tm, tn;
+  grouped_tile(bid, tiles_m, tiles_n, g.group_m, tm, tn);
   const int batch = blockIdx.y;
   const unsigned short* A = reinterpret_cast<const unsigned short*>(g.A) + batch * g.sA;
   const unsigned short* B = reinterpret_cast<const unsigned short*>(g.B) + batch * g.sB;
@@ -774,6 +776,16 @@ static int by_layout(int la, int lb, int epi, const Args& g, int batch, int spli
 
 using namespace irc;
 
+// IRC_GEMM_GROUP_M: grouped output-tile order of the 256-row GEMM kernels (rows per
+// group; 0 = row-major).  Read once.
+static int gemm_group_m() {
+  static const int gm = [] {
+    const char* e = getenv("IRC_GEMM_GROUP_M");
+    return e ? atoi(e) : 0;
+  }();
+  return gm;
+}
+
 // IRC_GEMM_PP=0 disables the ping-pong path (A/B experiments; read once).
 static bool pp_enabled() {
   static const bool on = [] {
@@ -829,7 +841,8 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
                                       ((uintptr_t)R % 16) == 0));
   gemm::Args g{A, B, C, bias, R, (int)M, (int)N, (int)K, lda, ldb, ldc, ldr,
                strideA, strideB, strideC, strideR, strideBias, alpha, accumulate, vec_a, vec_b,
-               vec_c, 0, splits > 1 ? static_cast<float*>(workspace) : nullptr};
+               vec_c, 0, splits > 1 ? static_cast<float*>(workspace) : nullptr,
+               gemm_group_m()};
   hipStream_t st = as_stream(stream);
   const int nb = (int)batch;
   if (in_dtype == 0 && pp_enabled()) {
@@ -843,6 +856,7 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
                     (int)K, sp > 1 ? (int)(((K + sp - 1) / sp + 63) / 64 * 64) : (int)K,
                     lda, ldb, ldc, ldr, strideA, strideB, strideC, strideR, strideBias, alpha,
                     accumulate, vec_c};
+      pa.group_m = gemm_group_m();
       prof_begin(st);
       gpp::run(out_dtype == 1, a_layout, b_layout, epilogue, pa, batch, sp, st);
       if (sp > 1) {

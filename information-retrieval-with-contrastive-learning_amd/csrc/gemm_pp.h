@@ -32,6 +32,8 @@ struct PArgs {
   // * sb[col] (+ bias ...): per-row dequantisation scales of both e4m3 operands
   const float* sa;
   const float* sb;
+  // grouped tile order (grouped_tile in irc_common.h); 0 / 1 = row-major
+  int group_m;
 };
 
 constexpr int EPI_SCAN = 7;

@@ -585,8 +585,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   }
   // EPI_SCAN: query tiles fastest, so the blocks of one doc tile run back to back
   // on one XCD and read it from that XCD's L2 (C4: 2048 queries = 8 query tiles)
-  const int tm = EPI == EPI_SCAN ? bid % tiles_m : bid / tiles_n;
-  const int tn = EPI == EPI_SCAN ? bid / tiles_m : bid % tiles_n;
+  int tm, tn;
+  if (EPI == EPI_SCAN) {
+    tm = bid % tiles_m;
+    tn = bid / tiles_m;
+  } else {
+    grouped_tile(bid, tiles_m, tiles_n, g.group_m, tm, tn);
+  }
   const int batch = blockIdx.y;
   const int kbeg = blockIdx.z * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
@@ -686,8 +691,16 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_pers_kernel(PArgs g, uint32_t* 
   const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
   // tile -> (row tile, col tile) as gemm_pp_kernel: EPI_SCAN walks query tiles fastest
-  auto tile_m = [&](int t) { return EPI == EPI_SCAN ? t % tiles_m : t / tiles_n; };
-  auto tile_n = [&](int t) { return EPI == EPI_SCAN ? t / tiles_m : t % tiles_n; };
+  auto tile_m = [&](int t) {
+    int tm, tn;
+    grouped_tile(t, tiles_m, tiles_n, g.group_m, tm, tn);
+    return EPI == EPI_SCAN ? t % tiles_m : tm;
+  };
+  auto tile_n = [&](int t) {
+    int tm, tn;
+    grouped_tile(t, tiles_m, tiles_n, g.group_m, tm, tn);
+    return EPI == EPI_SCAN ? t / tiles_m : tn;
+  };
   const int G = gridDim.x;  // <= ntiles
   int slot;
   {

@@ -102,6 +102,27 @@ __device__ __forceinline__ void wait_vmcnt_dyn(int ahead, int extra) {
 #undef IRC_VM_CASE
 }
 
+// Grouped output-tile order of the large GEMMs: runs of gm row tiles walk their
+// rows fastest, so the tiles one XCD has in flight share a few column tiles of B
+// (the weights, read by every row tile) that stay in its L2, instead of each row
+// block cycling through all of N.  gm <= 1: row-major (tm = t / tiles_n).  All
+// operands are wave-uniform (scalar arithmetic).
+__device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, int gm, int& tm,
+                                             int& tn) {
+  if (gm <= 1) {
+    tm = t / tiles_n;
+    tn = t % tiles_n;
+    return;
+  }
+  const int per = gm * tiles_n;
+  const int grp = t / per;
+  const int first = grp * gm;
+  const int rows = tiles_m - first < gm ? tiles_m - first : gm;
+  const int r = t - grp * per;
+  tm = first + r % rows;
+  tn = r / rows;
+}
+
 // Raw workgroup barrier that does NOT drain vmcnt (so LDS-DMA prefetches stay in
 // flight across it); the empty asm statements stop the compiler moving memory
 // operations across the barrier.
