@@ -19,9 +19,12 @@ def synthetic_vocab_file(vocab_size: int = 30522) -> str:
     path = os.path.join(tempfile.gettempdir(), f"irc_synthetic_vocab_{vocab_size}.txt")
     if not os.path.exists(path):
         toks = SPECIALS + [f"w{i}" for i in range(vocab_size - len(SPECIALS))]
-        with open(path + ".tmp", "w") as f:
+        # per-process temporary name: ranks started together each write their own
+        # copy and rename it into place atomically (the same content either way)
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
             f.write("\n".join(toks) + "\n")
-        os.replace(path + ".tmp", path)
+        os.replace(tmp, path)
     return path
 
 
