@@ -151,3 +151,27 @@ def test_gpu_wordpiece_training_batch(gpu, hf_tok):
         assert torch.equal(mask.cpu(), ref["attention_mask"])
     ids, mask = wp([])
     assert ids.shape[0] == 0
+
+
+def _vocab_worker(n):
+    from irc_amd.tokenizer import synthetic_vocab_file
+    return synthetic_vocab_file(n)
+
+
+def test_synthetic_vocab_file_concurrent_writers():
+    """Ranks that start together all create the synthetic vocab file: each writes its
+    own temporary copy and renames it into place, so none fails on a rename (the
+    2-rank DP test once did) and the file holds the full vocabulary."""
+    import multiprocessing as mp
+    import tempfile
+
+    n = 101
+    path = os.path.join(tempfile.gettempdir(), f"irc_synthetic_vocab_{n}.txt")
+    if os.path.exists(path):
+        os.remove(path)
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(4) as pool:
+        paths = pool.map(_vocab_worker, [n] * 16)
+    assert set(paths) == {path}
+    with open(path) as f:
+        assert len(f.read().split()) == n
