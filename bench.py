@@ -52,6 +52,9 @@ SCAN_N_PER_GPU, SCAN_Q, SCAN_D, SCAN_K = 100_000, 256, 768, 100
 # 2048 queries per batch; C4 is BERT-large (D = 1024, bf16), C5 fp8 (D = 768, e4m3)
 FP8_N_PER_GPU = 625_000
 C4_Q, C4_D, C5_Q = 2048, 1024, 2048
+# C3 retrieval leg: 1M docs over 4 GPUs = 250k x 768 bf16 per GPU (384 MB: larger
+# than the 256 MiB Infinity Cache, so its Q sweep is HBM-honest), 1024 queries
+C3_N_PER_GPU, C3_Q = 250_000, 1024
 PP_MIN_Q = 192  # irc_scan_topk's filter runs on the ping-pong GEMM kernel from this Q
 SCAN_DEPTH = 2  # query batches in flight in the retrieval legs (search_many)
 
@@ -142,6 +145,16 @@ def c2_config():
     return cfg
 
 
+def c4_config():
+    """Config C4's per-rank step: BERT-large frozen encoder (24 layers, H = 1024,
+    A = 16, I = 4096), so the BiLSTM head's input is 1024 wide; 256 pairs per rank
+    (global batch 2048 on 8 GPUs)."""
+    cfg = c2_config()
+    cfg["bert"] = dict(cfg.get("bert") or {}, name="bert-large-uncased")
+    cfg["model"]["LSTM"]["input_size"] = 1024
+    return cfg
+
+
 def _live_events(lib, name, fn, n):
     """The library's HIP-event timing of `name` over n more calls of fn.  Kept out of
     the timed regions: an event pair around every GEMM launch cost 5-8% of the C2
@@ -156,15 +169,16 @@ def _live_events(lib, name, fn, n):
     return _prof(lib, name)
 
 
-def run_train(args, rank, world, dev, weights="bf16"):
+def run_train(args, rank, world, dev, weights="bf16", cfg=None):
     """weights "fp8": config C5 -- the frozen encoder's nn.Linear layers on e4m3
-    (irc_gemm_fp8, per-channel weight / per-token input scales); same step."""
+    (irc_gemm_fp8, per-channel weight / per-token input scales); same step.
+    cfg: c2_config() (default) or c4_config() (BERT-large encoder)."""
     from irc_amd import _lib
     from src.model import build_model, get_optimizer
     from src.train import TrainState
 
     lib = _lib.load()
-    cfg = c2_config()
+    cfg = cfg or c2_config()
     ns = argparse.Namespace(config=cfg, loss="InfoNCE", model="LSTM", opt="adam",
                             sample="uniform")
     torch.manual_seed(1337)
@@ -469,6 +483,12 @@ def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16", nq=
         "query_doc_pairs_per_s": nq * n_per_gpu * world * reps / dt,
         "roofline": roof,
         "q_sweep_local": sweep,
+        "shard_bytes": n_per_gpu * dim * b,
+        "cache_resident": n_per_gpu * dim * b < 256 * 2**20 * 0.9,
+        "cache_note": ("the shard fits the 256 MiB Infinity Cache and is re-scanned batch after "
+                       "batch: its 'HBM' fractions are cache-assisted"
+                       if n_per_gpu * dim * b < 256 * 2**20 * 0.9 else
+                       "the shard exceeds the 256 MiB Infinity Cache: HBM-bound figures"),
     }
 
 
@@ -600,7 +620,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--part", default="all",
-                    choices=["all", "train", "train_fp8", "scan", "scan_c2", "bert"])
+                    choices=["all", "train", "train_fp8", "train_c4", "scan", "scan_c2",
+                             "scan_c3", "bert"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -627,12 +648,19 @@ def main():
     if args.part in ("all", "train_fp8"):
         _, train8 = run_train(args, rank, world, dev, weights="fp8")
         torch.cuda.empty_cache()
+    train_c4 = None
+    if args.part in ("all", "train_c4"):
+        _, train_c4 = run_train(args, rank, world, dev, cfg=c4_config())
+        torch.cuda.empty_cache()
     bert = None
     if args.part in ("all", "bert"):
         bert = run_train_bert(args, rank, world, dev)
-    scan_fp8 = scan_c4 = None
+    scan_fp8 = scan_c4 = scan_c3 = None
     if args.part == "scan_c2":  # the C2 leg alone (PMC passes: tools/pmc_traffic.sh)
         scan = run_scan(args, rank, world, dev, sweep=False)
+    if args.part in ("all", "scan", "scan_c3"):
+        scan_c3 = run_scan(args, rank, world, dev, C3_N_PER_GPU, "bf16", C3_Q, SCAN_D)
+        torch.cuda.empty_cache()
     if args.part in ("all", "scan"):
         scan = run_scan(args, rank, world, dev)
         torch.cuda.empty_cache()
@@ -657,6 +685,10 @@ def main():
             head = {"value": train["pairs_per_s"], "unit": "pairs/s",
                     "ms_per_step": train["ms_per_step"], "roofline": train["roofline"],
                     "cpu_baseline": cpu_t}
+        elif train_c4 is not None:
+            head = {"value": train_c4["pairs_per_s"], "unit": "pairs/s",
+                    "ms_per_step": train_c4["ms_per_step"], "roofline": train_c4["roofline"],
+                    "cpu_baseline": None}
         elif train8 is not None:
             head = {"value": train8["pairs_per_s"], "unit": "pairs/s",
                     "ms_per_step": train8["ms_per_step"], "roofline": train8["roofline"],
@@ -664,6 +696,10 @@ def main():
         elif bert is not None:
             head = {"value": bert["pairs_per_s"], "unit": "pairs/s",
                     "ms_per_step": bert["ms_per_step"], "roofline": bert["roofline"],
+                    "cpu_baseline": None}
+        elif scan is None:
+            head = {"value": scan_c3["value"], "unit": "queries/s",
+                    "ms_per_step": scan_c3["ms_per_batch"], "roofline": scan_c3["roofline"],
                     "cpu_baseline": None}
         else:
             head = {"value": scan["value"], "unit": "queries/s",
@@ -688,12 +724,23 @@ def main():
                                                    "flops_per_pair", "loss_last")}
         if bert is not None:
             line["train_bert"] = bert
+        if train_c4 is not None:
+            line["train_c4"] = dict(train_c4, workload=(
+                "C4 per-rank step: BERT-large frozen encoder (24L, H=1024, A=16, I=4096, bf16) "
+                "+ 3-layer BiLSTM 1024->256x2->128, 256 pairs per rank (global batch 2048 on "
+                "8 GPUs), L=64, queue 12544"))
         if train8 is not None:
             line["train_fp8"] = dict(train8, workload=(
                 "C5: fp8 (e4m3) frozen-encoder weights, d=768: the C2 step with every BERT-base "
                 "nn.Linear on irc_gemm_fp8 (per-channel weight / per-token input scales)"))
         if scan is not None:
             line["retrieval"] = scan
+        if scan_c3 is not None:
+            scan_c3["workload"] = (f"C3 retrieval shard: {C3_N_PER_GPU} bf16 docs/GPU x D="
+                                   f"{SCAN_D} (1M over 4 GPUs; 384 MB, beyond the 256 MiB "
+                                   f"Infinity Cache), {C3_Q} queries, top-{SCAN_K}; q_sweep "
+                                   "on this shard is the HBM-honest one")
+            line["retrieval_c3"] = scan_c3
         if scan_c4 is not None:
             scan_c4["workload"] = (f"C4 retrieval shard: {FP8_N_PER_GPU} bf16 docs/GPU x D="
                                    f"{C4_D} (BERT-large, 5M over 8 GPUs), {C4_Q} queries, "

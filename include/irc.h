@@ -54,6 +54,13 @@ int irc_scan_topk(const void* queries, const void* docs, int64_t Q, int64_t N, i
                   int64_t k, int64_t doc_offset, void* workspace, int64_t workspace_bytes,
                   float* out_score, int64_t* out_idx, irc_stream_t stream);
 
+/* Rescan statistics of the single-pass scan (Q <= 64): out[0] = queries whose
+ * exact select had to rescan a worker's docs (a truncated 4-key list could hide
+ * a winner), out[1] = workers rescanned, since the last reset.  out is a HOST
+ * pointer to 2 uint64; the call synchronises the device.  Test / diagnostic aid,
+ * no reference counterpart. */
+int irc_scan_rescan_stats(uint64_t* out, int reset);
+
 /* Merge P per-shard sorted top-k lists, in_score/in_idx [P, Q, kin] (global
  * indices, -1 = empty), into out [Q, kout] with the same (score desc, idx asc)
  * rule -- the reduce step of the sharded scan. kout <= 1024. */
@@ -261,7 +268,7 @@ int irc_nce_grads(const float* S, const float* LQ, const float* lse, int64_t N, 
                   float T, const float* gscale, float* GS, float* GQ, irc_stream_t stream);
 int irc_sum(const float* x, int64_t n, float scale, float* partial, float* out,
             irc_stream_t stream);
-int irc_grad_norm_clip(const float* g, int64_t n, float max_norm, float* partial, float* out,
+int irc_grad_norm_clip(const float* g, int64_t n, float max_norm, float* partial, float* out /* >= 3 */,
                        irc_stream_t stream);
 int irc_adam_step(float* p, const float* g, float* m, float* v, int64_t n, const float* coef,
                   float b1, float b2, float step_size, float bc2_sqrt, float eps,
@@ -274,6 +281,18 @@ int irc_adam_step_bf16(float* p, const float* g, float* m, float* v, int64_t n, 
                        void* p_bf16, irc_stream_t stream);
 int irc_momentum_update_bf16(float* pk, const float* pq, int64_t n, float mom, void* pk_bf16,
                              irc_stream_t stream);
+/* Fault gate of a training step (no host sync; replaces nothing in the reference,
+ * whose cuDNN LSTM cannot time out): coef[2] = 1 when *fault_a or *fault_b (uint32
+ * sticky timeout words of irc_lstm_coop_fault; either may be NULL) is set, else 0.
+ * coef is irc_grad_norm_clip's output (>= 3 floats; it sets coef[2] = 0).  The
+ * Adam steps skip every element while coef[2] != 0, and so does
+ * irc_momentum_update_gated (train.py:150-169's update, momentum:
+ * contrastive_module.py:43-53), so a step whose recurrence timed out (its
+ * outputs NaN-poisoned) leaves the parameters, moments and key encoder as they
+ * were.  pk_bf16 may be NULL. */
+int irc_fault_gate(const void* fault_a, const void* fault_b, float* coef, irc_stream_t stream);
+int irc_momentum_update_gated(float* pk, const float* pq, int64_t n, float mom, const float* gate,
+                              void* pk_bf16, irc_stream_t stream);
 int irc_enqueue(float* queue, const float* keys, int64_t* ptr, int64_t D, int64_t K, int64_t B,
                 irc_stream_t stream);
 int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t stream);

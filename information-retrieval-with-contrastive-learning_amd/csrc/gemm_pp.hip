@@ -816,9 +816,15 @@ static int cu_count() {
 
 // Tile-counter slots of the persistent launches, one 64-byte slot per launch in
 // rotation (so launches on concurrent streams never share one); zeroed once, and
-// each launch leaves its slot zeroed again.
+// each launch leaves its slot zeroed again.  A launch being captured into a HIP
+// graph gets no slot (nullptr: the caller takes the one-tile-per-workgroup
+// kernel): a replay would keep its slot forever while the rotation hands the
+// same slot to a later eager launch that may run beside that replay.
 constexpr int PERS_SLOTS = 1024;
-static uint32_t* pers_counter() {
+static uint32_t* pers_counter(hipStream_t st) {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone)
+    return nullptr;
   static std::mutex mu;
   static uint32_t* base[64] = {};
   static std::atomic<uint32_t> next{0};
@@ -843,7 +849,7 @@ void run_scan(const PArgs& a, hipStream_t st, bool fp8) {
   const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
   if (pers_enabled()) {
     const int ncu = cu_count();
-    uint32_t* ctr = (ncu > 0 && tiles > ncu) ? pers_counter() : nullptr;
+    uint32_t* ctr = (ncu > 0 && tiles > ncu) ? pers_counter(st) : nullptr;
     if (ctr != nullptr) {
       const int mode = pers_mode().load(std::memory_order_relaxed);
       if (fp8)
@@ -954,7 +960,7 @@ void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, in
   // persistent form: one launch-wide pass over more tiles than CUs, A K-major
   if (splits == 1 && batch == 1 && a.vec_c && la == 0 && pers_enabled()) {
     const int ncu = cu_count();
-    uint32_t* ctr = (ncu > 0 && tiles > ncu) ? pers_counter() : nullptr;
+    uint32_t* ctr = (ncu > 0 && tiles > ncu) ? pers_counter(st) : nullptr;
     if (ctr != nullptr) {
       if (out_f32) {
         if (lb == 0) launch_pers<true, true, float>(epi, a, (unsigned)ncu, ctr, st);

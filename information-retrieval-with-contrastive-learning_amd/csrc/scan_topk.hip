@@ -1313,6 +1313,9 @@ struct DenseArgs {
   int64_t* out_idx;
 };
 constexpr int SD_XCAP = 2048;  // rescanned keys held at once (>= SEL_MAXK + 4 * TD)
+// [queries whose select rescanned, workers rescanned] since the last reset
+// (irc_scan_rescan_stats): one vector atomic pair per query that rescans.
+__device__ unsigned long long g_dense_rescans[2];
 constexpr int SD_DCAP = 2048;  // docs listed per rescan phase (64 tiles x 32 rows)
 
 // Exact k-th largest nonzero key of v[] (registers, slot i = tid + 256 u) and
@@ -1529,6 +1532,10 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
     if (vflag[w]) vw[atomicAdd(&s_nv, 1u)] = (uint16_t)w;
   __syncthreads();
   const int nv = (int)s_nv;
+  if (nv > 0 && tid == 0) {
+    atomicAdd(&g_dense_rescans[0], 1ull);
+    atomicAdd(&g_dense_rescans[1], (unsigned long long)nv);
+  }
 #ifdef IRC_SCAN_STAMPS  // diagnostic: rescanned workers, queries with a rescan
   if (tid == 0) {
     atomicAdd((unsigned long long*)&dbg_stamps[3][30], (unsigned long long)nv);
@@ -2097,6 +2104,21 @@ extern "C" int irc_scan_dbg_stamps(uint64_t* out /* [4][32] */) {
   (void)out;
   return -1;
 #endif
+}
+
+// Rescan statistics of the single-pass scan's select (host pointer, synchronises
+// the device): out[0] = queries whose select rescanned, out[1] = workers rescanned.
+extern "C" int irc_scan_rescan_stats(uint64_t* out, int reset) {
+  IRC_REQUIRE(out != nullptr, "scan_rescan_stats: null out");
+  if (hipDeviceSynchronize() != hipSuccess) return check_launch("scan_rescan_stats");
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dense_rescans), 2 * sizeof(uint64_t)) != hipSuccess)
+    return check_launch("scan_rescan_stats");
+  if (reset) {
+    const unsigned long long z[2] = {0ull, 0ull};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dense_rescans), z, sizeof(z)) != hipSuccess)
+      return check_launch("scan_rescan_stats");
+  }
+  return IRC_OK;
 }
 
 extern "C" int64_t irc_scan_topk_workspace(int64_t Q, int64_t N, int64_t D, int64_t k) {

@@ -187,6 +187,7 @@ __global__ void finalize_kernel(const float* __restrict__ partial, int np, float
     out[0] = nrm;
     const float coef = max_norm / (nrm + 1e-6f);
     out[1] = coef < 1.f ? coef : 1.f;
+    out[2] = 0.f;  // step gate (irc_fault_gate): 0 = apply the update
   } else {
     out[0] = (float)(s * (double)scale);
   }
@@ -201,6 +202,7 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                             float bc2_sqrt, float eps, unsigned short* __restrict__ pb) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (coef && coef[2] != 0.f) return;  // gated: a recurrence timed out in this step
   const float c = coef ? coef[1] : 1.f;
   const float gi = g[i] * c;
   const float mi = m[i] + (1.f - b1) * (gi - m[i]);  // lerp, as torch
@@ -214,12 +216,24 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
 }
 
 __global__ void momentum_kernel(float* __restrict__ pk, const float* __restrict__ pq, int64_t n,
-                                float mom, unsigned short* __restrict__ pb) {
+                                float mom, unsigned short* __restrict__ pb,
+                                const float* __restrict__ gate) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (gate && gate[2] != 0.f) return;
   const float v = pk[i] * mom + pq[i] * (1.f - mom);
   pk[i] = v;
   if (pb) pb[i] = f32_to_bf16(v);
+}
+
+// coef[2] = 1 when either sticky fault word (the cluster recurrences' timeout
+// words of the query / key encoders) is set: the gated Adam / momentum updates of
+// this step then leave every parameter and moment untouched -- no host sync.
+__global__ void fault_gate_kernel(const unsigned* __restrict__ a, const unsigned* __restrict__ b,
+                                  float* __restrict__ coef) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const bool f = (a != nullptr && *a != 0u) || (b != nullptr && *b != 0u);
+  coef[2] = f ? 1.f : 0.f;
 }
 
 // queue[d, ptr + b] = keys[b, d]
@@ -535,15 +549,32 @@ extern "C" int irc_momentum_update_bf16(float* pk, const float* pq, int64_t n, f
                                         void* pk_bf16, irc_stream_t stream) {
   if (n == 0) return IRC_OK;
   hipLaunchKernelGGL(momentum_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), pk, pq, n,
-                     mom, (unsigned short*)pk_bf16);
+                     mom, (unsigned short*)pk_bf16, nullptr);
   return check_launch("momentum_bf16");
+}
+
+extern "C" int irc_momentum_update_gated(float* pk, const float* pq, int64_t n, float mom,
+                                         const float* gate, void* pk_bf16, irc_stream_t stream) {
+  if (n == 0) return IRC_OK;
+  IRC_REQUIRE(gate != nullptr, "momentum_update_gated: null gate");
+  hipLaunchKernelGGL(momentum_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), pk, pq, n,
+                     mom, (unsigned short*)pk_bf16, gate);
+  return check_launch("momentum_gated");
+}
+
+extern "C" int irc_fault_gate(const void* fault_a, const void* fault_b, float* coef,
+                              irc_stream_t stream) {
+  IRC_REQUIRE(coef != nullptr, "fault_gate: null coef");
+  hipLaunchKernelGGL(fault_gate_kernel, dim3(1), dim3(64), 0, as_stream(stream),
+                     (const unsigned*)fault_a, (const unsigned*)fault_b, coef);
+  return check_launch("fault_gate");
 }
 
 extern "C" int irc_momentum_update(float* pk, const float* pq, int64_t n, float mom,
                                    irc_stream_t stream) {
   if (n == 0) return IRC_OK;
   hipLaunchKernelGGL(momentum_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), pk, pq, n,
-                     mom, nullptr);
+                     mom, nullptr, nullptr);
   return check_launch("momentum");
 }
 

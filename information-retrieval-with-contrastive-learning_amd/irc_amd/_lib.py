@@ -28,6 +28,7 @@ SIGNATURES = {
     "irc_abi_version": (I32, []),
     "irc_scan_topk_workspace": (I64, [I64, I64, I64, I64]),
     "irc_scan_topk": (I32, [P, P, I64, I64, I64, I64, I64, P, I64, P, P, P]),
+    "irc_scan_rescan_stats": (I32, [P, I32]),
     "irc_topk_merge": (I32, [P, P, I64, I64, I64, I64, P, P, P]),
     "irc_scan_scores": (I32, [P, P, I64, I64, I64, P, P]),
     "irc_scan_topk_fp8_workspace": (I64, [I64, I64, I64, I64]),
@@ -80,6 +81,8 @@ SIGNATURES = {
     "irc_sum": (I32, [P, I64, F32, P, P, P]),
     "irc_grad_norm_clip": (I32, [P, I64, F32, P, P, P]),
     "irc_adam_step": (I32, [P, P, P, P, I64, P, F32, F32, F32, F32, F32, P]),
+    "irc_fault_gate": (I32, [P, P, P, P]),
+    "irc_momentum_update_gated": (I32, [P, P, I64, F32, P, P, P]),
     "irc_momentum_update": (I32, [P, P, I64, F32, P]),
     "irc_adam_step_bf16": (I32, [P, P, P, P, I64, P, F32, F32, F32, F32, F32, P, P]),
     "irc_momentum_update_bf16": (I32, [P, P, I64, F32, P, P]),

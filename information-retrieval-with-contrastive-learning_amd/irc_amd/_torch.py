@@ -83,3 +83,10 @@ def workspace(nbytes: int, device: torch.device, tag: str = "default") -> torch.
         buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
         _ws_cache[key] = buf
     return buf
+
+
+def take_workspace(device: torch.device, tag: str):
+    """Remove (device, tag)'s buffer from the shared cache and return it: the caller
+    (a captured HIP graph's slot) keeps it alive and nothing else can grow it."""
+    key = (device.index if device.index is not None else torch.cuda.current_device(), tag)
+    return _ws_cache.pop(key, None)

@@ -319,7 +319,7 @@ def grad_norm_clip(g, max_norm):
     """[||g||, min(1, max_norm / (||g|| + 1e-6))] as a device tensor (no sync)."""
     require_hip(g)
     partial = torch.empty((1024,), dtype=F32, device=g.device)
-    out = torch.empty((2,), dtype=F32, device=g.device)
+    out = torch.empty((4,), dtype=F32, device=g.device)  # [norm, coef, step gate, pad]
     _lib.call("irc_grad_norm_clip", ptr(g), g.numel(), float(max_norm), ptr(partial), ptr(out),
               stream_ptr(g.device))
     return out
@@ -329,6 +329,23 @@ def adam_step(p, g, m, v, coef, b1, b2, step_size, bc2_sqrt, eps):
     require_hip(p, g, m, v, coef)
     _lib.call("irc_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), ptr(coef), float(b1),
               float(b2), float(step_size), float(bc2_sqrt), float(eps), stream_ptr(p.device))
+
+
+def fault_gate(coef, *faults):
+    """coef[2] = 1 if any of the (<= 2) uint32 fault words is set: the gated updates
+    of this step are skipped on the device."""
+    require_hip(coef)
+    f = [t for t in faults if t is not None]
+    if len(f) > 2:
+        raise ValueError("fault_gate takes at most two fault words")
+    f += [None] * (2 - len(f))
+    _lib.call("irc_fault_gate", ptr(f[0]), ptr(f[1]), ptr(coef), stream_ptr(coef.device))
+
+
+def momentum_update_gated(pk, pq, mom, gate, shadow=None):
+    require_hip(pk, pq, gate)
+    _lib.call("irc_momentum_update_gated", ptr(pk), ptr(pq), pk.numel(), float(mom), ptr(gate),
+              ptr(shadow), stream_ptr(pk.device))
 
 
 def momentum_update(pk, pq, mom):

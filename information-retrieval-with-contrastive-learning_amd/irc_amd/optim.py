@@ -44,12 +44,19 @@ class FusedAdam:
             self.exp_avg_sq = self.exp_avg_sq.to(device)
         return self
 
-    def clip_and_step(self, max_norm: float | None = None):
+    def clip_and_step(self, max_norm: float | None = None, faults=()):
         """clip_grad_norm_(max_norm) (if given) + one Adam step; returns the device
-        tensor [norm, coef]."""
+        tensor [norm, coef, gate, -].  ``faults``: device fault words (the cluster
+        recurrences' sticky timeout words); when one is set the update is skipped on
+        the device (coef[2] = 1) -- parameters and moments stay as they were."""
         g = self.head.flat_grad
         m, v = self._moments()
         coef = ops.grad_norm_clip(g, max_norm if max_norm is not None else float("inf"))
+        faults = [f for f in faults if f is not None]
+        if faults:
+            ops.fault_gate(coef, *faults)
+            if max_norm is None:
+                max_norm = float("inf")  # the kernel reads the gate from coef
         self.last_norm = coef
         self.step_count += 1
         t = self.step_count

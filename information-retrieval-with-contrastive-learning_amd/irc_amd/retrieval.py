@@ -13,6 +13,8 @@ per-shard top-k lists and merges them with the same exact rule.
 """
 from __future__ import annotations
 
+import itertools
+
 import torch
 
 from . import _lib
@@ -107,6 +109,16 @@ def scan_scores_fp8(queries: torch.Tensor, docs: torch.Tensor) -> torch.Tensor:
     _lib.call("irc_scan_scores_fp8", ptr(q), ptr(d), q.shape[0], d.shape[0], q.shape[1],
               ptr(out), stream_ptr(q.device))
     return out
+
+
+def rescan_stats(reset: bool = True):
+    """(queries whose single-pass select rescanned, workers rescanned) since the
+    last reset -- synchronises the device (tests / diagnostics)."""
+    import ctypes
+
+    out = (ctypes.c_uint64 * 2)()
+    _lib.call("irc_scan_rescan_stats", ctypes.addressof(out), 1 if reset else 0)
+    return int(out[0]), int(out[1])
 
 
 def topk_merge(scores: torch.Tensor, idx: torch.Tensor, k: int):
@@ -282,7 +294,7 @@ class ShardedDenseIndex:
             st.wait_stream(cur)  # the batch's inputs were produced on `cur`
             with torch.cuda.stream(st):
                 if slots is not None:
-                    g, qin, so, io = slots[n % depth]
+                    g, qin, so, io, _ws = slots[n % depth]
                     qin.copy_(q)
                     g.replay()
                     res = (so.clone(), io.clone())
@@ -298,28 +310,39 @@ class ShardedDenseIndex:
         return out
 
     def _graph_slots(self, q0, k, depth, streams):
-        """Per stream: (graph, static query buffer, static scores, static ids) of the
-        local search for q0's shape, captured once and cached on the index."""
-        key = (tuple(q0.shape), q0.dtype, int(k), depth)
+        """Per stream: (graph, static query buffer, static scores, static ids, workspace)
+        of the local search for q0's shape, captured once and cached on the index.
+
+        Each slot OWNS its scan workspace: it is taken out of the shared grow-only
+        cache right after capture (under a tag no other call uses), so no later
+        call on any index can grow -- and free -- memory a captured graph points
+        into.  The key includes the shard tensor, so replacing ``self.docs``
+        captures anew instead of replaying against the old one."""
+        from ._torch import take_workspace
+
+        key = (tuple(q0.shape), q0.dtype, int(k), depth, self.docs.data_ptr(),
+               tuple(self.docs.shape), self.dtype)
         cache = self.__dict__.setdefault("_graphs", {})
         if key in cache:
             return cache[key]
         slots = []
-        for j, st in enumerate(streams):
+        for st in streams:
             qin = torch.empty_like(q0)
             qin.copy_(q0)
-            tag = f"gscan{j}"
+            tag = f"gscan:{next(_GRAPH_SERIAL)}"
             with torch.cuda.stream(st):
                 self._local_topk(qin, k, tag)  # warm-up: workspace sized outside the graph
             st.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=st):
                 so, io = self._local_topk(qin, k, tag)
-            slots.append((g, qin, so, io))
+            ws = take_workspace(self.docs.device, tag)  # owned by this slot from now on
+            slots.append((g, qin, so, io, ws))
         cache[key] = slots
         return slots
 
 
+_GRAPH_SERIAL = itertools.count()  # unique workspace tags of captured searches
 _SEARCH_STREAMS = {}
 
 

@@ -14,8 +14,9 @@ is the tokenizer's, character for character:
   * the vocab as an open-addressing FNV-1a table over code points, pieces
     stored without their "##" (continuation flag kept separately).
 Building cmap / cls calls the tokenizer's Rust normaliser and pre-tokeniser once
-per code point (~4 s); the result is cached in the temp directory, keyed by the
-tokenizers version and the normaliser / pre-tokeniser configuration.
+per code point (~4 s); the result is cached in a per-user cache directory, keyed
+by the tokenizers version and the normaliser / pre-tokeniser configuration, and
+spot-checked against the tokenizer on load (rebuilt when a check fails).
 
 Not reproduced: special-token strings typed literally in the input text
 ("[SEP]" inside a sentence), which the host tokenizer matches before
@@ -49,6 +50,67 @@ def _fnv(seed, cps):
     return h
 
 
+def _cache_dir():
+    """Per-user cache directory (not the shared temp directory: a stale or planted
+    file there would change every token id the GPU path produces)."""
+    base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
+    d = os.path.join(base, "irc_amd")
+    try:
+        os.makedirs(d, mode=0o700, exist_ok=True)
+        return d
+    except OSError:  # read-only home: a private directory of our own under tmp
+        d = os.path.join(tempfile.gettempdir(), f"irc_amd-{os.getuid()}")
+        os.makedirs(d, mode=0o700, exist_ok=True)
+        return d
+
+
+def _char_entry(norm, pre, c):
+    """(cmap word, pool code points, cls) of code point c: the normaliser's output
+    (1 char inline, several in the pool) and the pre-tokeniser's class."""
+    ch = chr(c)
+    out = norm.normalize_str(ch)
+    word, pool = 0, []
+    if len(out) == 1:
+        word = (ord(out) << 8) | 1
+    elif len(out) > 1:
+        if len(out) > 15:
+            raise ValueError(f"normaliser maps U+{c:04X} to {len(out)} characters")
+        word = (len(out) << 2) | 2  # pool offset added by the caller
+        pool = [ord(o) for o in out]
+    pieces = pre.pre_tokenize_str("a" + ch + "a")
+    cls = 0
+    if len(pieces) == 2 and [p[0] for p in pieces] == ["a", "a"]:
+        cls = 1
+    elif len(pieces) == 3 and pieces[1][0] == ch:
+        cls = 2
+    return word, pool, cls
+
+
+def _tables_valid(norm, pre, cmap, cpool, cls, n_check=512):
+    """Shapes / dtypes of a cached table set, and a spot check of n_check code
+    points (ASCII, Latin-1 and a seeded random sample) against the tokenizer."""
+    if cmap.shape != (N_CP,) or cls.shape != (N_CP,) or cmap.dtype != np.uint32 or \
+            cls.dtype != np.uint8 or cpool.dtype != np.uint32 or cpool.ndim != 1:
+        return False
+    rng = np.random.default_rng(0x1D)
+    sample = list(range(0x20, 0x100)) + [int(c) for c in rng.integers(0x100, N_CP, n_check)]
+    for c in sample:
+        if 0xD800 <= c < 0xE000:
+            continue
+        word, pool, cl = _char_entry(norm, pre, c)
+        if int(cls[c]) != cl:
+            return False
+        got = int(cmap[c])
+        if pool:
+            off, n = got >> 8, (got >> 2) & 15
+            if (got & 3) != 2 or n != len(pool) or off + n > len(cpool) or \
+                    [int(x) for x in cpool[off:off + n]] != pool:
+                return False
+        elif got != word:
+            return False
+    return True
+
+
 def _char_tables(backend):
     """(cmap uint32 [N_CP], cpool uint32, cls uint8 [N_CP]) from the tokenizer."""
     import tokenizers
@@ -57,30 +119,26 @@ def _char_tables(backend):
     key = json.dumps([tokenizers.__version__, str(norm.__getstate__()),
                       str(pre.__getstate__())])
     tag = hashlib.sha1(key.encode()).hexdigest()[:16]
-    path = os.path.join(tempfile.gettempdir(), f"irc_wordpiece_chars_{tag}.npz")
+    path = os.path.join(_cache_dir(), f"wordpiece_chars_{tag}.npz")
     if os.path.exists(path):
-        with np.load(path, allow_pickle=False) as z:  # our own cache file
-            return z["cmap"], z["cpool"], z["cls"]
+        try:
+            with np.load(path, allow_pickle=False) as z:  # our own cache file
+                cmap, cpool, cls = z["cmap"], z["cpool"], z["cls"]
+            if _tables_valid(norm, pre, cmap, cpool, cls):
+                return cmap, cpool, cls
+        except Exception:  # truncated / foreign file: rebuild below
+            pass
     cmap = np.zeros(N_CP, np.uint32)
     cls = np.zeros(N_CP, np.uint8)
     pool = []
     for c in range(N_CP):
         if 0xD800 <= c < 0xE000:
             continue
-        ch = chr(c)
-        out = norm.normalize_str(ch)
-        if len(out) == 1:
-            cmap[c] = (ord(out) << 8) | 1
-        elif len(out) > 1:
-            if len(out) > 15:
-                raise ValueError(f"normaliser maps U+{c:04X} to {len(out)} characters")
-            cmap[c] = (len(pool) << 8) | (len(out) << 2) | 2
-            pool.extend(ord(o) for o in out)
-        pieces = pre.pre_tokenize_str("a" + ch + "a")
-        if len(pieces) == 2 and [p[0] for p in pieces] == ["a", "a"]:
-            cls[c] = 1
-        elif len(pieces) == 3 and pieces[1][0] == ch:
-            cls[c] = 2
+        word, p, cls[c] = _char_entry(norm, pre, c)
+        if p:
+            word |= len(pool) << 8
+            pool.extend(p)
+        cmap[c] = word
     cpool = np.array(pool if pool else [0], np.uint32)
     tmp = path + f".{os.getpid()}.npz"
     np.savez(tmp, cmap=cmap, cpool=cpool, cls=cls)

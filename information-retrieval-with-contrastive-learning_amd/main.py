@@ -4,6 +4,15 @@
                    [--model LSTM|BERT] [--loss InfoNCE] [--opt adam] [--sample uniform|tf_idf]
                    [--seed 1337] [--logdir log] [--ckptdir ckpt] [--retrieval sparse|dense]
 
+Multi-GPU (one process per GPU):
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 main.py [same flags]
+When the launcher sets WORLD_SIZE > 1, the process group is initialised over RCCL
+(backend "nccl") on cuda:LOCAL_RANK before any other GPU call; training is data
+parallel (each rank a disjoint slice of the pairs, global in-batch negatives,
+gradient all-reduce; logging and checkpoints on rank 0) and ``--retrieval dense``
+shards the evidence corpus over the ranks.  IRC_DIST_BACKEND=gloo selects gloo
+(tests that share one GPU between ranks).
+
 --data doc trains (src.train.train); --data fever runs src.evaluation.predict:
 the reference's sparse candidate filter per claim (default) or, with
 ``--retrieval dense``, the bi-encoder's exact top-k over the evidence corpus.  The compute runs on the MI355X HIP kernels only:
@@ -55,8 +64,36 @@ def resolve_device(gpu: str) -> torch.device:
     return torch.device(f"cuda:{first}")
 
 
+def init_distributed():
+    """(group, rank, world, local_rank, created) from the launcher's environment
+    (torch.distributed.run / torchrun: WORLD_SIZE, RANK, LOCAL_RANK, MASTER_*), or
+    (None, 0, 1, None, False) for a single process; created: this call initialised
+    the default process group (main() then also destroys it).  Runs before any other GPU call:
+    RCCL's communicator is bound to cuda:LOCAL_RANK (device_id)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return None, 0, 1, None, False
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    backend = os.environ.get("IRC_DIST_BACKEND", "nccl")
+    created = not dist.is_initialized()
+    if created:
+        if backend == "nccl":
+            dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return dist.group.WORLD, dist.get_rank(), dist.get_world_size(), local, created
+
+
 def main(argv=None):
     args = get_args(argv)
+    group, rank, world, local, created = init_distributed()
+    args.dist_group, args.rank, args.world_size = group, rank, world
     torch.cuda.manual_seed(args.seed)
     torch.manual_seed(args.seed)
     np.random.seed(args.seed)
@@ -69,6 +106,8 @@ def main(argv=None):
 
         set_precision(prec)
     args.device = resolve_device(args.gpu)
+    if local is not None:  # one GPU per rank: cuda:LOCAL_RANK (wrapped on a shared box)
+        args.device = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     if args.data == "doc":
         from src.train import train
 
@@ -79,6 +118,11 @@ def main(argv=None):
         predict(args)
     else:
         raise SystemExit(f"unknown --data {args.data!r}")
+    if created:
+        import torch.distributed as dist
+
+        dist.barrier(group)
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -142,13 +142,20 @@ class RetrievalModelWrapper(nn.Module):
         return out[:n_anchor], out[n_anchor:]
 
     @torch.no_grad()
-    def _momentum_update_key_encoder(self):
+    def _momentum_update_key_encoder(self, gate=None):
         """theta_k <- m theta_k + (1 - m) theta_q: one fused launch over the flat buffers
-        (for the trainable BERT also rewriting encoder_k's bf16 operand shadow)."""
+        (for the trainable BERT also rewriting encoder_k's bf16 operand shadow).
+        ``gate`` (superset): the step's [norm, coef, gate] device tensor; the update
+        is skipped on the device when gate[2] is set (a recurrence timed out)."""
         mom = float(self.loss_config["momentum"])
         shadow = self.encoder_k.shadow_buffer() if hasattr(self.encoder_k, "shadow_buffer") \
             else None
-        if shadow is not None:
+        if gate is not None:
+            ops.momentum_update_gated(self.encoder_k.flat.detach(), self.encoder_q.flat.detach(),
+                                      mom, gate, shadow)
+            if hasattr(self.encoder_k, "after_update"):
+                self.encoder_k.after_update(shadow is not None)
+        elif shadow is not None:
             ops.momentum_update_bf16(self.encoder_k.flat.detach(), self.encoder_q.flat.detach(),
                                      mom, shadow)
             self.encoder_k.after_update(True)

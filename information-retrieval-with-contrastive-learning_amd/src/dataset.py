@@ -96,7 +96,14 @@ class FeverDataset(Dataset):
         return data
 
 
-def get_dataloader(args, train=True):
+def get_dataloader(args, train=True, distributed=None):
+    """dataset.py:159-182.  Under data parallelism (``args.dist_group`` set by
+    main.py from the launcher's WORLD_SIZE / RANK) each rank reads a disjoint
+    slice of the dataset through a DistributedSampler (shuffled per epoch with
+    ``args.seed``; ``set_epoch`` is called by the training loop), so the global
+    batch is ``batch_size * world`` distinct pairs.  ``distributed=False`` keeps
+    the whole dataset on every rank (the ProtoNCE feature pass, whose clustering
+    must be identical on every rank)."""
     bsz = args.config["train"]["batch_size"] if train else args.config["eval"]["batch_size"]
     n_jobs = args.config["train"]["n_jobs"] if train else args.config["eval"]["n_jobs"]
     if args.data == "doc":
@@ -106,6 +113,18 @@ def get_dataloader(args, train=True):
         collate_fn = dataset.collate_fn
     else:
         raise ValueError(args.data)
-    return torch.utils.data.DataLoader(dataset, batch_size=bsz, shuffle=train, num_workers=n_jobs,
-                                       drop_last=train, pin_memory=torch.cuda.is_available(),
+    group = getattr(args, "dist_group", None)
+    if distributed is None:
+        distributed = train
+    sampler = None
+    if distributed and group is not None:
+        import torch.distributed as dist
+
+        sampler = torch.utils.data.distributed.DistributedSampler(
+            dataset, num_replicas=dist.get_world_size(group), rank=dist.get_rank(group),
+            shuffle=train, seed=int(getattr(args, "seed", 0)), drop_last=train)
+    return torch.utils.data.DataLoader(dataset, batch_size=bsz,
+                                       shuffle=train if sampler is None else False,
+                                       sampler=sampler, num_workers=n_jobs, drop_last=train,
+                                       pin_memory=torch.cuda.is_available(),
                                        collate_fn=collate_fn)

@@ -72,7 +72,9 @@ def predict(args, k=100):
     assert args.ckpt is not None
     _, model, _, _ = load_model(args.ckpt)
     model = model.to(args.device)
-    fever_loader = get_dataloader(args, train=False)
+    # data parallel: each rank filters a disjoint share of the claim batches
+    fever_loader = get_dataloader(args, train=False,
+                                  distributed=getattr(args, "dist_group", None) is not None)
     ds = args.config["dataset"]
     _, metadata = load_sparse_csr(ds["tfidf"])
     count_matrix, _ = load_sparse_csr(ds["inverted_file"])
@@ -93,11 +95,23 @@ def predict(args, k=100):
 @torch.no_grad()
 def predict_dense(args, k=100):
     """Dense claim -> evidence-line retrieval with the trained bi-encoder: prints
-    each batch's latency and the evidence recall@k; returns recall@k."""
+    each batch's latency and the evidence recall@k; returns recall@k.
+
+    Under data parallelism (``args.dist_group``, main.py under torchrun) the
+    evidence corpus is sharded: rank r encodes and keeps only its contiguous
+    slice (irc_amd.retrieval.shard_bounds) in HBM, each claim batch is split over
+    the ranks, and ShardedDenseIndex.search all-gathers the claim embeddings,
+    scans every shard and merges the per-shard top-k -- every rank receives the
+    global result for the whole batch."""
+    from irc_amd.retrieval import shard_bounds
+
     assert args.ckpt is not None
     _, model, _, _ = load_model(args.ckpt)
     model = model.to(args.device).eval()
-    loader = get_dataloader(args, train=False)
+    loader = get_dataloader(args, train=False, distributed=False)
+    group = getattr(args, "dist_group", None)
+    world = int(getattr(args, "world_size", 1)) if group is not None else 1
+    rank = int(getattr(args, "rank", 0)) if group is not None else 0
     # evidence corpus = every evidence document line of the dev set's wiki pages
     titles, texts = [], []
     for title, page in loader.dataset.wiki.items():
@@ -105,19 +119,27 @@ def predict_dense(args, k=100):
             if line.strip():
                 titles.append(title)
                 texts.append(line)
-    index = ShardedDenseIndex(encode_corpus(model, texts, args.device))
+    lo, hi = shard_bounds(len(texts), world, rank)
+    index = ShardedDenseIndex(encode_corpus(model, texts[lo:hi], args.device), doc_offset=lo,
+                              group=group)
+    dim = model.loss_config["dim"]
     hits = total = 0
-    for batch in tqdm(loader, desc="Iteration"):
+    for batch in tqdm(loader, desc="Iteration", disable=rank != 0):
         claims = [d["claim"] for d in batch]
         s = time.time()
-        q = model.ctx2vec(claims, args.device)
-        scores, idx = index.search(q, k)
+        c0, c1 = shard_bounds(len(claims), world, rank)
+        mine = claims[c0:c1]
+        q = model.ctx2vec(mine, args.device) if mine else \
+            torch.empty((0, dim), dtype=torch.float32, device=args.device)
+        scores, idx = index.search(q, k)  # rows: the whole batch, in order
         torch.cuda.synchronize()
-        print(f"batch of {len(claims)} claims: {time.time() - s:.4f}s")
+        if rank == 0:
+            print(f"batch of {len(claims)} claims: {time.time() - s:.4f}s")
         idx = idx.cpu().tolist()
         for d, row in zip(batch, idx):
             gold = {e["title"] for e in d["evidences"]}
             hits += int(any(titles[j] in gold for j in row if j >= 0))
             total += 1
-    print(f"evidence recall@{k}: {hits / max(total, 1):.4f}")
+    if rank == 0:
+        print(f"evidence recall@{k}: {hits / max(total, 1):.4f}")
     return hits / max(total, 1)

@@ -60,11 +60,13 @@ def build_model(args):
 
 def save_model(model, optimizer, args, current_step):
     path = f"{args.ckptdir}/{args.sample}_{args.loss}_{args.model}_{current_step}.pth"
+    # the live process group is a handle of this run, not a setting: not stored
+    saved_args = argparse.Namespace(**{k: v for k, v in vars(args).items() if k != "dist_group"})
     all_states = {
         "Model": model.state_dict(),
         "Optimizer": optimizer.state_dict(),
         "Current_step": current_step,
-        "Args": args,
+        "Args": saved_args,
     }
     torch.save(all_states, path)
 

@@ -9,6 +9,12 @@ catch-and-skip (matching "HIP out of memory" as well as the CUDA text).
 
 Differences on purpose: the clip is fused into the optimizer step (no host
 sync); TensorBoard is used when importable, else the scalars are printed.
+
+Data parallel (main.py under torchrun sets ``args.dist_group``): every rank
+steps its own disjoint micro-batches (DistributedSampler, reseeded per epoch),
+the embeddings are all-gathered for global in-batch negatives and the head
+gradient all-reduced (TrainState.set_process_group); the log directory, the
+scalars, the progress bar and the checkpoints belong to rank 0.
 """
 import math
 import os
@@ -23,6 +29,14 @@ from src.contrastor.utils import run_hierarchical_clustering, run_kmeans
 from src.model import build_model, get_optimizer, load_model, save_model
 
 OOM_MARKERS = ("CUDA out of memory", "HIP out of memory", "out of memory")
+
+
+class _NullWriter:
+    def add_scalar(self, tag, value, step):
+        pass
+
+    def close(self):
+        pass
 
 
 class _PrintWriter:
@@ -89,6 +103,16 @@ class TrainState:
             if enc is not None and hasattr(enc, "check_fault"):
                 enc.check_fault()
 
+    def fault_words(self):
+        """The heads' sticky device fault words (cluster recurrences), if any."""
+        out = []
+        for name in ("encoder_q", "encoder_k"):
+            enc = getattr(self.model, name, None)
+            w = getattr(enc, "coop_fault", None)
+            if w is not None and w.is_cuda:
+                out.append(w)
+        return out
+
     def _maybe_enable_queue(self):
         m = self.model
         if m.use_queue and self.step_sum >= self.cfg["loss"][self.args.loss]["queue_start_steps"] \
@@ -127,9 +151,15 @@ class TrainState:
                 from irc_amd.dist import all_reduce_sum_
 
                 all_reduce_sum_(self.model.encoder_q.flat_grad, self.process_group)
-            self.grad_norm = self.optimizer.clip_and_step(self.max_norm)
-            if self.model.use_momentum:
-                self.model._momentum_update_key_encoder()
+            faults = self.fault_words()
+            if faults:  # a timed-out recurrence's step changes no parameter (no host sync)
+                self.grad_norm = self.optimizer.clip_and_step(self.max_norm, faults=faults)
+                if self.model.use_momentum:
+                    self.model._momentum_update_key_encoder(gate=self.grad_norm)
+            else:
+                self.grad_norm = self.optimizer.clip_and_step(self.max_norm)
+                if self.model.use_momentum:
+                    self.model._momentum_update_key_encoder()
             self.optimizer.zero_grad()
             self.loss_record.append(self.loss_sum)
             self.step_sum += 1
@@ -137,6 +167,17 @@ class TrainState:
             self.loss_sum = 0.0
             stepped = True
         return loss, stepped
+
+
+def _log_and_save(log, pbar, model, optimizer, args, step, loss_avg, grad_norm):
+    """train.py:178-188 (rank 0 only under data parallelism)."""
+    if math.isnan(grad_norm) or math.isinf(grad_norm):
+        print(f"[Runner] - Error : grad norm is nan/inf at step {step}")
+    log.add_scalar("train_loss", loss_avg, step)
+    log.add_scalar("grad_norm", grad_norm, step)
+    pbar.set_description("Train_Loss %.5f" % (loss_avg))
+    print("Train_Loss %.5f" % (loss_avg))
+    save_model(model, optimizer, args, step)
 
 
 def train(args):
@@ -168,18 +209,26 @@ def train(args):
             return fn(cfg, feat_loader, model, args.device)
         return cluster_result
 
+    group = getattr(args, "dist_group", None)
+    rank0 = int(getattr(args, "rank", 0)) == 0
     args.logdir = f"{args.logdir}/{args.loss}_{args.model}"
-    if os.path.isdir(args.logdir):
-        shutil.rmtree(args.logdir)
-    os.makedirs(args.logdir)
-    log = _writer(args.logdir)
-    os.makedirs(args.ckptdir, exist_ok=True)
+    if rank0:
+        if os.path.isdir(args.logdir):
+            shutil.rmtree(args.logdir)
+        os.makedirs(args.logdir)
+        os.makedirs(args.ckptdir, exist_ok=True)
+    log = _writer(args.logdir) if rank0 else _NullWriter()
 
     st = TrainState(args, model, optimizer, init_step)
+    if group is not None:
+        st.set_process_group(group)
     total_steps = args.config["train"]["total_steps"]
     log_step = int(args.config["train"]["log_step"])
-    print("[Runner] - Start training")
-    pbar = tqdm(initial=init_step, total=total_steps, dynamic_ncols=True)
+    if rank0:
+        print("[Runner] - Start training")
+    pbar = tqdm(initial=init_step, total=total_steps, dynamic_ncols=True, disable=not rank0)
+    sampler = getattr(train_loader, "sampler", None)
+    epoch = 0
 
     # LSTM heads on frozen BERT: the next micro-batch's BERT features are issued on
     # a side stream before this micro-batch's heads step (bert_extract_async), so
@@ -191,6 +240,9 @@ def train(args):
         return idx, model.bert_extract_texts_async(a, p, args.device)
 
     while st.step_sum < total_steps:
+        if hasattr(sampler, "set_epoch"):  # DistributedSampler: a new permutation per pass
+            sampler.set_epoch(epoch)
+        epoch += 1
         it = iter(train_loader)
         nxt = next(it, None)
         pending = _issue(nxt) if (prefetch and nxt is not None) else None
@@ -223,13 +275,9 @@ def train(args):
                         st.loss_record = []
                         grad_norm = float(st.grad_norm[0].item())
                         st.check_faults()
-                        if math.isnan(grad_norm) or math.isinf(grad_norm):
-                            print(f"[Runner] - Error : grad norm is nan/inf at step {st.step_sum}")
-                        log.add_scalar("train_loss", loss_avg, st.step_sum)
-                        log.add_scalar("grad_norm", grad_norm, st.step_sum)
-                        pbar.set_description("Train_Loss %.5f" % (loss_avg))
-                        print("Train_Loss %.5f" % (loss_avg))
-                        save_model(model, optimizer, args, st.step_sum)
+                        if rank0:
+                            _log_and_save(log, pbar, model, optimizer, args, st.step_sum,
+                                          loss_avg, grad_norm)
             except RuntimeError as e:
                 if not any(m in str(e) for m in OOM_MARKERS):
                     raise

@@ -156,6 +156,71 @@ def gen_nce_c2(out):
     print("nce_c2:", {k: v for k, v in res.items() if k.endswith("_loss")})
 
 
+def gen_nce_c34(out):
+    """NCELoss at the C3 / C4 global batches (N = 1024 and 2048, D = 128,
+    K = 12544), with and without the queue: the same fixture layout as nce_c2.
+    Plus the reference's enqueue rule at these batch sizes: 12544 % B != 0, so
+    _dequeue_and_enqueue (contrastive_module.py:55-68) leaves queue and queue_ptr
+    untouched -- recorded from the reference method itself."""
+    import types as _types
+
+    sys.path.insert(0, os.path.dirname(HERE))
+    import synth_inputs as SI
+    from src.contrastor.contrastive_loss import NCELoss
+    from src.contrastor.contrastive_module import RetrievalModelWrapper
+
+    res = {}
+    for (n, d, kq, seed) in SI.NCE_C34_CASES:
+        q, k, queue = SI.nce_c2_inputs(n, d, kq, seed)
+        crit = NCELoss({"temperature": 0.05})
+        for with_q in (False, True):
+            qq = torch.from_numpy(q).clone().requires_grad_(True)
+            loss = crit(qq, torch.from_numpy(k), torch.from_numpy(queue) if with_q else None)
+            loss.backward()
+            dq = _np(qq.grad)
+            tag = f"n{n}_d{d}_k{kq}_{'q' if with_q else 'noq'}"
+            res[f"{tag}_loss"] = np.float64(loss.item())
+            res[f"{tag}_dq_head"] = dq[:16]
+            res[f"{tag}_dq_tail"] = dq[-16:]
+            res[f"{tag}_dq_rownorm"] = np.linalg.norm(dq.astype(np.float64), axis=1)
+            res[f"{tag}_dq_colsum"] = dq.astype(np.float64).sum(axis=0)
+        # the reference's enqueue at B = n (and at B = 256 for contrast)
+        for b in (n, 256):
+            me = _types.SimpleNamespace(
+                queue=torch.from_numpy(queue.copy()), queue_ptr=torch.zeros(1, dtype=torch.long),
+                loss_config={"queue_size": kq})
+            RetrievalModelWrapper._dequeue_and_enqueue(me, torch.from_numpy(k[:b]))
+            res[f"enq_b{b}_k{kq}_ptr"] = np.int64(int(me.queue_ptr[0]))
+            res[f"enq_b{b}_k{kq}_changed_cols"] = np.int64(
+                int((me.queue.numpy() != queue).any(axis=0).sum()))
+    np.savez_compressed(os.path.join(out, "nce_c34.npz"), **res)
+    print("nce_c34:", {k: v for k, v in res.items() if k.endswith("_loss") or "enq" in k})
+
+
+def gen_bert_large(out):
+    """HF BertModel at BERT-large size (24 layers, H = 1024, A = 16, I = 4096),
+    the frozen encoder of config C4, B = 2, L = 64 with padding; weights from the
+    same per-parameter numpy streams as gen_bert_base."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    import synth_inputs as SI
+    from transformers import BertConfig, BertModel
+
+    m = BertModel(BertConfig(**SI.BERT_LARGE)).eval()
+    sd = {n: torch.from_numpy(SI.bert_param(n, tuple(v.shape)))
+          for n, v in m.state_dict().items() if "position_ids" not in n}
+    missing = m.load_state_dict(sd, strict=False).missing_keys
+    assert not [n for n in missing if "position_ids" not in n], missing
+    ids, mask = SI.bert_base_batch(seed=8, lens=SI.BERT_LARGE_LENS)
+    with torch.no_grad():
+        hs = m(input_ids=torch.from_numpy(ids), attention_mask=torch.from_numpy(mask))
+    hs = _np(hs.last_hidden_state)
+    pooled = hs.astype(np.float64).mean(axis=1)
+    np.savez_compressed(os.path.join(out, "bert_large.npz"), input_ids=ids, attention_mask=mask,
+                        last_hidden_state=hs,
+                        seq2vec=(pooled / np.linalg.norm(pooled, axis=1, keepdims=True)))
+    print("bert_large:", hs.shape, float(np.abs(hs).mean()))
+
+
 def gen_bert_base(out):
     """HF BertModel at BERT-base size (12 layers, H = 768, A = 12, I = 3072) with
     padding, B = 4, L = 64 -- the frozen encoder of config C2 as the reference
@@ -455,7 +520,9 @@ def main():
             return
         gen_nce(HERE)
         gen_nce_c2(HERE)
+        gen_nce_c34(HERE)
         gen_bert_base(HERE)
+        gen_bert_large(HERE)
         gen_lstm_init(HERE)
         gen_seq2vec(HERE, tmp)
         gen_bert(HERE, tmp)

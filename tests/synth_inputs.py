@@ -20,6 +20,8 @@ def unit_cols(seed, d, k):
 
 
 NCE_C2_CASES = [(256, 128, 12544, 21), (256, 768, 12544, 22)]  # (N, D, K, seed)
+# C3 / C4 global batches (B = 1024 over 4 GPUs, 2048 over 8) with the LSTM head's D
+NCE_C34_CASES = [(1024, 128, 12544, 31), (2048, 128, 12544, 32)]
 
 
 def nce_c2_inputs(n, d, k, seed):
@@ -28,6 +30,11 @@ def nce_c2_inputs(n, d, k, seed):
 
 BERT_BASE = dict(vocab_size=30522, hidden_size=768, num_hidden_layers=12, num_attention_heads=12,
                  intermediate_size=3072, max_position_embeddings=512)
+
+
+BERT_LARGE = dict(vocab_size=30522, hidden_size=1024, num_hidden_layers=24,
+                  num_attention_heads=16, intermediate_size=4096, max_position_embeddings=512)
+BERT_LARGE_LENS = (64, 29)  # B = 2 sequences, one full length, one padded
 
 
 def bert_param(name, shape):

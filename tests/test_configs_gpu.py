@@ -106,7 +106,7 @@ def test_bert_base_12_layers_bf16(gpu):
 
 
 # ------------------------------------------------------------------ C2 train step
-def _c2_step(gpu, precision):
+def _c2_step(gpu, precision, weights="bf16", B=256):
     from bench import c2_config, synthetic_batch
     from irc_amd.precision import get_precision, set_precision
     from src.model import build_model, get_optimizer
@@ -115,16 +115,18 @@ def _c2_step(gpu, precision):
     set_precision(precision)
     try:
         cfg = c2_config()
+        cfg["train"].update(batch_size=B, acml_batch_size=B)
         ns = argparse.Namespace(config=cfg, loss="InfoNCE", model="LSTM", opt="adam",
                                 sample="uniform")
         torch.manual_seed(1337)
         model = build_model(ns).to(gpu).train()
+        model.bert_model.set_weight_format(weights)
         model.add_queue_to_loss = True
         opt = get_optimizer(ns, model)
-        ids, mask = synthetic_batch(512, 64, 1337)
+        ids, mask = synthetic_batch(2 * B, 64, 1337)
         ids, mask = ids.to(gpu), mask.to(gpu)
         queue0 = model.queue.clone()
-        a, p = model.bert_extract_ids(ids, mask, 256)
+        a, p = model.bert_extract_ids(ids, mask, B)
         with torch.no_grad():
             emb_k = model.seq2vec(p, query=False)
         loss = model.forward_features(a, p)  # heads, loss, enqueue
@@ -153,6 +155,101 @@ def test_c2_train_step_full_size(gpu):
     assert int(m16.queue_ptr.item()) == 256
     assert torch.equal(m16.queue[:, 256:], q0[:, 256:])
     np.testing.assert_allclose(m16.queue[:, :256].T.cpu().numpy(), k16.cpu().numpy(), atol=1e-6)
+
+
+def test_c5_fp8_step_loss_vs_fp32(gpu):
+    """C5: the C2 step with every frozen-encoder nn.Linear on e4m3 (per-channel
+    weight, per-token input scales).  Its InfoNCE loss against the fp32-mode step
+    on the same inputs and initial weights: the fp8 quantisation of 72 GEMM inputs
+    perturbs the features (pooled cosine ~0.998, tests/test_fp8_encoder_gpu.py), so
+    the bound is looser than bf16's 1e-3; the measured delta is printed."""
+    l8, g8, _, _, _, m8 = _c2_step(gpu, "bf16", weights="fp8")
+    l32, g32, _, _, _, _ = _c2_step(gpu, "fp32")
+    rel = abs(l8 - l32) / abs(l32)
+    grel = ((g8 - g32).norm() / g32.norm()).item()
+    print(f"C5 fp8 step: loss {l8:.6f} vs fp32 {l32:.6f} (rel {rel:.2e}); grad rel {grel:.2e}")
+    assert np.isfinite(l8)
+    assert rel <= 5e-3
+    assert grel <= 0.25
+    assert torch.isfinite(m8.encoder_q.flat).all()
+
+
+@pytest.mark.parametrize("case", [0, 1])
+@pytest.mark.parametrize("with_q", [False, True])
+def test_nce_c34_global_batch_vs_reference(gpu, case, with_q):
+    """C3 / C4 global batches: NCELoss at N = 1024 and 2048 (D = 128, K = 12544)
+    against the reference's values (tests/golden/nce_c34.npz)."""
+    from irc_amd.nce import info_nce
+
+    g = load_golden("nce_c34.npz")
+    n, d, kq, seed = SI.NCE_C34_CASES[case]
+    q, k, queue = SI.nce_c2_inputs(n, d, kq, seed)
+    tag = f"n{n}_d{d}_k{kq}_{'q' if with_q else 'noq'}"
+    qq = torch.from_numpy(q).to(gpu).requires_grad_(True)
+    loss = info_nce(qq, torch.from_numpy(k).to(gpu),
+                    torch.from_numpy(queue).to(gpu) if with_q else None, 0.05)
+    loss.backward()
+    dq = qq.grad.cpu().numpy().astype(np.float64)
+    ref = float(g[f"{tag}_loss"])
+    rel = abs(loss.item() - ref) / abs(ref)
+    print(f"{tag}: loss {loss.item():.4f} vs reference {ref:.4f} (rel {rel:.2e})")
+    assert rel <= 1e-5
+    np.testing.assert_allclose(dq[:16], g[f"{tag}_dq_head"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(dq[-16:], g[f"{tag}_dq_tail"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(np.linalg.norm(dq, axis=1), g[f"{tag}_dq_rownorm"], rtol=1e-4)
+    np.testing.assert_allclose(dq.sum(axis=0), g[f"{tag}_dq_colsum"], rtol=1e-3, atol=1e-4)
+
+
+def test_c3_global_batch_step_never_enqueues(gpu):
+    """One full training step at global B = 1024 (C3) on one GPU: 12544 % 1024 != 0,
+    so the reference never enqueues (contrastive_module.py:59; nce_c34.npz holds
+    the reference's own behaviour) -- queue and queue_ptr stay bit-identical."""
+    g = load_golden("nce_c34.npz")
+    assert int(g["enq_b1024_k12544_ptr"]) == 0
+    loss, grad, coef, _, q0, m = _c2_step(gpu, "bf16", B=1024)
+    print(f"C3 step B=1024: loss {loss:.4f}, grad norm {coef[0].item():.4f}")
+    assert np.isfinite(loss) and torch.isfinite(grad).all()
+    assert int(m.queue_ptr.item()) == 0
+    assert torch.equal(m.queue, q0)
+
+
+# ------------------------------------------------------------------ C4 encoder
+def _bert_large_out(gpu):
+    from irc_amd.bert import BertConfig, BertModel
+
+    g = load_golden("bert_large.npz")
+    m = BertModel(BertConfig(**SI.BERT_LARGE))
+    sd = {n: torch.from_numpy(SI.bert_param(n, tuple(v.shape)))
+          for n, v in m.state_dict().items() if "position_ids" not in n}
+    missing = m.load_state_dict(sd, strict=False).missing_keys
+    assert not [n for n in missing if "position_ids" not in n]
+    m = m.to(gpu)
+    out = m.encode(torch.from_numpy(g["input_ids"]).to(gpu),
+                   torch.from_numpy(g["attention_mask"]).to(gpu)).float().cpu().numpy()
+    return g, out
+
+
+def test_bert_large_24_layers_fp32(gpu, fp32_mode):
+    """C4 encoder: BERT-large (24 layers, H=1024, A=16, I=4096) in fp32 parity
+    mode against HF's last_hidden_state."""
+    g, out = _bert_large_out(gpu)
+    err = np.abs(out - g["last_hidden_state"]).max()
+    print(f"BERT-large fp32 mode: max abs err {err:.2e}")
+    np.testing.assert_allclose(out, g["last_hidden_state"], rtol=1e-4, atol=3e-4)
+
+
+def test_bert_large_24_layers_bf16(gpu):
+    """C4 encoder in production precision: error stated, pooled direction held to
+    cosine >= 0.9999 of the reference's."""
+    g, out = _bert_large_out(gpu)
+    err = np.abs(out - g["last_hidden_state"]).max()
+    rms = np.sqrt(np.mean((out - g["last_hidden_state"]) ** 2))
+    pooled = out.astype(np.float64).mean(axis=1)
+    pooled /= np.linalg.norm(pooled, axis=1, keepdims=True)
+    cos = (pooled * g["seq2vec"]).sum(axis=1)
+    print(f"BERT-large bf16: max abs err {err:.3e}, rms {rms:.3e}, pooled cosine {cos.min():.6f}")
+    assert err <= 0.25 and rms <= 0.03
+    assert cos.min() >= 0.9999
 
 
 # ------------------------------------------------------------------ C3 / C4 shards

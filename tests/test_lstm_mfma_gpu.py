@@ -213,3 +213,47 @@ def test_coop_forced_timeout_raises_in_train_step(gpu, forced_coop_timeout, bf16
     mask = torch.ones_like(ids)
     with pytest.raises(IRCError, match="timed out"):
         st.micro_batch(32, lambda: model.forward_features(*model.bert_extract_ids(ids, mask, 32)))
+
+
+def test_coop_forced_timeout_step_changes_no_parameter(gpu, forced_coop_timeout, bf16_mode):
+    """between a timeout and the raise at log_step the loop
+    takes steps without syncing; the fault word gates Adam and the momentum update
+    on the device, so those steps change no parameter, moment or key-encoder
+    weight (and nothing turns NaN)."""
+    import argparse
+
+    import yaml
+
+    from conftest import PKG
+    from src.model import build_model, get_optimizer
+    from src.train import TrainState
+
+    with open(f"{PKG}/config.yaml") as f:
+        cfg = yaml.safe_load(f)
+    cfg["bert"] = {"name": "tiny", "config": {"vocab_size": 200, "hidden_size": 64,
+                                              "num_hidden_layers": 1, "num_attention_heads": 2,
+                                              "intermediate_size": 128,
+                                              "max_position_embeddings": 64}}
+    cfg["model"]["LSTM"].update(input_size=64, hidden_size=H, num_layers=2, output_size=32)
+    cfg["loss"]["InfoNCE"].update(queue_size=64)
+    cfg["train"].update(batch_size=32, acml_batch_size=32)
+    args = argparse.Namespace(config=cfg, loss="InfoNCE", model="LSTM", opt="adam",
+                              sample="uniform")
+    torch.manual_seed(0)
+    model = build_model(args).to(gpu).train()
+    opt = get_optimizer(args, model)
+    st = TrainState(args, model, opt)
+    q0, k0 = model.encoder_q.flat.detach().clone(), model.encoder_k.flat.detach().clone()
+    ids = torch.randint(5, 200, (64, 16), device=gpu)
+    mask = torch.ones_like(ids)
+    for _ in range(2):  # sync_loss=False: the production loop's no-sync micro-batches
+        _, stepped = st.micro_batch(
+            32, lambda: model.forward_features(*model.bert_extract_ids(ids, mask, 32)),
+            sync_loss=False)
+        assert stepped
+    torch.cuda.synchronize()
+    assert int(model.encoder_q.coop_fault.item()) != 0
+    assert float(st.grad_norm[2].item()) == 1.0  # gated
+    assert torch.equal(model.encoder_q.flat.detach(), q0)
+    assert torch.equal(model.encoder_k.flat.detach(), k0)
+    assert torch.isfinite(opt.exp_avg).all() and not opt.exp_avg.any()

@@ -213,16 +213,10 @@ def test_nce_c2_shapes_match_reference(case):
         np.testing.assert_allclose(dq.sum(axis=0), g[f"{tag}_dq_colsum"], rtol=1e-4, atol=1e-5)
 
 
-def test_bert_base_12_layers_matches_reference():
-    """The oracle's BERT at BERT-base size (12 layers, H=768) against HF's
-    last_hidden_state (the reference's frozen encoder), padded B=4, L=64."""
-    import synth_inputs as SI
-
-    g = load_golden("bert_base.npz")
+def _bert_shapes(cfg):
     names = ["embeddings.word_embeddings.weight", "embeddings.position_embeddings.weight",
              "embeddings.token_type_embeddings.weight", "embeddings.LayerNorm.weight",
              "embeddings.LayerNorm.bias"]
-    cfg = SI.BERT_BASE
     H, I = cfg["hidden_size"], cfg["intermediate_size"]
     shapes = {names[0]: (cfg["vocab_size"], H), names[1]: (cfg["max_position_embeddings"], H),
               names[2]: (2, H), names[3]: (H,), names[4]: (H,)}
@@ -234,10 +228,48 @@ def test_bert_base_12_layers_matches_reference():
             shapes[p + n + ".weight"], shapes[p + n + ".bias"] = s, (s[0],)
         for n in ("attention.output.LayerNorm", "output.LayerNorm"):
             shapes[p + n + ".weight"] = shapes[p + n + ".bias"] = (H,)
-    w = {n: SI.bert_param(n, s) for n, s in shapes.items()}
+    return shapes
+
+
+@pytest.mark.parametrize("size", ["base", "large"])
+def test_bert_matches_reference(size):
+    """The oracle's BERT against HF's last_hidden_state (the reference's frozen
+    encoder): BERT-base (12 layers, H=768; padded B=4, L=64) and BERT-large
+    (config C4: 24 layers, H=1024, A=16, I=4096; padded B=2, L=64)."""
+    import synth_inputs as SI
+
+    g = load_golden(f"bert_{size}.npz")
+    cfg = SI.BERT_BASE if size == "base" else SI.BERT_LARGE
+    w = {n: SI.bert_param(n, s) for n, s in _bert_shapes(cfg).items()}
     hs = O.bert_forward(g["input_ids"], g["attention_mask"], w, cfg["num_hidden_layers"],
                         cfg["num_attention_heads"])
-    np.testing.assert_allclose(hs, g["last_hidden_state"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(hs, g["last_hidden_state"], rtol=1e-4, atol=2e-4)
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_nce_c34_global_batch_matches_reference(case):
+    """NCELoss at the C3 / C4 global batches (N = 1024 / 2048, D = 128, K = 12544)
+    against the reference's values, and the reference's enqueue rule at those B:
+    12544 % B != 0, so the queue and its pointer stay untouched (the golden holds
+    what the reference's own _dequeue_and_enqueue did)."""
+    import synth_inputs as SI
+
+    g = load_golden("nce_c34.npz")
+    n, d, kq, seed = SI.NCE_C34_CASES[case]
+    q, k, queue = SI.nce_c2_inputs(n, d, kq, seed)
+    for with_q in (False, True):
+        tag = f"n{n}_d{d}_k{kq}_{'q' if with_q else 'noq'}"
+        loss, dq = O.nce_info_loss(q, k, queue if with_q else None, 0.05)
+        assert abs(loss - g[f"{tag}_loss"]) <= 1e-5 * abs(g[f"{tag}_loss"])
+        np.testing.assert_allclose(dq[:16], g[f"{tag}_dq_head"], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(dq[-16:], g[f"{tag}_dq_tail"], rtol=1e-4, atol=1e-6)
+        np.testing.assert_allclose(np.linalg.norm(dq, axis=1), g[f"{tag}_dq_rownorm"], rtol=1e-5)
+        np.testing.assert_allclose(dq.sum(axis=0), g[f"{tag}_dq_colsum"], rtol=1e-4, atol=1e-5)
+    for b in (n, 256):
+        q2, ptr = O.dequeue_and_enqueue(queue, 0, k[:b])
+        assert ptr == int(g[f"enq_b{b}_k{kq}_ptr"])
+        assert int((q2 != queue).any(axis=0).sum()) == int(g[f"enq_b{b}_k{kq}_changed_cols"])
+    assert int(g[f"enq_b{n}_k{kq}_ptr"]) == 0 and int(g[f"enq_b{n}_k{kq}_changed_cols"]) == 0
 
 
 def test_torch_cpu_baseline_restatement_matches_reference():

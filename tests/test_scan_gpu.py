@@ -238,3 +238,70 @@ def test_graphed_search_many_equals_serial_search(gpu):
         for q, (s, i) in zip(batches, many):
             s0, i0 = index.search(q, 40)
             assert torch.equal(s, s0) and torch.equal(i, i0), dtype
+
+
+def test_graphed_search_many_survives_workspace_growth(gpu):
+    """a captured graph must keep its own scan workspace.  The
+    sequence Q=64 -> Q=256 (bigger workspace) -> Q=64 on one index, then a second
+    index with a larger shard and a bigger k, then the first index's Q=64 graphs
+    again, and finally the shard tensor replaced in place of the attribute: every
+    replay equals a serial search() on the current shard."""
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(13)
+    small = retrieval.ShardedDenseIndex(_dev(_grid(rng, (9000, 256), 3), gpu), doc_offset=1)
+    big = retrieval.ShardedDenseIndex(_dev(_grid(rng, (60000, 256), 3), gpu), doc_offset=2)
+
+    def check(index, q, k):
+        many = index.search_many([q, q, q], k, depth=2, graphs=True)
+        s0, i0 = index.search(q, k)
+        for s, i in many:
+            assert torch.equal(s, s0) and torch.equal(i, i0)
+
+    q64 = _dev(_grid(rng, (64, 256), 3), gpu)
+    q256 = _dev(_grid(rng, (256, 256), 3), gpu)
+    check(small, q64, 30)
+    check(small, q256, 30)
+    check(small, q64, 30)
+    check(big, q256, 120)
+    check(big, q64, 120)
+    check(small, q64, 30)  # the first graphs replay after every growth above
+    small.docs = _dev(_grid(rng, (9000, 256), 3), gpu).to(torch.bfloat16)
+    check(small, q64, 30)  # new shard tensor: captured anew, not the old pointer
+
+
+@pytest.mark.parametrize("Q,D,fp8", [(1, 256, False), (16, 768, False), (64, 256, False),
+                                      (32, 256, True)])
+def test_rescan_bit_exact_vs_oracle_on_grid(gpu, Q, D, fp8):
+    """the single-pass scan's rescan path pinned to
+    the oracle.  Integer-grid corpus (every score exact in fp32 in any order) with
+    a block of 600 consecutive docs aligned with the queries: all k = 100 winners
+    sit in a few workers, whose 4-key lists provably overflow, so select_dense
+    must rescan.  The rescan counter proves it happened; indices and scores are
+    compared bit for bit with the oracle (ties: lower index first)."""
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(100 + Q)
+    N, k, lo = 40_000, 100, 17_000
+    lim, step = (7, 16) if fp8 else (40, 128)  # fp8: e4m3-exact values m/16, |m| <= 15
+    base = rng.integers(-lim, lim + 1, D)
+    docs = rng.integers(-2, 3, (N, D))
+    docs[lo:lo + 600] = base + rng.integers(-3, 4, (600, D))
+    qs = base + rng.integers(-3, 4, (Q, D))
+    d = (docs / step).astype(np.float32)
+    q = (qs / step).astype(np.float32)
+    retrieval.rescan_stats(reset=True)
+    if fp8:
+        q8, d8 = O.quantize_e4m3(q), O.quantize_e4m3(d)
+        assert np.array_equal(O.dequantize_e4m3(d8), d)  # the grid is e4m3-exact
+        s, i = retrieval.scan_topk_fp8(_dev(q8, gpu), _dev(d8, gpu), k, 3, 1.0 / 256)
+        ri, rs = O.scan_topk_fp8(q8, d8, k, doc_offset=3, score_scale=1.0 / 256)
+    else:
+        s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), k, 3)
+        ri, rs = O.scan_topk(q, d, k, doc_offset=3)
+    nq, nw = retrieval.rescan_stats(reset=True)
+    print(f"Q={Q} D={D} fp8={fp8}: {nq} queries rescanned, {nw} workers")
+    assert nq >= 1 and nw >= nq  # the block's truncated lists forced rescans
+    np.testing.assert_array_equal(i.cpu().numpy(), ri)
+    np.testing.assert_array_equal(s.cpu().numpy(), rs)
+    assert ((ri >= lo + 3) & (ri < lo + 603)).all()

@@ -121,6 +121,28 @@ def test_tables_reproduce_tokenizer_cpu(hf_tok):
         assert [2] + g + [3] == r, repr(t)
 
 
+def test_table_cache_rejects_tampered_file(hf_tok, tmp_path, monkeypatch):
+    """the cached normaliser / pre-tokeniser tables live in a per-user
+    cache directory and are spot-checked on load: a tampered or truncated file is
+    rebuilt, never used."""
+    from irc_amd import wordpiece as W
+
+    monkeypatch.setenv("XDG_CACHE_HOME", str(tmp_path))
+    backend = hf_tok.backend_tokenizer
+    cmap, cpool, cls = W._char_tables(backend)  # builds into tmp_path/irc_amd
+    files = list((tmp_path / "irc_amd").glob("wordpiece_chars_*.npz"))
+    assert len(files) == 1
+    bad = cmap.copy()
+    bad[ord("a")] = (ord("b") << 8) | 1  # 'a' would normalise to 'b'
+    np.savez(files[0], cmap=bad, cpool=cpool, cls=cls)
+    assert not W._tables_valid(backend.normalizer, backend.pre_tokenizer, bad, cpool, cls)
+    c2, p2, k2 = W._char_tables(backend)
+    assert np.array_equal(c2, cmap) and np.array_equal(p2, cpool) and np.array_equal(k2, cls)
+    files[0].write_bytes(b"truncated")
+    c3, _, _ = W._char_tables(backend)
+    assert np.array_equal(c3, cmap)
+
+
 @pytest.mark.gpu
 def test_gpu_wordpiece_matches_tokenizer(gpu, hf_tok):
     from irc_amd.wordpiece import GpuWordPiece
