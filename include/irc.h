@@ -328,6 +328,35 @@ int irc_gemm_fp8(const void* A8, int64_t lda, const float* sa, const void* B8, i
                  const float* sb, int64_t M, int64_t N, int64_t K, const float* bias,
                  const void* R, int64_t ldr, void* C, int64_t ldc, int epi, irc_stream_t stream);
 
+/* MX-fp8: the CDNA4-native form of the same layers.  An MX-fp8 matrix [rows][K]
+ * is e4m3 codes [rows][ld] plus one E8M0 scale (2^(byte - 127)) per 32 consecutive
+ * values of a row, the smallest power of two for which the block's max / scale
+ * <= 448 (no saturation; 2^0 for an all-zero block).  The scales live in the "MX
+ * layout": K/128 records of mpad * 4 bytes (mpad = rows rounded up to 256), each
+ * 256-row block's 1 KB ordered [row bit 7][k-block][row bits 0-3][row bits 4-6]
+ * (csrc/mx.h mx_scale_index), which the GEMM DMAs into LDS with its K-tiles.
+ * irc_quantize_mx_fp8: x bf16 (0) / fp32 (1) [M][ldx] -> out [M][ldo], scales.
+ * irc_gemm_mx: C = A . B^T with both operands' block scales applied inside
+ *   v_mfma_scale_f32_16x16x128_f8f6f4 (+ bias / GELU / residual as irc_gemm_fp8);
+ *   C bf16 [M][ldc], or, when cx != NULL, MX-fp8 (C = e4m3 bytes, ldc in bytes, cx
+ *   its scales with mpad rows: the FFN1 + GELU output feeding FFN2).  K % 128, N % 32.
+ * irc_layernorm_mx: irc_layernorm (bf16, H 512 / 768 / 1024) that also writes the
+ *   MX-fp8 copy y8 / ys of its bf16 output (the next projection's A operand).
+ * irc_attention_mx: irc_attention's MFMA path (head dim 64, L % 32 == 0, L <= 128)
+ *   with the context written as MX-fp8 only (ctx8 / cs) for the out-projection.
+ * Producers quantise their bf16-rounded outputs, so each MX operand equals
+ * irc_quantize_mx_fp8 of the bf16 tensor the bf16 path would have produced. */
+int irc_quantize_mx_fp8(int in_dtype, const void* x, int64_t ldx, int64_t M, int64_t K, void* out,
+                        int64_t ldo, void* scales, int64_t mpad, irc_stream_t stream);
+int irc_gemm_mx(const void* A8, int64_t lda, const void* sa, int64_t mpad, const void* B8,
+                int64_t ldb, const void* sb, int64_t npad, int64_t M, int64_t N, int64_t K,
+                const float* bias, const void* R, int64_t ldr, void* C, int64_t ldc, void* cx,
+                int epi, irc_stream_t stream);
+int irc_layernorm_mx(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
+                     int64_t H, float eps, void* y8, void* ys, int64_t mpad, irc_stream_t stream);
+int irc_attention_mx(const void* qkv, const int64_t* mask, void* ctx8, void* cs, int64_t mpad,
+                     int64_t B, int64_t L, int64_t H, int64_t heads, irc_stream_t stream);
+
 /* ------------------------------------------------- input pipeline (csrc/wordpiece.hip)
  * BERT WordPiece tokenisation + joint padding on the device: replaces the
  * reference's per-micro-batch host call bert_tokenizer(d1 + d2, padding=True,

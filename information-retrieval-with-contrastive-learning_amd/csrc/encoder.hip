@@ -7,6 +7,7 @@
 //    online softmax; PAD query rows are computed and kept, as HF does.
 // Element type T is bf16 (uint16 bits) or fp32; statistics are always fp32.
 #include "irc_common.h"
+#include "mx.h"
 
 namespace irc {
 namespace enc {
@@ -108,12 +109,19 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
 // (32 lanes) per row, 16-byte loads/stores (H/256 chunks of 8 per lane), the
 // two half-waves of a wave on consecutive rows; statistics fp32 in the same
 // order-independent two-pass form as layernorm_kernel.
-template <int CPL>
+// MXO: the row is ALSO written as MX-fp8 (e4m3 y8 [rows][H] + E8M0 block scales
+// ys in the MX layout, mpad rows): the next fp8 linear layer's A operand, with no
+// separate quantisation pass (config C5).  One 32-value block = 4 consecutive
+// lanes' chunks of 8.
+template <int CPL, bool MXO = false>
 __global__ __launch_bounds__(256) void layernorm_vec_kernel(const unsigned short* __restrict__ x,
                                                            unsigned short* __restrict__ y,
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta,
-                                                           int64_t rows, float eps) {
+                                                           int64_t rows, float eps,
+                                                           unsigned char* __restrict__ y8 = nullptr,
+                                                           unsigned char* __restrict__ ys = nullptr,
+                                                           int64_t mpad = 0) {
   constexpr int H = CPL * 256;
   const int lane = threadIdx.x & 63, hl = lane & 31;
   const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
@@ -155,9 +163,23 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const unsigned short
     const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
     const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
     u16x8 o;
+    float r[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) o[t] = f32_to_bf16((v[i][t] - mean) * rstd * gg[t] + bb[t]);
+    for (int t = 0; t < 8; ++t) {
+      r[t] = (v[i][t] - mean) * rstd * gg[t] + bb[t];
+      o[t] = f32_to_bf16(r[t]);
+    }
     *reinterpret_cast<u16x8*>(y + row * H + c0) = o;
+    if constexpr (MXO) {
+      // quantise the bf16-rounded values: the fp8 operand is the bf16 activation's
+      // quantisation, exactly as the standalone quantiser would produce it
+#pragma unroll
+      for (int t = 0; t < 8; ++t) r[t] = bf16_to_f32(o[t]);
+      uint2 q8;
+      const unsigned e8 = gpp::mx_quant8(r, q8);
+      *reinterpret_cast<uint2*>(y8 + row * H + c0) = q8;
+      if ((hl & 3) == 0) ys[gpp::mx_scale_index(row, c0, mpad)] = (unsigned char)e8;
+    }
   }
 }
 
@@ -239,11 +261,18 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
 //  * O = P . V: P goes straight from registers into the A operand; summing over
 //    keys in the lane's permuted key order is matched by reading the V operand
 //    from a per-wave transposed V^T copy in LDS (two ds_read_b64 per fragment).
-template <int NJ>
+//  * MXO (config C5): ctx leaves as MX-fp8 instead of bf16 -- e4m3 bytes ctx8
+//    [B*L][H] and one E8M0 scale per (token, 32 head columns) in the MX layout
+//    (cs, mpad rows) -- the out-projection's A operand, no quantisation pass; each
+//    block is one half-wave's 32 lanes (the block max by 5 lane exchanges).
+template <int NJ, bool MXO = false>
 __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned short* __restrict__ qkv,
                                                             const int64_t* __restrict__ mask,
                                                             unsigned short* __restrict__ ctx,
-                                                            int B, int H, int heads, float scale) {
+                                                            int B, int H, int heads, float scale,
+                                                            unsigned char* __restrict__ ctx8 = nullptr,
+                                                            unsigned char* __restrict__ cs = nullptr,
+                                                            int64_t mpad = 0) {
   constexpr int L = 32 * NJ, DH = 64;
   constexpr int VP = L + 4;  // V^T row pitch (u16): 8-byte aligned, conflict-free b64 reads
   __shared__ __attribute__((aligned(16))) unsigned short vt[4][DH][VP];
@@ -335,6 +364,26 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
       }
     }
   // O C layout: col = d (lane), row = query 32ib + (e&3) + 8(e>>2) + 4h
+  if constexpr (MXO) {
+    const int64_t row0 = (int64_t)b * L + 32 * ib;
+    unsigned char* out8 = ctx8 + row0 * H + a * DH;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int i = (e & 3) + 8 * (e >> 2) + 4 * h;
+        // bf16-rounded like the bf16 path's ctx, then quantised per 32 columns
+        const float v = bf16_to_f32(f32_to_bf16(o[db][e]));
+        float am = fabsf(v);
+#pragma unroll
+        for (int m = 1; m < 32; m <<= 1) am = fmaxf(am, __shfl_xor(am, m, 64));
+        const int p = gpp::mx_exponent(am);
+        const uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(v * ldexpf(1.f, -p), 0.f, 0u, false);
+        out8[(int64_t)i * H + 32 * db + r32] = (unsigned char)(w & 0xffu);
+        if (r32 == 0) cs[gpp::mx_scale_index(row0 + i, a * DH + 32 * db, mpad)] = (unsigned char)(p + 127);
+      }
+    return;
+  }
   unsigned short* out = ctx + ((int64_t)b * L + 32 * ib) * H + a * DH;
 #pragma unroll
   for (int db = 0; db < 2; ++db)
@@ -383,6 +432,69 @@ extern "C" int irc_layernorm(int dtype, const void* x, void* y, const float* gam
     hipLaunchKernelGGL((enc::layernorm_kernel<float>), grid, dim3(256), 0, as_stream(stream),
                        (const float*)x, (float*)y, gamma, beta, rows, (int)H, eps);
   return check_launch("layernorm_kernel");
+}
+
+// LayerNorm (bf16, H in {512, 768, 1024}) that also emits the MX-fp8 copy of its
+// output (config C5): y bf16 as irc_layernorm, y8 e4m3 [rows][H] and ys E8M0 block
+// scales in the MX layout with mpad (>= rows rounded up to 256) rows.
+extern "C" int irc_layernorm_mx(const void* x, void* y, const float* gamma, const float* beta,
+                                int64_t rows, int64_t H, float eps, void* y8, void* ys,
+                                int64_t mpad, irc_stream_t stream) {
+  IRC_REQUIRE(H == 512 || H == 768 || H == 1024, "layernorm_mx: H=%lld unsupported", (long long)H);
+  IRC_REQUIRE(mpad >= (rows + 255) / 256 * 256, "layernorm_mx: mpad must cover rows rounded to 256");
+  IRC_REQUIRE((((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta |
+                (uintptr_t)y8) % 16) == 0, "layernorm_mx: 16-byte aligned operands required");
+  if (rows == 0) return IRC_OK;
+  const dim3 g8((unsigned)((rows + 7) / 8));
+  hipStream_t st = as_stream(stream);
+  prof_begin(st);
+  auto* yy8 = static_cast<unsigned char*>(y8);
+  auto* yys = static_cast<unsigned char*>(ys);
+  if (H == 768)
+    hipLaunchKernelGGL((enc::layernorm_vec_kernel<3, true>), g8, dim3(256), 0, st,
+                       (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
+                       yys, mpad);
+  else if (H == 1024)
+    hipLaunchKernelGGL((enc::layernorm_vec_kernel<4, true>), g8, dim3(256), 0, st,
+                       (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
+                       yys, mpad);
+  else
+    hipLaunchKernelGGL((enc::layernorm_vec_kernel<2, true>), g8, dim3(256), 0, st,
+                       (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
+                       yys, mpad);
+  prof_end("layernorm", st, (double)rows * H * 5.0);
+  return check_launch("layernorm_mx");
+}
+
+// MFMA attention (bf16 QKV, head dim 64, L % 32 == 0, L <= 128) whose context
+// leaves as MX-fp8 (ctx8 e4m3 [B*L][H], cs E8M0 scales in the MX layout, mpad rows):
+// the fp8 out-projection's A operand (config C5).
+extern "C" int irc_attention_mx(const void* qkv, const int64_t* mask, void* ctx8, void* cs,
+                                int64_t mpad, int64_t B, int64_t L, int64_t H, int64_t heads,
+                                irc_stream_t stream) {
+  IRC_REQUIRE(heads >= 1 && H % heads == 0 && H / heads == 64 && L % 32 == 0 && L >= 32 &&
+                  L <= 128, "attention_mx: head dim 64 and L in {32, 64, 96, 128} required");
+  IRC_REQUIRE(mpad >= (B * L + 255) / 256 * 256, "attention_mx: mpad must cover B*L rounded to 256");
+  if (B == 0) return IRC_OK;
+  hipStream_t st = as_stream(stream);
+  const int64_t waves = B * heads * (L / 32);
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  const float sc = 0.125f;
+  auto* c8 = static_cast<unsigned char*>(ctx8);
+  auto* css = static_cast<unsigned char*>(cs);
+  prof_begin(st);
+  switch (L / 32) {
+#define IRC_ATTX(NJ)                                                                             \
+  case NJ:                                                                                       \
+    hipLaunchKernelGGL((enc::attention_mfma_kernel<NJ, true>), grid, dim3(256), 0, st,          \
+                       (const unsigned short*)qkv, mask, (unsigned short*)nullptr, (int)B, (int)H, \
+                       (int)heads, sc, c8, css, mpad);                                           \
+    break;
+    IRC_ATTX(1) IRC_ATTX(2) IRC_ATTX(3) IRC_ATTX(4)
+#undef IRC_ATTX
+  }
+  prof_end("attention", st, (double)B * L * (3 * H * 2.0 + H));
+  return check_launch("attention_mx");
 }
 
 extern "C" int irc_embed_ln(int dtype, const int64_t* ids, const void* word, const void* pos,

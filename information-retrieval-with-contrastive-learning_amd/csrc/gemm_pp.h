@@ -34,6 +34,14 @@ struct PArgs {
   const float* sb;
   // grouped tile order (grouped_tile in irc_common.h); 0 / 1 = row-major
   int group_m;
+  // MX-fp8 linear layers (run_mx): E8M0 block scales of A / B in the MX layout
+  // [K8/128][rows padded to 256][4] (mpad / npad = the padded row counts), and,
+  // when cx != null, an MX-fp8 OUTPUT: C holds e4m3 bytes (ldc in bytes) and cx
+  // its block scales ([N/128][mpad][4]); else C is bf16.
+  const unsigned char* sax;
+  const unsigned char* sbx;
+  int mpad, npad;
+  unsigned char* cx;
 };
 
 constexpr int EPI_SCAN = 7;
@@ -51,6 +59,9 @@ void run_scores_fp8(const PArgs& a, hipStream_t st);
 // e4m3 linear layer: bf16 C = (A8 . B8^T) * sa[m] * sb[n] (+ bias / GELU / residual);
 // both operands K-major, K / lda / ldb in 2-byte units, vec_c layout required
 void run_fp8(int epi, const PArgs& a, hipStream_t st);
+// MX-fp8 linear layer: C = (A8 . B8^T with per-32-k E8M0 block scales) (+ bias /
+// GELU / residual); bf16 C, or MX-fp8 C when a.cx != null (epilogues 1, 2 only)
+void run_mx(int epi, const PArgs& a, hipStream_t st);
 
 }  // namespace gpp
 }  // namespace irc

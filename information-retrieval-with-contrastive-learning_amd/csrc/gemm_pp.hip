@@ -31,6 +31,7 @@
 //    fused bias / GELU / GELU' / residual / pre-activation save / fp32 accumulate,
 //    or raw fp32 split-K slabs reduced afterwards in a fixed order.
 #include "gemm_pp.h"
+#include "mx.h"
 
 #include <atomic>
 #include <cstdlib>
@@ -211,13 +212,63 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int row0, int s, int lan
 // fragments take the same bytes of the row, so the k order is consistent.
 typedef int v8i32 __attribute__((ext_vector_type(8)));
 
+// MX MFMA with the A / B scale bytes chosen by op_sel (immediates: the callers'
+// unrolled loop indices fold the switch to one instruction).
+template <int OA, int OB>
+__device__ __forceinline__ f32x4 mfma_mx(v8i32 a, v8i32 b, f32x4 c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, OA, sa, OB, sb);
+}
+__device__ __forceinline__ f32x4 mfma_mx_sel(int oa, int ob, v8i32 a, v8i32 b, f32x4 c, int sa,
+                                             int sb) {
+  switch (oa * 4 + ob) {
+#define IRC_MXS(OA, OB) \
+  case OA * 4 + OB:     \
+    return mfma_mx<OA, OB>(a, b, c, sa, sb);
+    IRC_MXS(0, 0) IRC_MXS(0, 1) IRC_MXS(0, 2) IRC_MXS(0, 3)
+    IRC_MXS(1, 0) IRC_MXS(1, 1) IRC_MXS(1, 2) IRC_MXS(1, 3)
+    IRC_MXS(2, 0) IRC_MXS(2, 1) IRC_MXS(2, 2) IRC_MXS(2, 3)
+    IRC_MXS(3, 0) IRC_MXS(3, 1) IRC_MXS(3, 2)
+#undef IRC_MXS
+    default:
+      return mfma_mx<3, 3>(a, b, c, sa, sb);
+  }
+}
+
+// MX-fp8 (F8 == 2, the encoder's fp8 linear layers): e4m3 operands with one
+// power-of-two (E8M0) scale per 32 consecutive k of a row, applied by the MFMA
+// itself (v_mfma_scale_f32_16x16x128_f8f6f4's per-lane block scales).  Scale
+// layout in HBM ("MX layout"): [K8 / 128][rows padded to 256][4] bytes, so one
+// 256-row K-tile's scales are 1 KB contiguous; they ride the tile's DMA into LDS
+// at MX_SC_OFF + buffer * 2 KB as [A half 0 | B half 0 | A half 1 | B half 1].
+constexpr int MX_SC_OFF = 2 * buf_bytes(true, true);  // 128 KB: past both K-major buffers
+static_assert(MX_SC_OFF + 2 * 2048 <= LDS_BYTES, "MX scale slots");
+
+// The scales of K-tile `kt` (64 two-byte units = 128 e4m3) for group g's A and B
+// halves (512 contiguous bytes each, mx_scale_index): wave 0 of the group, lanes
+// 0-31 the A half, 32-63 the B half.
+__device__ __forceinline__ void stage_scales(const PArgs& g, int m0, int n0, int kt, char* sc,
+                                             int grp, int wq, int lane) {
+  if (wq != 0) return;
+  // re-derived per call: hoisted out of the K loop, the per-lane pointer would hold
+  // two more VGPRs through it (the MX loop sits at the 256-register limit)
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+  const bool isb = ln >= 32;
+  const unsigned char* src = isb ? g.sbx + (int64_t)kt * g.npad * 4 + (n0 >> 8) * 1024
+                                 : g.sax + (int64_t)kt * g.mpad * 4 + (m0 >> 8) * 1024;
+  glds16(src + grp * 512 + 16 * (ln & 31), sc + grp * 1024);
+}
+
 // One 64-deep K-tile of both operands into the LDS image at `base`: group g stages
 // A rows/cols [128g, +128) and B rows/cols [128g, +128).
-template <bool AK, bool BK_>
+template <bool AK, bool BK_, bool REDERIVE = false>
 __device__ __forceinline__ void stage_tile(const PArgs& g, const unsigned short* A,
                                            const unsigned short* B, int m0, int n0, int k0,
                                            char* base, int grp, int wq, int lane) {
   constexpr int SA = slot_bytes(AK), SB = slot_bytes(BK_);
+  if constexpr (REDERIVE) {  // per-lane DMA addresses recomputed per call, not kept live
+    asm volatile("" : "+v"(lane));
+  }
   stage_half<AK>(A, g.lda, m0 + 128 * grp, g.M, k0, base + grp * SA, wq, lane);
   stage_half<BK_>(B, g.ldb, n0 + 128 * grp, g.N, k0, base + 2 * SA + grp * SB, wq, lane);
 }
@@ -229,7 +280,7 @@ __device__ __forceinline__ void stage_tile(const PArgs& g, const unsigned short*
 // loop.  On return every wave of the CALLER's group is past its last MFMA and every
 // wave of both groups past its last fragment read; group 1 may still be in its last
 // MFMAs when group 0 returns (registers only: LDS is free for the epilogue).
-template <bool AK, bool BK_, bool F8>
+template <bool AK, bool BK_, int F8>
 __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A,
                                          const unsigned short* B, int m0, int n0, int kbeg,
                                          int nk, char* lds, int pitch, int par, bool staged,
@@ -245,31 +296,79 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
 
   if (nk > 0) {
     if (!staged) stage_tile<AK, BK_>(g, A, B, m0, n0, kbeg, lds + par * pitch, grp, wq, lane);
+    if constexpr (F8 == 2) stage_scales(g, m0, n0, kbeg / BK, lds + MX_SC_OFF + par * 2048, grp, wq, lane);
     wait_vmcnt<0>();
     wg_barrier();
     if (grp == 1) wg_barrier();  // group 1 runs one section behind
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = (kt + par) & 1;
       // ---- L section: next tile's DMA, this tile's fragments
-      if (kt + 1 < nk)
-        stage_tile<AK, BK_>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch, grp,
-                            wq, lane);
+      if (kt + 1 < nk) {
+        stage_tile<AK, BK_, F8 == 2>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch,
+                                     grp, wq, lane);
+        if constexpr (F8 == 2)
+          stage_scales(g, m0, n0, kbeg / BK + kt + 1, lds + MX_SC_OFF + (cur ^ 1) * 2048, grp, wq,
+                       lane);
+      }
       const char* la = lds + cur * pitch + grp * SA;
       const char* lb = lds + cur * pitch + 2 * SA + bh * SB;
       bf16x8 fa[8][2], fb[4][2];
+      uint2 xa;     // MX: the lane's E8M0 block scales of its A rows 16 i + r (byte i)
+      uint32_t xb;  // ... and of its B cols (byte j)
+      if constexpr (F8 == 2) {
+        // lane l feeds k-block q = l >> 4 of row/col l & 15: 32 contiguous e4m3 =
+        // 16-byte chunks 2q, 2q + 1 of the 128-byte K-tile row (K-major images)
+        const int q = lane >> 4;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+        for (int c = 0; c < 2; ++c) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j][s] = frag<BK_>(lb, bcol + 16 * j, s, lane);
+          for (int j = 0; j < 4; ++j) {
+            const int row = bcol + 16 * j + (lane & 15);
+            fb[j][c] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + 16 * ((2 * q + c) ^ (row & 7)));
+          }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) fa[i][s] = frag<AK>(la, 16 * i, s, lane);
+          for (int i = 0; i < 8; ++i) {
+            const int row = 16 * i + (lane & 15);
+            fa[i][c] = *reinterpret_cast<const bf16x8*>(la + row * 128 + 16 * ((2 * q + c) ^ (row & 7)));
+          }
+        }
+        const char* sc = lds + MX_SC_OFF + cur * 2048;
+        const int rq = (q * 16 + (lane & 15)) * 8;
+        xa = *reinterpret_cast<const uint2*>(sc + grp * 1024 + rq);
+        xb = *reinterpret_cast<const uint32_t*>(sc + bh * 1024 + 512 + rq + 4 * (wn & 1));
+      } else {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fb[j][s] = frag<BK_>(lb, bcol + 16 * j, s, lane);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) fa[i][s] = frag<AK>(la, 16 * i, s, lane);
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (grp == 1) wait_vmcnt<0>();  // group 0 reads this DMA in the next section
       wg_barrier();
       // ---- M section
       __builtin_amdgcn_s_setprio(1);
-      if constexpr (F8) {
+      if constexpr (F8 == 2) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bf16x8 a2[2] = {fa[i][0], fa[i][1]};
+            const bf16x8 b2[2] = {fb[j][0], fb[j][1]};
+#ifdef IRC_MX_NO_OPSEL  // A/B build: bytes extracted by shifts instead of op_sel
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                __builtin_bit_cast(v8i32, a2), __builtin_bit_cast(v8i32, b2), acc[i][j], 0, 0, 0,
+                (int)(((i < 4 ? xa.x : xa.y) >> (8 * (i & 3))) & 0xffu), 0,
+                (int)((xb >> (8 * j)) & 0xffu));
+#else  // op_sel picks byte (i & 3) / j of the packed scale registers
+            acc[i][j] = mfma_mx_sel(i & 3, j, __builtin_bit_cast(v8i32, a2),
+                                    __builtin_bit_cast(v8i32, b2), acc[i][j],
+                                    (int)(i < 4 ? xa.x : xa.y), (int)xb);
+#endif
+          }
+      } else if constexpr (F8) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -317,7 +416,7 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
 // split-K slabs): per wave, four 32-row passes through its LDS staging rows (the
 // first 8 * 32 * EP_PITCH floats of LDS), fused bias / GELU / GELU' / residual /
 // pre-activation save / fp32 accumulate, then coalesced 16-byte stores.
-template <typename TO, int EPI, bool F8>
+template <typename TO, int EPI, int F8>
 __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[8][4], char* lds,
                                              int m0, int n0, int batch, int grp, int wn, int wave,
                                              int lane) {
@@ -337,7 +436,7 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
     // fp8 linear layers: per-row (A) and per-column (B) dequantisation scales
     float sbv[4] = {1.f, 1.f, 1.f, 1.f};
     float sav[8][4];
-    if constexpr (F8) {
+    if constexpr (F8 == 1) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int col = cbase + 16 * j + (lane & 15);
@@ -360,7 +459,7 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
           f32x2 v[2];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            if constexpr (F8)
+            if constexpr (F8 == 1)
               v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * (alpha * sav[2 * p + ii][e] * sbv[j]) +
                                  bv[j];
             else
@@ -432,6 +531,19 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
             }
             *reinterpret_cast<u16x8*>(const_cast<unsigned short*>(R) + (int64_t)row * g.ldr + col) =
                 pre;
+          }
+          if (F8 == 2 && g.cx != nullptr) {
+            // MX-fp8 output (the next GEMM's A operand): 4 lanes = one 32-col block;
+            // rows / cols past the tile edge are never stored (N, M multiples of 32
+            // and 8 for this path, checked by the host)
+            uint2 q8;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) v[t] = bf16_to_f32(f32_to_bf16(v[t]));  // as the bf16 output
+            const unsigned e8 = mx_quant8(v, q8);
+            unsigned char* C8 = reinterpret_cast<unsigned char*>(g.C);
+            *reinterpret_cast<uint2*>(C8 + (int64_t)row * g.ldc + col) = q8;
+            if ((lane & 3) == 0) g.cx[mx_scale_index(row, col, g.mpad)] = (unsigned char)e8;
+            continue;
           }
           u16x8 o;
 #pragma unroll
@@ -572,7 +684,7 @@ __device__ __forceinline__ void epilogue_scan(const PArgs& g, const f32x4 (&acc)
     g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = cnt[threadIdx.x];
 }
 
-template <bool AK, bool BK_, typename TO, int EPI, bool F8 = false>
+template <bool AK, bool BK_, typename TO, int EPI, int F8 = 0>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
   const int tiles_m = (g.M + BM - 1) / BM;
@@ -682,7 +794,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
 constexpr int PBUF = 8 * 32 * EP_PITCH * 4;  // 69,632 B
 static_assert(PBUF >= buf_bytes(false, false) && 2 * PBUF <= LDS_BYTES, "persistent LDS plan");
 
-template <bool AK, bool BK_, typename TO, int EPI, bool F8 = false>
+template <bool AK, bool BK_, typename TO, int EPI, int F8 = 0>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_pers_kernel(PArgs g, uint32_t* ctr, int mode) {
   // mode 1: dynamic tiles + prestage; 2: static waves of G tiles + prestage;
   // 3: static, no prestage (A/B of what each part buys)
@@ -873,6 +985,20 @@ void run_scores_fp8(const PArgs& a, hipStream_t st) {
   const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
   hipLaunchKernelGGL((gemm_pp_kernel<true, true, float, EPI_NONE, true>), dim3((unsigned)tiles),
                      dim3(NT), 0, st, a);
+}
+
+void run_mx(int epi, const PArgs& a, hipStream_t st) {
+  const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
+  const dim3 grid((unsigned)tiles);
+  switch (epi) {
+#define IRC_PPX(E)                                                                        \
+  case E:                                                                                 \
+    hipLaunchKernelGGL((gemm_pp_kernel<true, true, unsigned short, E, 2>), grid, dim3(NT), 0, \
+                       st, a);                                                            \
+    break;
+    IRC_PPX(0) IRC_PPX(1) IRC_PPX(2) IRC_PPX(3)
+#undef IRC_PPX
+  }
 }
 
 void run_fp8(int epi, const PArgs& a, hipStream_t st) {

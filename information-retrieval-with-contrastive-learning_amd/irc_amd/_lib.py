@@ -94,6 +94,11 @@ SIGNATURES = {
     "irc_colsum_batched": (I32, [I32, P, I64, I64, I64, I64, I64, P, I64, I32, P, I64, P]),
     "irc_quantize_rows_fp8": (I32, [I32, P, I64, I64, I64, P, I64, P, P]),
     "irc_gemm_fp8": (I32, [P, I64, P, P, I64, P, I64, I64, I64, P, P, I64, P, I64, I32, P]),
+    "irc_quantize_mx_fp8": (I32, [I32, P, I64, I64, I64, P, I64, P, I64, P]),
+    "irc_gemm_mx": (I32, [P, I64, P, I64, P, I64, P, I64, I64, I64, I64, P, P, I64, P, I64, P,
+                          I32, P]),
+    "irc_layernorm_mx": (I32, [P, P, P, P, I64, I64, F32, P, P, I64, P]),
+    "irc_attention_mx": (I32, [P, P, P, P, I64, I64, I64, I64, I64, P]),
     "irc_wordpiece": (I32, [P, P, I64, P, P, P, P, P, I64, P, P, P, I64, I64, I64, P, P, P, P]),
     "irc_wordpiece_pad": (I32, [P, P, I64, I64, I64, I64, I64, I64, P, P, P]),
     "irc_prof_enable": (I32, [I32]),

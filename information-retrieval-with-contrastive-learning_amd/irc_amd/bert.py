@@ -145,8 +145,8 @@ class BertModel(nn.Module):
         self.pooler = _Pooler(config.hidden_size)  # kept for checkpoint compatibility
         self._init_weights(seed)
         self._cache = {}
-        # "bf16" (default) or "fp8": e4m3 weights (per output channel scales) and
-        # per-token e4m3 inputs for every nn.Linear of the frozen encoder (config C5)
+        # "bf16" (default) or "fp8": MX-fp8 weights and inputs (e4m3 with one E8M0 scale
+        # per 32 consecutive values) for every nn.Linear of the frozen encoder (config C5)
         self.weight_format = os.environ.get("IRC_ENCODER_WEIGHTS", "bf16")
         self.eval()
 
@@ -212,8 +212,8 @@ class BertModel(nn.Module):
         cast = (lambda t: t.detach().to(dt).contiguous())
         f32 = (lambda t: t.detach().float().contiguous())
         castw = cast
-        if fp8:  # linear weights: (e4m3 bytes, per-output-channel scales) of the fp32 weight
-            castw = (lambda t: ops.quantize_rows_fp8(t.detach().float().contiguous()))  # noqa: E731
+        if fp8:  # linear weights as MX-fp8: e4m3 + one E8M0 scale per 32 k of a channel
+            castw = (lambda t: ops.quantize_mx(t.detach().float().contiguous()))  # noqa: E731
         e = self.embeddings
         w = {"word": cast(e.word_embeddings.weight), "pos": cast(e.position_embeddings.weight),
              "type0": cast(e.token_type_embeddings.weight[0]), "ln_g": f32(e.LayerNorm.weight),
@@ -259,26 +259,31 @@ class BertModel(nn.Module):
         return x.view(B, L, H)
 
     def _encode_fp8(self, ids, mask, w):
-        """encode() with every nn.Linear on e4m3 (irc_gemm_fp8): the input rows are
-        quantised per token, the weights per output channel; embeddings, attention,
-        LayerNorm and the epilogues stay bf16 / fp32."""
+        """encode() with every nn.Linear on MX-fp8 (irc_gemm_mx, config C5): e4m3
+        operands with one power-of-two scale per 32 k of a row, applied inside the
+        MFMA.  Each GEMM input arrives already quantised from its producer -- the
+        LayerNorms write a bf16 (residual) and an MX copy, attention writes its
+        context as MX only, FFN1's GELU epilogue writes MX for FFN2 -- so there is
+        no separate quantisation pass per layer (only the embeddings' output is
+        quantised once).  Attention, LayerNorm and the epilogues stay bf16 / fp32."""
         c = self.config
         B, L = ids.shape
         H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
         x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
-
-        def lin(inp, wq, bias, epi, residual=None):
-            aq, sa = ops.quantize_rows_fp8(inp)
-            return ops.gemm_fp8(aq, sa, wq[0], wq[1], bias=bias, epilogue=epi, residual=residual)
-
-        for lw in w["layers"]:
-            qkv = lin(x, lw["wqkv"], lw["bqkv"], ops.EPI_BIAS)
-            ctx = ops.attention(qkv, mask, B, L, H, heads)
-            a = lin(ctx, lw["wo"], lw["bo"], ops.EPI_BIAS_RESID, residual=x)
-            a = ops.layernorm(a, lw["ln1_g"], lw["ln1_b"], eps, out=a)
-            i = lin(a, lw["w1"], lw["b1"], ops.EPI_BIAS_GELU)
-            x = lin(i, lw["w2"], lw["b2"], ops.EPI_BIAS_RESID, residual=a)
-            x = ops.layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, out=x)
+        x8 = ops.quantize_mx(x)
+        nl = len(w["layers"])
+        for li, lw in enumerate(w["layers"]):
+            qkv = ops.gemm_mx(x8, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
+            ctx8 = ops.attention_mx(qkv, mask, B, L, H, heads)
+            a = ops.gemm_mx(ctx8, lw["wo"], bias=lw["bo"], residual=x,
+                            epilogue=ops.EPI_BIAS_RESID)
+            a, a8 = ops.layernorm_mx(a, lw["ln1_g"], lw["ln1_b"], eps, out=a)
+            i8 = ops.gemm_mx(a8, lw["w1"], bias=lw["b1"], epilogue=ops.EPI_BIAS_GELU, out_mx=True)
+            x = ops.gemm_mx(i8, lw["w2"], bias=lw["b2"], residual=a, epilogue=ops.EPI_BIAS_RESID)
+            if li + 1 < nl:
+                x, x8 = ops.layernorm_mx(x, lw["ln2_g"], lw["ln2_b"], eps, out=x)
+            else:
+                x = ops.layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, out=x)
         return x
 
     def forward(self, input_ids=None, attention_mask=None, **kw):

@@ -520,3 +520,86 @@ def gemm_fp8(aq, sa, bq, sb, bias=None, epilogue=EPI_NONE, residual=None):
               K, ptr(bias), ptr(residual), residual.stride(0) if residual is not None else 0,
               ptr(out), out.stride(0), int(epilogue), stream_ptr(aq.device))
     return out
+
+
+# ---- MX-fp8 (e4m3 + E8M0 per-32 block scales; csrc/mx.h, config C5) ----
+class MX:
+    """An MX-fp8 matrix: codes uint8 [rows, K] and block scales uint8 in the MX
+    layout (K / 128 records of mpad * 4 bytes, mpad = rows rounded up to 256)."""
+
+    __slots__ = ("codes", "scales", "mpad")
+
+    def __init__(self, codes, scales, mpad):
+        self.codes, self.scales, self.mpad = codes, scales, int(mpad)
+
+    @property
+    def shape(self):
+        return self.codes.shape
+
+
+def mx_pad(rows: int) -> int:
+    return (int(rows) + 255) // 256 * 256
+
+
+def mx_empty(rows, K, device):
+    mp = mx_pad(rows)
+    return MX(torch.empty((rows, K), dtype=torch.uint8, device=device),
+              torch.zeros((K // 128) * mp * 4, dtype=torch.uint8, device=device), mp)
+
+
+def quantize_mx(x):
+    """x bf16 / fp32 [M, K] (K % 128 == 0) -> MX: per 32 consecutive values of a row
+    the smallest power-of-two scale s with max|x| / s <= 448, codes e4m3(RNE(x / s))."""
+    require_hip(x)
+    if x.dtype not in (BF16, F32):
+        raise TypeError(f"quantize_mx: bf16 or fp32 input, got {x.dtype}")
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    M, K = x.shape
+    out = mx_empty(M, K, x.device)
+    _lib.call("irc_quantize_mx_fp8", 0 if x.dtype == BF16 else 1, ptr(x), x.stride(0), M, K,
+              ptr(out.codes), K, ptr(out.scales), out.mpad, stream_ptr(x.device))
+    return out
+
+
+def gemm_mx(a: MX, b: MX, bias=None, epilogue=EPI_NONE, residual=None, out_mx=False):
+    """a [M, K] . b [N, K]^T of two MX-fp8 operands (block scales applied in the MFMA)
+    (+ bias) (-> GELU) (+ residual bf16): bf16 [M, N], or MX when out_mx (epilogues
+    EPI_BIAS / EPI_BIAS_GELU; the FFN1 output that FFN2 reads)."""
+    require_hip(a.codes, b.codes, bias, residual)
+    M, K = a.codes.shape
+    N = b.codes.shape[0]
+    if b.codes.shape[1] != K:
+        raise ValueError(f"gemm_mx inner dims differ: {K} vs {b.codes.shape[1]}")
+    if out_mx:
+        out = mx_empty(M, N, a.codes.device)
+        c, ldc, cx = out.codes, N, out.scales
+    else:
+        out = torch.empty((M, N), dtype=BF16, device=a.codes.device)
+        c, ldc, cx = out, N, None
+    _lib.call("irc_gemm_mx", ptr(a.codes), a.codes.stride(0), ptr(a.scales), a.mpad,
+              ptr(b.codes), b.codes.stride(0), ptr(b.scales), b.mpad, M, N, K, ptr(bias),
+              ptr(residual), residual.stride(0) if residual is not None else 0, ptr(c), ldc,
+              ptr(cx), int(epilogue), stream_ptr(a.codes.device))
+    return out
+
+
+def layernorm_mx(x, gamma, beta, eps=1e-12, out=None):
+    """(bf16 LN(x), its MX-fp8 copy) in one pass (x bf16 [rows, H])."""
+    require_hip(x, gamma, beta)
+    out = torch.empty_like(x) if out is None else out
+    H = x.shape[-1]
+    rows = x.numel() // H
+    mx = mx_empty(rows, H, x.device)
+    _lib.call("irc_layernorm_mx", ptr(x), ptr(out), ptr(gamma), ptr(beta), rows, H, float(eps),
+              ptr(mx.codes), ptr(mx.scales), mx.mpad, stream_ptr(x.device))
+    return out, mx
+
+
+def attention_mx(qkv, mask, B, L, H, heads):
+    """The attention context as MX-fp8 only (the fp8 out-projection's A operand)."""
+    require_hip(qkv, mask)
+    mx = mx_empty(B * L, H, qkv.device)
+    _lib.call("irc_attention_mx", ptr(qkv), ptr(mask), ptr(mx.codes), ptr(mx.scales), mx.mpad,
+              B, L, H, heads, stream_ptr(qkv.device))
+    return mx

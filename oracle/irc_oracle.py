@@ -159,6 +159,60 @@ def quantize_rows_e4m3(x: np.ndarray):
     return codes, scale
 
 
+def mx_pad(rows: int) -> int:
+    return (int(rows) + 255) // 256 * 256
+
+
+def mx_scale_index(row, col, mpad):
+    """Byte offset of (row, column)'s E8M0 scale in the MX layout (csrc/mx.h):
+    per 128-column K-tile one record of mpad * 4 bytes; within it per 256-row block
+    1 KB ordered [row bit 7][k-block = col bits 5-6][row bits 0-3][row bits 4-6]."""
+    row = np.asarray(row, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    return ((col >> 7) * mpad * 4 + (row >> 8) * 1024 + ((row >> 7) & 1) * 512 +
+            ((col >> 5) & 3) * 128 + (row & 15) * 8 + ((row >> 4) & 7))
+
+
+def mx_exponent(amax: np.ndarray) -> np.ndarray:
+    """Smallest p with amax / 2^p <= 448 (0 for amax == 0), clamped to [-127, 127]."""
+    amax = np.asarray(amax, dtype=F64)
+    p = np.zeros(amax.shape, np.int64)
+    nz = amax > 0
+    e = np.ceil(np.log2(np.where(nz, amax, 1.0) / 448.0)).astype(np.int64)
+    e = np.where(np.ldexp(448.0, e - 1) >= amax, e - 1, e)  # exact checks in fp64
+    e = np.where(np.ldexp(448.0, e) < amax, e + 1, e)
+    p[nz] = e[nz]
+    return np.clip(p, -127, 127)
+
+
+def quantize_mx_e4m3(x: np.ndarray):
+    """MX-fp8 of x [M, K] (K % 128 == 0; config C5's CDNA4 block-scaled MFMA operand,
+    not in the reference): per 32 consecutive values of a row the power-of-two scale
+    2^p of mx_exponent(block max), codes e4m3(RNE(x / 2^p)).  Returns (codes uint8
+    [M, K], scales uint8 in the MX layout with mpad = mx_pad(M) rows, E8M0 = p + 127)."""
+    x = np.asarray(x, dtype=F32)
+    M, K = x.shape
+    blk = x.reshape(M, K // 32, 32)
+    p = mx_exponent(np.max(np.abs(blk), axis=2))                  # [M, K/32]
+    scaled = (blk.astype(F64) * np.ldexp(1.0, -p)[..., None]).astype(F32)  # exact (power of 2)
+    codes = quantize_e4m3(scaled.reshape(M, K))
+    mp = mx_pad(M)
+    scales = np.zeros((K // 128) * mp * 4, np.uint8)
+    rows, kb = np.meshgrid(np.arange(M), np.arange(K // 32), indexing="ij")
+    scales[mx_scale_index(rows, kb * 32, mp)] = (p + 127).astype(np.uint8)
+    return codes, scales
+
+
+def dequantize_mx_e4m3(codes: np.ndarray, scales: np.ndarray) -> np.ndarray:
+    """float64 values of an MX-fp8 matrix (codes [M, K], scales in the MX layout)."""
+    M, K = codes.shape
+    mp = mx_pad(M)
+    rows, kb = np.meshgrid(np.arange(M), np.arange(K // 32), indexing="ij")
+    p = scales[mx_scale_index(rows, kb * 32, mp)].astype(np.int64) - 127
+    v = e4m3_decode_table()[codes].astype(F64).reshape(M, K // 32, 32)
+    return (v * np.ldexp(1.0, p)[..., None]).reshape(M, K)
+
+
 def dequantize_e4m3(codes: np.ndarray) -> np.ndarray:
     return e4m3_decode_table()[np.asarray(codes, dtype=np.uint8)]
 

@@ -6,6 +6,13 @@ BERT of src/contrastor/contrastive_module.py:36-41 -> HF nn.Linear layers).
 * irc_gemm_fp8 against a torch fp32 reference of the SAME dequantised operands
   (products of e4m3 values are exact in fp32; only the summation order and the
   bf16 output rounding differ).
+* MX-fp8 (the encoder's fp8 path since round 3: e4m3 + one E8M0 scale per 32
+  values, applied inside v_mfma_scale_f32_16x16x128_f8f6f4): irc_quantize_mx_fp8
+  bit-exact against oracle.quantize_mx_e4m3; irc_gemm_mx against the fp64 product
+  of the oracle-dequantised operands with block scales spread over 2^-20..2^20
+  (a scale applied to the wrong k-block / row / column is off by orders of
+  magnitude); the fused producers (LayerNorm, attention, the GEMM's GELU epilogue)
+  bit-exact against quantising the bf16 output of their bf16 forms.
 * The fp8 BERT-base forward against the reference's fp32 HF output
   (tests/golden/bert_base.npz) by tolerance: the error of e4m3 weights and
   inputs is stated and bounded: on MI355X rms 7.1e-2 on O(1) LayerNorm outputs
@@ -85,3 +92,104 @@ def test_bert_base_fp8_weights_vs_reference(gpu):
           f"{cos.min():.6f}")
     assert np.isfinite(out).all()
     assert rms <= 0.1 and cos.min() >= 0.995
+
+
+def _mx_matrix(gen, M, K, spread=20):
+    """[M, K] fp32 whose 32-value blocks have wildly different magnitudes."""
+    x = torch.randn(M, K, generator=gen)
+    mag = torch.pow(2.0, torch.randint(-spread, spread + 1, (M, K // 32), generator=gen).float())
+    return x * mag.repeat_interleave(32, dim=1)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_quantize_mx_bit_exact(gpu, dtype):
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(5)
+    x = _mx_matrix(g, 300, 768).to(dtype)
+    x[7, :32] = 0          # zero block -> scale 2^0
+    x[9, 64:96] = 448.0    # exactly at the e4m3 maximum -> scale 2^0
+    x[9, 96:128] = 448.25  # just above -> scale 2^1
+    mx = ops.quantize_mx(x.to(gpu))
+    rc, rs = O.quantize_mx_e4m3(x.float().numpy())
+    np.testing.assert_array_equal(mx.codes.cpu().numpy(), rc)
+    np.testing.assert_array_equal(mx.scales.cpu().numpy(), rs)
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(300, 384, 512), (1024, 768, 768), (260, 2304, 1024)])
+def test_gemm_mx_vs_oracle(gpu, epi, M, N, K):
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(M + N + K + epi)
+    a = _mx_matrix(g, M, K)
+    w = _mx_matrix(g, N, K)
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g).bfloat16()
+    am, wm = ops.quantize_mx(a.to(gpu)), ops.quantize_mx(w.to(gpu))
+    A = O.dequantize_mx_e4m3(am.codes.cpu().numpy(), am.scales.cpu().numpy())
+    W = O.dequantize_mx_e4m3(wm.codes.cpu().numpy(), wm.scales.cpu().numpy())
+    ref = A @ W.T  # exact products; fp64 sums
+    scale = np.abs(A) @ np.abs(W).T  # the fp32-accumulation error scale
+    out = ops.gemm_mx(am, wm, bias=bias.to(gpu) if epi else None, epilogue=epi,
+                      residual=res.to(gpu) if epi == 3 else None).float().cpu().numpy()
+    if epi:
+        ref = ref + bias.double().numpy()
+        scale = scale + np.abs(bias.double().numpy())
+    if epi == 2:
+        ref = torch.nn.functional.gelu(torch.from_numpy(ref)).numpy()
+    if epi == 3:
+        ref = ref + res.double().numpy()
+        scale = scale + np.abs(res.double().numpy())
+    err = np.abs(out - ref)
+    bad = err > 4e-3 * np.abs(ref) + 1e-5 * scale + 1e-30
+    assert not bad.any(), (err / (np.abs(ref) + 1e-5 * scale)).max()
+
+
+@pytest.mark.parametrize("epi", [1, 2])
+def test_gemm_mx_output_equals_quantised_bf16(gpu, epi):
+    """FFN1's MX epilogue: the e4m3 output + scales equal quantize_mx of the same
+    GEMM's bf16 output, bit for bit."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(11 + epi)
+    M, N, K = 700, 3072, 768
+    am = ops.quantize_mx(torch.randn(M, K, generator=g).to(gpu))
+    wm = ops.quantize_mx((torch.randn(N, K, generator=g) * 0.03).to(gpu))
+    bias = (torch.randn(N, generator=g) * 0.1).to(gpu)
+    y = ops.gemm_mx(am, wm, bias=bias, epilogue=epi)
+    ym = ops.gemm_mx(am, wm, bias=bias, epilogue=epi, out_mx=True)
+    ref = ops.quantize_mx(y)
+    assert torch.equal(ym.codes, ref.codes)
+    assert torch.equal(ym.scales, ref.scales)
+
+
+@pytest.mark.parametrize("H", [768, 1024])
+def test_layernorm_mx_equals_quantised_layernorm(gpu, H):
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(H)
+    x = (torch.randn(1000, H, generator=g) * 3).bfloat16().to(gpu)
+    gam = (1 + 0.1 * torch.randn(H, generator=g)).to(gpu)
+    bet = (0.1 * torch.randn(H, generator=g)).to(gpu)
+    y = ops.layernorm(x, gam, bet, 1e-12)
+    y2, ym = ops.layernorm_mx(x, gam, bet, 1e-12)
+    assert torch.equal(y, y2)
+    ref = ops.quantize_mx(y)
+    assert torch.equal(ym.codes, ref.codes) and torch.equal(ym.scales, ref.scales)
+
+
+def test_attention_mx_equals_quantised_attention(gpu):
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(17)
+    B, L, H, heads = 9, 64, 768, 12
+    qkv = torch.randn(B * L, 3 * H, generator=g).bfloat16().to(gpu)
+    mask = torch.ones(B, L, dtype=torch.int64)
+    mask[3, 40:] = 0
+    mask[5, 1:] = 0
+    mask = mask.to(gpu)
+    ctx = ops.attention(qkv, mask, B, L, H, heads)
+    cm = ops.attention_mx(qkv, mask, B, L, H, heads)
+    ref = ops.quantize_mx(ctx)
+    assert torch.equal(cm.codes, ref.codes) and torch.equal(cm.scales, ref.scales)
