@@ -357,6 +357,24 @@ int irc_layernorm_mx(const void* x, void* y, const float* gamma, const float* be
 int irc_attention_mx(const void* qkv, const int64_t* mask, void* ctx8, void* cs, int64_t mpad,
                      int64_t B, int64_t L, int64_t H, int64_t heads, irc_stream_t stream);
 
+/* ------------------------------------------------- device corpus (csrc/corpus.hip)
+ * The training corpus tokenised once and resident in HBM, so a micro-batch is
+ * the sampler's sentence indices only (replaces the DataLoader string batches of
+ * src/dataset.py:89-101, 159-182 and the per-batch tokenizer call of
+ * src/contrastor/contrastive_module.py:36-41).
+ * irc_corpus_pack: rows of irc_wordpiece's tok [n][max_tokens] (tok_len valid
+ *   ids each) -> flat int32 at offsets[i] (int64 [n+1], the exclusive scan of
+ *   tok_len).
+ * irc_pair_batch: ids / mask int64 [rows][L] = [CLS] flat[offsets[sel[r]] ..]
+ *   (truncated to L - 2) [SEP] [PAD]..., mask 1 on [CLS] .. [SEP]: the output of
+ *   bert_tokenizer(sentences, padding=True, truncation=True) for the selected
+ *   sentences when L = min(max length, 510) + 2. */
+int irc_corpus_pack(const int* tok, const int* tok_len, int64_t n, int64_t max_tokens,
+                    const int64_t* offsets, int* flat, irc_stream_t stream);
+int irc_pair_batch(const int* flat, const int64_t* offsets, const int64_t* sel, int64_t rows,
+                   int64_t L, int64_t cls_id, int64_t sep_id, int64_t pad_id, int64_t* ids,
+                   int64_t* mask, irc_stream_t stream);
+
 /* ------------------------------------------------- input pipeline (csrc/wordpiece.hip)
  * BERT WordPiece tokenisation + joint padding on the device: replaces the
  * reference's per-micro-batch host call bert_tokenizer(d1 + d2, padding=True,

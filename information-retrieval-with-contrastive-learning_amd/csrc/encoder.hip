@@ -165,8 +165,8 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const unsigned short
     u16x8 o;
     float r[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      r[t] = (v[i][t] - mean) * rstd * gg[t] + bb[t];
+    for (int t = 0; t < 8; ++t) {  // explicit fma: the same rounding in every variant
+      r[t] = __builtin_fmaf((v[i][t] - mean) * rstd, gg[t], bb[t]);
       o[t] = f32_to_bf16(r[t]);
     }
     *reinterpret_cast<u16x8*>(y + row * H + c0) = o;

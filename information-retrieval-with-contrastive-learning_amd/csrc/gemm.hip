@@ -524,7 +524,11 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
   const int swz = r32 & 7;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
+#ifdef IRC_PP_DIAG_NODMA  // diagnostic build: only K-tile 0 is loaded
+    if (kt + 1 < nk && kt < 0) {
+#else
     if (kt + 1 < nk) {
+#endif
       char* nxt = lds + (cur ^ 1) * STAGE;
       big::stage<BM>(A, g.lda, m0, g.M, (kt + 1) * BK, nxt, wave, lane);
       big::stage<BN>(B, g.ldb, n0, g.N, (kt + 1) * BK, nxt + A_BYTES, wave, lane);
@@ -551,6 +555,19 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
     __syncthreads();
   }
 
+#ifdef IRC_PP_DIAG_NOEPI  // diagnostic build: main loop only (every accumulator kept live)
+  {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < WNB; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) t += acc[i][j][e];
+    if (t == 1234.5f) reinterpret_cast<float*>(g.C)[threadIdx.x] = t;
+    return;
+  }
+#endif
   const float* bias = g.bias ? g.bias + batch * g.sBias : nullptr;
   const TO* R = g.R ? reinterpret_cast<const TO*>(g.R) + batch * g.sR : nullptr;
   constexpr int WCOLS = 32 * WNB;  // columns per wave
@@ -616,6 +633,9 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
           u16x8 o;
 #pragma unroll
           for (int t = 0; t < 8; ++t) o[t] = f32_to_bf16(v[t]);
+#ifdef IRC_PP_DIAG_NOSTORE  // diagnostic build: the epilogue without its C stores
+          if (o[0] == 0x7fc1 && o[7] == 0x7fc3)
+#endif
           *reinterpret_cast<u16x8*>(reinterpret_cast<unsigned short*>(C) + (int64_t)row * g.ldc +
                                     col) = o;
         }

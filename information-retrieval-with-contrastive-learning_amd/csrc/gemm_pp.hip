@@ -303,7 +303,11 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = (kt + par) & 1;
       // ---- L section: next tile's DMA, this tile's fragments
+#ifdef IRC_PP_DIAG_NODMA  // diagnostic build: only K-tile 0 is loaded (MFMA + LDS-read rate)
+      if (kt + 1 < nk && kt < 0) {
+#else
       if (kt + 1 < nk) {
+#endif
         stage_tile<AK, BK_, F8 == 2>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch,
                                      grp, wq, lane);
         if constexpr (F8 == 2)
@@ -548,6 +552,9 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
           u16x8 o;
 #pragma unroll
           for (int t = 0; t < 8; ++t) o[t] = f32_to_bf16(v[t]);
+#ifdef IRC_PP_DIAG_NOSTORE  // diagnostic build: the epilogue without its C stores
+          if (o[0] == 0x7fc1 && o[7] == 0x7fc3)
+#endif
           *reinterpret_cast<u16x8*>(C + (int64_t)row * g.ldc + col) = o;
         }
       } else {
@@ -729,6 +736,17 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
     epilogue_scan(g, acc, lds, m0, n0, tn, grp, wn, lane, [] {});
     return;
   }
+#ifdef IRC_PP_DIAG_NOEPI  // diagnostic build: main loop only (a guarded store of the sum of
+  {                        // every accumulator keeps all the MFMAs live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 1234.5f) reinterpret_cast<float*>(g.C)[threadIdx.x] = t;
+    return;
+  }
+#endif
   if (g.P != nullptr || g.vec_c) {
     epilogue_vec<TO, EPI, F8>(g, acc, lds, m0, n0, batch, grp, wn, wave, lane);
     return;

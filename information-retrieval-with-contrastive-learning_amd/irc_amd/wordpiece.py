@@ -219,15 +219,15 @@ class GpuWordPiece:
         self._max_len = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._host_len = torch.zeros(1, dtype=torch.int32, pin_memory=True)
 
-    def __call__(self, texts):
-        texts = list(texts)
+    def _raw(self, texts, st):
+        """WordPiece ids without special tokens on stream st: (tok int32 [n, max_tokens],
+        tok_len int32 [n], the inputs kept alive); the longest length lands in
+        self._max_len (device)."""
         n = len(texts)
         enc = [t.encode("utf-8") for t in texts]
         offs = np.zeros(n + 1, np.int64)
         np.cumsum([len(e) for e in enc], out=offs[1:])
         blob = np.frombuffer(b"".join(enc) or b"\0", np.uint8)
-        cur = torch.cuda.current_stream(self.device)
-        st = self.stream  # independent of the compute in flight on `cur`: no wait
         with torch.cuda.stream(st):
             b = torch.from_numpy(blob.copy()).pin_memory().to(self.device, non_blocking=True)
             o = torch.from_numpy(offs).pin_memory().to(self.device, non_blocking=True)
@@ -239,6 +239,15 @@ class GpuWordPiece:
                       ptr(t["cls"]), ptr(t["hid"]), ptr(t["hh"]), self.hsize, ptr(t["voff"]),
                       ptr(t["vcps"]), ptr(t["vcont"]), self.max_piece, self.unk,
                       self.max_tokens, ptr(tok), ptr(tlen), ptr(self._max_len), stream_ptr(st))
+        return tok, tlen, (b, o)
+
+    def __call__(self, texts):
+        texts = list(texts)
+        n = len(texts)
+        cur = torch.cuda.current_stream(self.device)
+        st = self.stream  # independent of the compute in flight on `cur`: no wait
+        tok, tlen, keep = self._raw(texts, st)
+        with torch.cuda.stream(st):
             self._host_len.copy_(self._max_len, non_blocking=True)
             st.synchronize()  # this stream only: the tokenizer's own work
             L = max(int(self._host_len[0]), 2)
@@ -249,6 +258,33 @@ class GpuWordPiece:
         cur.wait_stream(st)
         for x in (ids, mask):
             x.record_stream(cur)
-        for x in (b, o, tok, tlen):
+        for x in (tok, tlen) + keep:
             x.record_stream(st)
         return ids, mask
+
+    def tokenize_corpus(self, texts, chunk: int = 65536):
+        """The whole sentence list tokenised once: (flat int32 ids, offsets int64
+        [n + 1] on the device, host int32 lengths [n]) -- the DeviceCorpus layout."""
+        texts = list(texts)
+        n = len(texts)
+        st = self.stream
+        toks, lens = [], []
+        for c0 in range(0, n, chunk):
+            tok, tlen, keep = self._raw(texts[c0:c0 + chunk], st)
+            toks.append((tok, tlen, keep))
+            lens.append(tlen[:min(chunk, n - c0)])
+        with torch.cuda.stream(st):
+            tl = torch.cat(lens) if lens else torch.zeros(0, dtype=torch.int32, device=self.device)
+            host_len = tl.cpu().numpy().astype(np.int32)  # synchronises st
+        offs = np.zeros(n + 1, np.int64)
+        np.cumsum(host_len, out=offs[1:])
+        d_off = torch.from_numpy(offs).to(self.device)
+        flat = torch.empty((max(int(offs[-1]), 1),), dtype=torch.int32, device=self.device)
+        with torch.cuda.stream(st):
+            for ci, (tok, tlen, _) in enumerate(toks):
+                c0 = ci * chunk
+                m = min(chunk, n - c0)
+                _lib.call("irc_corpus_pack", ptr(tok), ptr(tlen), m, self.max_tokens,
+                          ptr(d_off[c0:]), ptr(flat), stream_ptr(st))
+            st.synchronize()
+        return flat, d_off, host_len

@@ -131,6 +131,18 @@ class RetrievalModelWrapper(nn.Module):
             ids, mask = self.tokenize(list(anchors) + list(positives), dev)
         return self.bert_extract_async(ids, mask, len(anchors), inputs_ready=True)
 
+    @torch.no_grad()
+    def bert_extract_corpus_async(self, corpus, sel, n_anchor):
+        """The device-corpus input path (irc_amd.corpus): gather + jointly pad the
+        selected sentences' resident token ids AND encode them, all on the
+        "bert_prefetch" side stream -- the micro-batch crosses the host boundary as
+        its sentence indices only.  Returns a handle for features_ready()."""
+        dev = corpus.device
+        side = side_stream(dev, "bert_prefetch")
+        with torch.cuda.stream(side):
+            ids, mask = corpus.batch(sel)
+        return self.bert_extract_async(ids, mask, n_anchor, inputs_ready=True)
+
     @staticmethod
     def features_ready(handle):
         """(anchor, positive) features of a bert_extract_async handle, usable on the

@@ -128,3 +128,61 @@ def get_dataloader(args, train=True, distributed=None):
                                        sampler=sampler, num_workers=n_jobs, drop_last=train,
                                        pin_memory=torch.cuda.is_available(),
                                        collate_fn=collate_fn)
+
+
+class PairSampler:
+    """The training DataLoader's iteration (shuffle, batch_size, drop_last; a
+    DistributedSampler slice under data parallelism) with each item's sentence
+    pair drawn exactly as DocDataset.__getitem__ draws it -- uniform:
+    np.random.choice over the document's sentences without replacement (the same
+    RNG consumption as choosing from the sentence list); tf_idf: random.choice
+    over the top 10% similar pairs -- in the main process (the reference's
+    n_jobs = 0 order).  Yields (indexes LongTensor [B, 1], sentence indices int64
+    [2B]: the anchors, then the positives) into a DeviceCorpus's numbering
+    (doc_start[d] + s), so no string ever leaves the host."""
+
+    def __init__(self, args, dataset=None):
+        self.dataset = dataset if dataset is not None else DocDataset(args)
+        docs = self.dataset.data
+        self.doc_start = np.zeros(len(docs) + 1, np.int64)
+        np.cumsum([len(d) for d in docs], out=self.doc_start[1:])
+        self.bsz = int(args.config["train"]["batch_size"])
+        group = getattr(args, "dist_group", None)
+        if group is not None:
+            import torch.distributed as dist
+
+            self.sampler = torch.utils.data.distributed.DistributedSampler(
+                self.dataset, num_replicas=dist.get_world_size(group), rank=dist.get_rank(group),
+                shuffle=True, seed=int(getattr(args, "seed", 0)), drop_last=True)
+        else:
+            self.sampler = torch.utils.data.RandomSampler(self.dataset)
+
+    def __len__(self):
+        return len(self.sampler) // self.bsz
+
+    def pair(self, idx):
+        ds = self.dataset
+        doc = ds.data[idx]
+        if ds.sample_method == "uniform":
+            i, j = np.random.choice(len(doc), size=2, replace=False)
+        elif ds.sample_method == "tf_idf":
+            sims = ds.docs_sents_similarity[idx]
+            k = math.ceil(len(sims) * ds.ratio)
+            (i, j), _ = random.choice(sims[:k])
+        else:
+            raise ValueError(ds.sample_method)
+        return int(self.doc_start[idx] + i), int(self.doc_start[idx] + j)
+
+    def __iter__(self):
+        # a DataLoader iterator draws its workers' base seed from torch's default
+        # generator before the sampler draws its permutation seed: draw it too, so
+        # the permutation (and so the pairs) are the DataLoader's
+        torch.empty((), dtype=torch.int64).random_()
+        batch = []
+        for idx in self.sampler:
+            batch.append(int(idx))
+            if len(batch) == self.bsz:
+                pairs = [self.pair(i) for i in batch]
+                sel = np.array([a for a, _ in pairs] + [b for _, b in pairs], np.int64)
+                yield torch.LongTensor(batch).view(-1, 1), sel
+                batch = []

@@ -24,7 +24,7 @@ import numpy as np
 import torch
 from tqdm import tqdm
 
-from src.dataset import get_dataloader
+from src.dataset import PairSampler, get_dataloader
 from src.contrastor.utils import run_hierarchical_clustering, run_kmeans
 from src.model import build_model, get_optimizer, load_model, save_model
 
@@ -191,7 +191,18 @@ def train(args):
     optimizer.to(args.device)
     model.train()
 
-    train_loader = get_dataloader(args, train=True)
+    # LSTM heads on frozen BERT, on the GPU: the device-corpus input path (the corpus
+    # tokenised once into HBM, micro-batches as sentence indices; the same pairs as
+    # the DataLoader with n_jobs = 0) unless dataset.device_corpus is False
+    prefetch = model.use_LSTM and args.device.type == "cuda"
+    corpus = None
+    if prefetch and args.config["dataset"].get("device_corpus", True) and args.data == "doc":
+        from irc_amd.corpus import DeviceCorpus
+
+        train_loader = PairSampler(args)
+        corpus = DeviceCorpus(train_loader.dataset.data, model.bert_tokenizer, args.device)
+    else:
+        train_loader = get_dataloader(args, train=True)
     feat_loader = None
     if args.loss in ["ProtoNCE", "HProtoNCE"]:  # train.py:62-64
         feat_loader = get_dataloader(args, train=False)
@@ -233,9 +244,11 @@ def train(args):
     # LSTM heads on frozen BERT: the next micro-batch's BERT features are issued on
     # a side stream before this micro-batch's heads step (bert_extract_async), so
     # the two overlap; the loss values are those of the sequential loop.
-    prefetch = model.use_LSTM and args.device.type == "cuda"
 
     def _issue(b):
+        if corpus is not None:
+            idx, sel = b
+            return idx, model.bert_extract_corpus_async(corpus, sel, idx.shape[0])
         idx, a, p = b
         return idx, model.bert_extract_texts_async(a, p, args.device)
 
@@ -250,7 +263,10 @@ def train(args):
             batch, nxt = nxt, next(it, None)
             try:
                 cluster_result = _maybe_recluster(cluster_result)
-                indexes, anchor_sample, positive_sample = batch
+                if corpus is not None:
+                    indexes = batch[0]
+                else:
+                    indexes, anchor_sample, positive_sample = batch
                 if prefetch:
                     cur_idx, handle = pending
                     pending = _issue(nxt) if nxt is not None else None

@@ -197,3 +197,29 @@ def test_synthetic_vocab_file_concurrent_writers():
     assert set(paths) == {path}
     with open(path) as f:
         assert len(f.read().split()) == n
+
+
+@pytest.mark.gpu
+def test_device_corpus_batches_match_tokenizer(gpu, hf_tok):
+    """irc_amd.corpus.DeviceCorpus: the corpus tokenised once (in several chunks)
+    and packed in HBM; any selection of its sentences, gathered and jointly padded
+    by irc_pair_batch, is token-exact with the tokenizer's padding=True,
+    truncation=True output for those sentences (incl. one over the 512 limit)."""
+    from irc_amd.corpus import DeviceCorpus
+
+    texts = _corpus(np.random.default_rng(3))
+    long_one = " ".join(["supercalifragilistic"] * 400)  # > 510 pieces: truncated
+    docs = [texts[i:i + 5] for i in range(0, len(texts), 5)] + [[long_one, "short one ."]]
+    flat = [s for d in docs for s in d]
+    corpus = DeviceCorpus(docs, hf_tok, gpu, chunk=16)  # several tokenisation chunks
+    assert corpus.n_sentences == len(flat)
+    rng = np.random.default_rng(4)
+    for n in (1, 7, 64, len(flat)):
+        sel = rng.choice(len(flat), n, replace=False)
+        ids, mask = corpus.batch(sel)
+        ref = hf_tok([flat[i] for i in sel], padding=True, truncation=True, return_tensors="pt")
+        assert torch.equal(ids.cpu(), ref["input_ids"]), n
+        assert torch.equal(mask.cpu(), ref["attention_mask"]), n
+    sel = np.array([corpus.sentence_index(len(docs) - 1, 0)])
+    ids, _ = corpus.batch(sel)
+    assert ids.shape[1] == 512

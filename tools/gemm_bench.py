@@ -44,7 +44,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--layouts", action="store_true")
+    ap.add_argument("--only", default="", help="comma-separated shape names")
     args = ap.parse_args()
+    only = set(filter(None, args.only.split(",")))
     from irc_amd import ops
 
     dev = torch.device("cuda:0")
@@ -70,6 +72,8 @@ def main():
             print(f"square4k {lay:6s} {us:9.1f} us  {tf:7.1f} TF/s  {tf / 2500:.1%}", flush=True)
         return
     for name, M, N, K, epi in SHAPES:
+        if only and name not in only:
+            continue
         if epi < 0:  # K-outer operands: C[M,N] = A[K,M]^T B[K,N], fp32 accumulate
             a = torch.randn((K, M), device=dev).to(torch.bfloat16)
             b = torch.randn((K, N), device=dev).to(torch.bfloat16)
