@@ -266,6 +266,27 @@ int irc_nce_lse(const float* S, const float* LQ, int64_t N, int64_t K, float T, 
                 float* loss_row, irc_stream_t stream);
 int irc_nce_grads(const float* S, const float* LQ, const float* lse, int64_t N, int64_t K,
                   float T, const float* gscale, float* GS, float* GQ, irc_stream_t stream);
+/* Fused InfoNCE for D in {32, 64, ..., 256} (the LSTM head's embedding width):
+ * NCELoss._compute_info_loss (src/contrastor/contrastive_loss.py:56-93) without
+ * materialising S = F F^T [2N, 2N] or q . queue [N, K] in HBM.  F = [q; k] fp32
+ * [2N][D], queue fp32 [D][K] (K = 0: no queue).  Exact-fp32 MFMA logits, online
+ * row max / sum exp, fixed-order partial reductions (deterministic).
+ * The rows computed are those of the pairs [p_lo, p_hi): q rows p_lo .. p_hi-1 and
+ * k rows N + p_lo .. N + p_hi-1 -- all 2N rows for [0, N) (any N); a sub-range (a
+ * data-parallel rank's local pairs) needs N, p_lo, p_hi multiples of 32.
+ * irc_nce_fused_fwd: lse[r], loss_row[r] = lse_r - logit_{r, pos(r)} for the rows
+ *   computed (lse / loss_row indexed by absolute row, [2N]).
+ * irc_nce_fused_bwd: dF [2P][D] (P = p_hi - p_lo; q rows then k rows) = d(loss) /
+ *   d(F rows) with loss = sum over ALL 2N rows of loss_row / 2, times *gscale;
+ *   needs every row's lse (a sub-range caller all-gathers them first).
+ * workspace: irc_nce_fused_workspace bytes (the same for both calls). */
+int64_t irc_nce_fused_workspace(int64_t N, int64_t D, int64_t K, int64_t p_lo, int64_t p_hi);
+int irc_nce_fused_fwd(const float* F, const float* queue, int64_t N, int64_t D, int64_t K,
+                      float T, int64_t p_lo, int64_t p_hi, void* ws, int64_t ws_bytes, float* lse,
+                      float* loss_row, irc_stream_t stream);
+int irc_nce_fused_bwd(const float* F, const float* queue, const float* lse, int64_t N, int64_t D,
+                      int64_t K, float T, const float* gscale, int64_t p_lo, int64_t p_hi,
+                      void* ws, int64_t ws_bytes, float* dF, irc_stream_t stream);
 int irc_sum(const float* x, int64_t n, float scale, float* partial, float* out,
             irc_stream_t stream);
 int irc_grad_norm_clip(const float* g, int64_t n, float max_norm, float* partial, float* out /* >= 3 */,

@@ -479,6 +479,21 @@ __device__ __forceinline__ void stage(const unsigned short* __restrict__ X, int6
     glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
   }
 }
+// passes [P0, P1) of stage<ROWS> (spreading one K-tile's DMA over the k-steps)
+template <int ROWS, int P0, int P1>
+__device__ __forceinline__ void stage_part(const unsigned short* __restrict__ X, int64_t ld,
+                                           int r0, int nrows, int k0, char* lds_tile, int wave,
+                                           int lane) {
+#pragma unroll
+  for (int i = P0; i < P1; ++i) {
+    const int p = (i * NW + wave) * 64 + lane;
+    const int row = p >> 3;
+    const int c = (p & 7) ^ (row & 7);
+    int gr = r0 + row;
+    gr = gr < nrows ? gr : nrows - 1;
+    glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
+  }
+}
 }  // namespace big
 
 template <typename TO, int EPI, int WNB>
@@ -525,18 +540,32 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
 #ifdef IRC_PP_DIAG_NODMA  // diagnostic build: only K-tile 0 is loaded
-    if (kt + 1 < nk && kt < 0) {
+    const bool more = kt + 1 < nk && kt < 0;
 #else
-    if (kt + 1 < nk) {
+    const bool more = kt + 1 < nk;
 #endif
+#ifndef IRC_BIG_SPREAD
+    if (more) {
       char* nxt = lds + (cur ^ 1) * STAGE;
       big::stage<BM>(A, g.lda, m0, g.M, (kt + 1) * BK, nxt, wave, lane);
       big::stage<BN>(B, g.ldb, n0, g.N, (kt + 1) * BK, nxt + A_BYTES, wave, lane);
     }
+#endif
     const char* la = lds + cur * STAGE;
     const char* lb = la + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
+#ifdef IRC_BIG_SPREAD  // A/B build: the next K-tile's DMA spread over the 4 k-steps
+      if (more) {
+        char* nxt = lds + (cur ^ 1) * STAGE;
+        constexpr int PA = BM * 8 / NT, PB = BN * 8 / NT;  // 4, 2 * WNB passes
+        const int k1 = (kt + 1) * BK;
+        if (kk == 0) big::stage_part<BM, 0, PA / 2>(A, g.lda, m0, g.M, k1, nxt, wave, lane);
+        if (kk == 1) big::stage_part<BM, PA / 2, PA>(A, g.lda, m0, g.M, k1, nxt, wave, lane);
+        if (kk == 2) big::stage_part<BN, 0, PB / 2>(B, g.ldb, n0, g.N, k1, nxt + A_BYTES, wave, lane);
+        if (kk == 3) big::stage_part<BN, PB / 2, PB>(B, g.ldb, n0, g.N, k1, nxt + A_BYTES, wave, lane);
+      }
+#endif
       const int coff = (((2 * kk + h) ^ swz) * 16);
       bf16x8 fa[4], fb[WNB];
 #pragma unroll
@@ -589,6 +618,21 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+#ifdef IRC_BIG_RPRE  // A/B build: the pass's residual rows loaded before its LDS staging
+      constexpr int CPRR = WCOLS / 8, NRR = 32 * CPRR / 64;
+      u16x8 rpre[NRR];
+      if constexpr (sizeof(TO) == 2 && (EPI == EPI_BIAS_RESID || EPI == EPI_RESID)) {
+#pragma unroll
+        for (int it = 0; it < NRR; ++it) {
+          const int c = it * 64 + lane;
+          const int row = rbase0 + i * 32 + c / CPRR, col = cbase + (c % CPRR) * 8;
+          rpre[it] = (row < g.M && col < g.N)
+                         ? *reinterpret_cast<const u16x8*>(
+                               reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col)
+                         : (u16x8)0;
+        }
+      }
+#endif
 #pragma unroll
       for (int j = 0; j < WNB; ++j)
 #pragma unroll
@@ -613,8 +657,13 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
           const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c8 + 4]);
           float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
           if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
+#ifdef IRC_BIG_RPRE
+            const u16x8 rr = EPI == EPI_DGELU ? *reinterpret_cast<const u16x8*>(
+                reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col) : rpre[it];
+#else
             const u16x8 rr = *reinterpret_cast<const u16x8*>(
                 reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col);
+#endif
 #pragma unroll
             for (int t = 0; t < 8; ++t)
               v[t] = EPI == EPI_DGELU ? v[t] * gelu_grad_fast(bf16_to_f32(rr[t]))

@@ -308,8 +308,13 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
 #else
       if (kt + 1 < nk) {
 #endif
+#ifdef IRC_MX_NO_REDERIVE  // A/B build: DMA addresses kept live as in the bf16 loop
+        stage_tile<AK, BK_, false>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch,
+                                   grp, wq, lane);
+#else
         stage_tile<AK, BK_, F8 == 2>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch,
                                      grp, wq, lane);
+#endif
         if constexpr (F8 == 2)
           stage_scales(g, m0, n0, kbeg / BK + kt + 1, lds + MX_SC_OFF + (cur ^ 1) * 2048, grp, wq,
                        lane);
@@ -320,21 +325,19 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
       uint2 xa;     // MX: the lane's E8M0 block scales of its A rows 16 i + r (byte i)
       uint32_t xb;  // ... and of its B cols (byte j)
       if constexpr (F8 == 2) {
-        // lane l feeds k-block q = l >> 4 of row/col l & 15: 32 contiguous e4m3 =
-        // 16-byte chunks 2q, 2q + 1 of the 128-byte K-tile row (K-major images)
+        // The 16x16x128 f8 MFMA's operand map (probed on MI355X, tools/probe/mx_probe.hip):
+        // lane l holds k [16q, 16q + 16) and [64 + 16q, 64 + 16q + 16) of row / col
+        // l & 15, q = l >> 4 -- the same two 16-byte chunks q, q + 4 as the
+        // unit-scale path -- and the scale of row i, 32-k block b comes from lane
+        // i + 16 b.  So the fragments keep the natural k order and lane l supplies
+        // the E8M0 byte of block q = l >> 4.
         const int q = lane >> 4;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int row = bcol + 16 * j + (lane & 15);
-            fb[j][c] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + 16 * ((2 * q + c) ^ (row & 7)));
-          }
+          for (int j = 0; j < 4; ++j) fb[j][c] = frag<BK_>(lb, bcol + 16 * j, c, lane);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int row = 16 * i + (lane & 15);
-            fa[i][c] = *reinterpret_cast<const bf16x8*>(la + row * 128 + 16 * ((2 * q + c) ^ (row & 7)));
-          }
+          for (int i = 0; i < 8; ++i) fa[i][c] = frag<AK>(la, 16 * i, c, lane);
         }
         const char* sc = lds + MX_SC_OFF + cur * 2048;
         const int rq = (q * 16 + (lane & 15)) * 8;

@@ -29,6 +29,7 @@ import torch.nn as nn
 from irc_amd import ops
 from irc_amd._torch import side_stream
 from irc_amd.dist import gather_rows
+from irc_amd.nce import dist_fused_ok, info_nce_dist
 from irc_amd.bert import BertModel
 from irc_amd.bert_train import BertEncoder, seq2vec_ids
 from irc_amd.lstm_head import LSTMHead, seq2vec as head_seq2vec
@@ -248,6 +249,16 @@ class RetrievalModelWrapper(nn.Module):
     def _loss_tail(self, emb_q, emb_k, cluster_result, indexes):
         """contrastive_module.py:85-92: (global negatives,) loss, enqueue."""
         group = getattr(self, "dist_group", None)
+        if group is not None and cluster_result is None and emb_q.is_cuda and \
+                dist_fused_ok(emb_q.shape[0], emb_q.shape[1]):
+            # data parallel, fused InfoNCE: this rank computes only its own pairs'
+            # loss rows over the gathered batch (irc_amd.nce.info_nce_dist)
+            keys = emb_k if not self.use_momentum else emb_k.detach()
+            queue = None if not self.use_queue or not self.add_queue_to_loss else self.queue
+            loss = info_nce_dist(emb_q, keys, queue, self.criterion.T, group)
+            if self.use_queue and self.training:
+                self._dequeue_and_enqueue(gather_rows(emb_k.detach(), group))
+            return loss
         if group is not None:  # global in-batch negatives (irc_amd.dist)
             emb_q = gather_rows(emb_q, group)
             # keys carry autograd only without the momentum encoder (then they come

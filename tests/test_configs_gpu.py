@@ -320,3 +320,40 @@ def test_every_doc_survives_at_q2048(gpu):
     assert torch.equal(i, want_i)
     ref = retrieval.scan_scores(q, d[:1])
     assert torch.equal(s, ref.expand(Q, k))
+
+
+@pytest.mark.parametrize("case", [0, 1])
+def test_nce_fused_matches_unfused_and_times(gpu, case, monkeypatch):
+    """The fused InfoNCE (csrc/nce_fused.hip; S and LQ never in HBM) against the
+    unfused GEMM path at the C3 / C4 global batches: same loss (fp32 exact MFMA in
+    both, different summation order) and dq; both timed (forward + backward, HIP
+    events), the fused one expected no slower."""
+    from irc_amd import nce
+
+    n, d, kq, seed = SI.NCE_C34_CASES[case]
+    q, k, queue = SI.nce_c2_inputs(n, d, kq, seed)
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("IRC_NCE_FUSED", fused)
+        qq = torch.from_numpy(q).to(gpu).requires_grad_(True)
+        kk, qu = torch.from_numpy(k).to(gpu), torch.from_numpy(queue).to(gpu)
+
+        def run():
+            qq.grad = None
+            loss = nce.info_nce(qq, kk, qu, 0.05)
+            loss.backward()
+            return loss
+
+        for _ in range(3):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            loss = run()
+        e1.record()
+        torch.cuda.synchronize()
+        out[fused] = (loss.item(), qq.grad.clone(), e0.elapsed_time(e1) / 10 * 1e3)
+    (lf, gf, tf), (lu, gu, tu) = out["1"], out["0"]
+    print(f"N={n} K={kq}: fused {tf:.1f} us, unfused {tu:.1f} us (fwd+bwd); loss {lf:.4f} / {lu:.4f}")
+    assert abs(lf - lu) <= 1e-5 * abs(lu)
+    assert ((gf - gu).norm() / gu.norm()).item() <= 1e-5

@@ -141,9 +141,14 @@ def test_gemm_mx_vs_oracle(gpu, epi, M, N, K):
     if epi == 3:
         ref = ref + res.double().numpy()
         scale = scale + np.abs(res.double().numpy())
+    # bf16 output rounding + fp32 accumulation of terms spanning 2^80 (blocks scaled
+    # 2^-20..2^20 on both sides): 1e-4 of the |A||W| scale; a scale applied to the
+    # wrong block / row / column is wrong by orders of magnitude
     err = np.abs(out - ref)
-    bad = err > 4e-3 * np.abs(ref) + 1e-5 * scale + 1e-30
-    assert not bad.any(), (err / (np.abs(ref) + 1e-5 * scale)).max()
+    bad = err > 4e-3 * np.abs(ref) + 1e-4 * scale + 1e-30
+    worst = (err / (np.abs(ref) + 1e-4 * scale)).max()
+    print(f"gemm_mx M={M} N={N} K={K} epi={epi}: worst err / (|ref| + 1e-4 scale) {worst:.3e}")
+    assert not bad.any(), worst
 
 
 @pytest.mark.parametrize("epi", [1, 2])

@@ -125,9 +125,9 @@ def main():
     lens = []
     f_issue = CM.RetrievalModelWrapper.bert_extract_async
 
-    def issue(self, ids, mask, n):
+    def issue(self, ids, mask, n, **kw):
         lens.append(ids.shape[1])
-        return f_issue(self, ids, mask, n)
+        return f_issue(self, ids, mask, n, **kw)
     CM.RetrievalModelWrapper.bert_extract_async = issue
     wrap(CM.RetrievalModelWrapper, "bert_extract_async", "bert_issue")
     wrap(T.TrainState, "micro_batch", "step_issue")

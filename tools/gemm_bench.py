@@ -45,8 +45,11 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--layouts", action="store_true")
     ap.add_argument("--only", default="", help="comma-separated shape names")
+    ap.add_argument("--mx", action="store_true", help="MX-fp8 GEMMs (irc_gemm_mx) of the BERT shapes")
     args = ap.parse_args()
     only = set(filter(None, args.only.split(",")))
+    if args.mx:
+        return mx_shapes(args)
     from irc_amd import ops
 
     dev = torch.device("cuda:0")
@@ -116,6 +119,37 @@ def main():
         tf = 2.0 * M * N * K / us / 1e6
         print(f"{name:14s} M={M:6d} N={N:5d} K={K:5d} epi={epi}  {us:9.1f} us  {tf:7.1f} TF/s  "
               f"{tf / 2500:.1%}", flush=True)
+
+
+def mx_shapes(args):
+    """The frozen encoder's four linear layers on MX-fp8 at M = 32768 (C5): HIP-event
+    time per launch and the fraction of the 5 PF dense fp8 peak."""
+    from irc_amd import ops
+
+    dev = torch.device("cuda:0")
+    for name, M, N, K, epi, omx in (("qkv", 32768, 2304, 768, 1, False),
+                                    ("attn_out+res", 32768, 768, 768, 3, False),
+                                    ("ffn1+gelu>mx", 32768, 3072, 768, 2, True),
+                                    ("ffn1+gelu", 32768, 3072, 768, 2, False),
+                                    ("ffn2+res", 32768, 768, 3072, 3, False)):
+        a = ops.quantize_mx(torch.randn((M, K), device=dev).to(torch.bfloat16))
+        w = ops.quantize_mx(torch.randn((N, K), device=dev) * 0.03)
+        bias = torch.randn((N,), device=dev)
+        res = torch.randn((M, N), device=dev).to(torch.bfloat16) if epi == 3 else None
+        run = lambda: ops.gemm_mx(a, w, bias=bias, epilogue=epi, residual=res, out_mx=omx)  # noqa: E731
+        for _ in range(3):
+            run()
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(args.iters):
+            run()
+        e1.record(st)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / args.iters
+        tf = 2.0 * M * N * K / us / 1e6
+        print(f"mx {name:14s} M={M:6d} N={N:5d} K={K:5d} epi={epi}  {us:9.1f} us  {tf:7.1f} TF/s  "
+              f"{tf / 5000:.1%}", flush=True)
 
 
 if __name__ == "__main__":
