@@ -14,11 +14,21 @@ namespace gpp {
 // p = 0 for an all-zero block.  Matches oracle.quantize_mx_e4m3 bit for bit.
 __device__ __forceinline__ int mx_exponent(float amax) {
   if (!(amax > 0.f)) return 0;
-  int e;
-  (void)frexpf(amax / 448.f, &e);  // amax/448 ~ f * 2^e, f in [0.5, 1): 2^(e-1) <= . < 2^e
-  if (ldexpf(448.f, e - 1) >= amax) e -= 1;  // rounding of amax / 448 at a power of two
-  if (ldexpf(448.f, e) < amax) e += 1;
+  // amax = m 2^E, m in [1, 2) (E = -127 for subnormals, which clamp anyway):
+  // amax <= 448 2^p = 1.75 2^(p + 8)  <=>  p >= E - 8 + (m > 1.75), from the bits
+  // (no division: this runs per lane in every MX epilogue)
+  const uint32_t b = __float_as_uint(amax);
+  const int e = (int)(b >> 23) - 135 + ((b & 0x7fffffu) > 0x600000u ? 1 : 0);
   return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+
+// max over the 4 lanes of a quad (lane ^ 1, lane ^ 2) by DPP quad permutes: no LDS
+// traffic (the epilogues around this are LDS-bound already)
+__device__ __forceinline__ float quad_max(float x) {
+  const int xi = __float_as_int(x);
+  float y = fmaxf(x, __int_as_float(__builtin_amdgcn_mov_dpp(xi, 0xB1, 0xF, 0xF, false)));  // [1,0,3,2]
+  const int yi = __float_as_int(y);
+  return fmaxf(y, __int_as_float(__builtin_amdgcn_mov_dpp(yi, 0x4E, 0xF, 0xF, false)));  // [2,3,0,1]
 }
 
 // Quantise 8 fp32 values of one 32-value MX block (the other 24 held by the lanes
@@ -27,8 +37,7 @@ __device__ __forceinline__ unsigned mx_quant8(const float (&v)[8], uint2& out) {
   float am = 0.f;
 #pragma unroll
   for (int t = 0; t < 8; ++t) am = fmaxf(am, fabsf(v[t]));
-  am = fmaxf(am, __shfl_xor(am, 1, 64));
-  am = fmaxf(am, __shfl_xor(am, 2, 64));
+  am = quad_max(am);
   const int p = mx_exponent(am);
   const float inv = ldexpf(1.f, -p);
   uint32_t w0 = 0, w1 = 0;

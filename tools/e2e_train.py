@@ -95,16 +95,22 @@ def main():
 
     from src import train as T
 
-    stamps = []
+    stamps, events = [], []
     orig = T.TrainState.micro_batch
 
     def timed(self, *a, **k):
         out = orig(self, *a, **k)
-        stamps.append(time.perf_counter())  # after loss.item(): the step's GPU work done
+        stamps.append(time.perf_counter())
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()  # the step's work on the training stream (it joins the others)
+        events.append(ev)
         return out
 
-    T.TrainState.micro_batch = timed  # stamps are host enqueue times: the rate is taken
-    # from stamp w to the final device synchronisation below
+    # The rate is taken between device events recorded after step w and after the
+    # last step, so the host's end-of-run work (checkpoint save, writer close) is
+    # not charged to the loop; host stalls between steps (DataLoader, sampling,
+    # tokenisation) still show as gaps between the events.
+    T.TrainState.micro_batch = timed
     # host-time breakdown of the loop (seconds spent inside each call)
     from src.contrastor import contrastive_module as CM
 
@@ -139,7 +145,7 @@ def main():
     torch.cuda.synchronize()
     t_end = time.perf_counter()
     w = min(5, len(stamps) - 2)
-    dt = (t_end - stamps[w]) / (len(stamps) - 1 - w)
+    dt = events[w].elapsed_time(events[-1]) * 1e-3 / (len(stamps) - 1 - w)
     print(f"end-to-end main.py train: {args.batch / dt:.0f} pairs/s ({dt * 1e3:.2f} ms/step over "
           f"{len(stamps) - 1 - w} steps, {args.workers} DataLoader workers, B = {args.batch})")
     tot = t_end - t_start
