@@ -249,8 +249,11 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
   }
 }
 
-// MFMA attention, bf16, head dim 64, L = 32*NJ (NJ <= 4): one wave per
-// (sequence, head, block of 32 queries).
+// MFMA attention, bf16, head dim 64, L <= 32*NJ (NJ <= 4, any L: the joint
+// padding of a batch gives e.g. L = 72): one wave per (sequence, head, block of
+// 32 queries).  Key rows past L are read clamped and carry a -3e30 bias (below a
+// masked key's -1e30, so an all-masked row still averages its L keys), V rows
+// past L are zero in LDS, query rows past L are never stored.
 //  * S^T[j][i] = K[j] . Q[i] on v_mfma_f32_32x32x16_bf16 (A = K rows, B = Q rows,
 //    both read straight from the fused QKV rows as 16-byte fragments), so lane
 //    (i, half) holds query i's scores for the keys j = 32jb + (e&3) + 8(e>>2) + 4*half:
@@ -272,9 +275,11 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
                                                             int B, int H, int heads, float scale,
                                                             unsigned char* __restrict__ ctx8 = nullptr,
                                                             unsigned char* __restrict__ cs = nullptr,
-                                                            int64_t mpad = 0) {
+                                                            int64_t mpad = 0, int Lr = 32 * NJ) {
   constexpr int L = 32 * NJ, DH = 64;
-  constexpr int VP = L + 4;  // V^T row pitch (u16): 8-byte aligned, conflict-free b64 reads
+  // V^T row pitch (u16): 8-byte aligned, conflict-free b64 reads (MXO at L = 32: 68,
+  // so the slot also holds the 32 x 68-float O staging)
+  constexpr int VP = (MXO && L + 4 < 68) ? 68 : L + 4;
   __shared__ __attribute__((aligned(16))) unsigned short vt[4][DH][VP];
   __shared__ __attribute__((aligned(16))) float mb[4][L];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -285,20 +290,23 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
   const int a = active ? (int)(item / NJ % heads) : 0;
   const int b = active ? (int)(item / NJ / heads) : 0;
   const int64_t ld3 = 3LL * H;
-  const unsigned short* base = qkv + (int64_t)b * L * ld3 + a * DH;  // + j*ld3: Q | +H: K | +2H: V
+  const unsigned short* base = qkv + (int64_t)b * Lr * ld3 + a * DH;  // + j*ld3: Q | +H: K | +2H: V
   if (active) {
     for (int p = lane; p < (L / 2) * 8; p += 64) {
       const int dc = p & 7, j = (p >> 3) * 2;  // 8-wide d chunk, key pair (j, j+1)
-      const u16x8 v0 = *reinterpret_cast<const u16x8*>(base + (int64_t)j * ld3 + 2 * H + dc * 8);
+      const u16x8 v0 = j < Lr ? *reinterpret_cast<const u16x8*>(base + (int64_t)j * ld3 + 2 * H + dc * 8)
+                              : (u16x8)0;
       const u16x8 v1 =
-          *reinterpret_cast<const u16x8*>(base + (int64_t)(j + 1) * ld3 + 2 * H + dc * 8);
+          j + 1 < Lr ? *reinterpret_cast<const u16x8*>(base + (int64_t)(j + 1) * ld3 + 2 * H + dc * 8)
+                     : (u16x8)0;
 #pragma unroll
       for (int dd = 0; dd < 8; ++dd)
         *reinterpret_cast<uint32_t*>(&vt[wv][dc * 8 + dd][j]) =
             (uint32_t)v0[dd] | ((uint32_t)v1[dd] << 16);
     }
     for (int j = lane; j < L; j += 64)
-      mb[wv][j] = (mask == nullptr || mask[(int64_t)b * L + j] != 0) ? 0.f : -1e30f;
+      mb[wv][j] = j >= Lr ? -3e30f
+                          : ((mask == nullptr || mask[(int64_t)b * Lr + j] != 0) ? 0.f : -1e30f);
   }
   __syncthreads();
   if (!active) return;  // past the only barrier
@@ -306,15 +314,16 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
   bf16x8 qf[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk)
-    qf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)(32 * ib + r32) * ld3 + 16 * kk + 8 * h);
+    qf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)min(32 * ib + r32, Lr - 1) * ld3 +
+                                               16 * kk + 8 * h);
   f32x16 s[NJ];
 #pragma unroll
   for (int jb = 0; jb < NJ; ++jb) {
     s[jb] = (f32x16)0.f;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(base + (int64_t)(32 * jb + r32) * ld3 + H +
-                                                         16 * kk + 8 * h);
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(
+          base + (int64_t)min(32 * jb + r32, Lr - 1) * ld3 + H + 16 * kk + 8 * h);
       s[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], s[jb], 0, 0, 0);
     }
   }
@@ -365,32 +374,60 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
     }
   // O C layout: col = d (lane), row = query 32ib + (e&3) + 8(e>>2) + 4h
   if constexpr (MXO) {
-    const int64_t row0 = (int64_t)b * L + 32 * ib;
-    unsigned char* out8 = ctx8 + row0 * H + a * DH;
+    // O (bf16-rounded like the bf16 path's ctx) goes through this wave's V^T slot,
+    // free once the P.V reads have returned, as [32 rows][OP floats]; each lane
+    // then owns one MX block (row lane >> 1, 32 columns): lane-local block max,
+    // 32 codes in two 16-byte stores, one scale byte.
+    constexpr int OP = 68;  // row pitch (floats): 16-byte rows, h halves 16 banks apart
+    static_assert(32 * OP * 4 <= (int)sizeof(vt[0]), "O staging fits the V^T slot");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    float* os = reinterpret_cast<float*>(&vt[wv][0][0]);
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int i = (e & 3) + 8 * (e >> 2) + 4 * h;
-        // bf16-rounded like the bf16 path's ctx, then quantised per 32 columns
-        const float v = bf16_to_f32(f32_to_bf16(o[db][e]));
-        float am = fabsf(v);
-#pragma unroll
-        for (int m = 1; m < 32; m <<= 1) am = fmaxf(am, __shfl_xor(am, m, 64));
-        const int p = gpp::mx_exponent(am);
-        const uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(v * ldexpf(1.f, -p), 0.f, 0u, false);
-        out8[(int64_t)i * H + 32 * db + r32] = (unsigned char)(w & 0xffu);
-        if (r32 == 0) cs[gpp::mx_scale_index(row0 + i, a * DH + 32 * db, mpad)] = (unsigned char)(p + 127);
+        os[i * OP + 32 * db + r32] = bf16_to_f32(f32_to_bf16(o[db][e]));
       }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int i = lane >> 1, cb = 32 * (lane & 1);
+    float v[32];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(&os[i * OP + cb + 4 * t]);
+      v[4 * t] = x[0];
+      v[4 * t + 1] = x[1];
+      v[4 * t + 2] = x[2];
+      v[4 * t + 3] = x[3];
+    }
+    float am = 0.f;
+#pragma unroll
+    for (int t = 0; t < 32; ++t) am = fmaxf(am, fabsf(v[t]));
+    const int p = gpp::mx_exponent(am);
+    const float sc = ldexpf(1.f, -p);
+    uint32_t w[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      uint32_t x = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * t] * sc, v[4 * t + 1] * sc, 0u, false);
+      w[t] = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * t + 2] * sc, v[4 * t + 3] * sc, x, true);
+    }
+    if (32 * ib + i >= Lr) return;
+    const int64_t row = (int64_t)b * Lr + 32 * ib + i;
+    uint4* dst = reinterpret_cast<uint4*>(ctx8 + row * H + a * DH + cb);
+    dst[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    dst[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    cs[gpp::mx_scale_index(row, a * DH + cb, mpad)] = (unsigned char)(p + 127);
     return;
   }
-  unsigned short* out = ctx + ((int64_t)b * L + 32 * ib) * H + a * DH;
+  unsigned short* out = ctx + ((int64_t)b * Lr + 32 * ib) * H + a * DH;
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int i = (e & 3) + 8 * (e >> 2) + 4 * h;
-      out[(int64_t)i * H + 32 * db + r32] = f32_to_bf16(o[db][e]);
+      if (32 * ib + i < Lr) out[(int64_t)i * H + 32 * db + r32] = f32_to_bf16(o[db][e]);
     }
 }
 
@@ -466,29 +503,30 @@ extern "C" int irc_layernorm_mx(const void* x, void* y, const float* gamma, cons
   return check_launch("layernorm_mx");
 }
 
-// MFMA attention (bf16 QKV, head dim 64, L % 32 == 0, L <= 128) whose context
+// MFMA attention (bf16 QKV, head dim 64, L <= 128) whose context
 // leaves as MX-fp8 (ctx8 e4m3 [B*L][H], cs E8M0 scales in the MX layout, mpad rows):
 // the fp8 out-projection's A operand (config C5).
 extern "C" int irc_attention_mx(const void* qkv, const int64_t* mask, void* ctx8, void* cs,
                                 int64_t mpad, int64_t B, int64_t L, int64_t H, int64_t heads,
                                 irc_stream_t stream) {
-  IRC_REQUIRE(heads >= 1 && H % heads == 0 && H / heads == 64 && L % 32 == 0 && L >= 32 &&
-                  L <= 128, "attention_mx: head dim 64 and L in {32, 64, 96, 128} required");
+  IRC_REQUIRE(heads >= 1 && H % heads == 0 && H / heads == 64 && L >= 1 && L <= 128,
+              "attention_mx: head dim 64 and L <= 128 required");
   IRC_REQUIRE(mpad >= (B * L + 255) / 256 * 256, "attention_mx: mpad must cover B*L rounded to 256");
+  IRC_REQUIRE((uintptr_t)ctx8 % 16 == 0 && H % 16 == 0, "attention_mx: 16-byte aligned ctx8 rows");
   if (B == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
-  const int64_t waves = B * heads * (L / 32);
+  const int64_t waves = B * heads * ((L + 31) / 32);
   const dim3 grid((unsigned)((waves + 3) / 4));
   const float sc = 0.125f;
   auto* c8 = static_cast<unsigned char*>(ctx8);
   auto* css = static_cast<unsigned char*>(cs);
   prof_begin(st);
-  switch (L / 32) {
+  switch ((L + 31) / 32) {
 #define IRC_ATTX(NJ)                                                                             \
   case NJ:                                                                                       \
     hipLaunchKernelGGL((enc::attention_mfma_kernel<NJ, true>), grid, dim3(256), 0, st,          \
                        (const unsigned short*)qkv, mask, (unsigned short*)nullptr, (int)B, (int)H, \
-                       (int)heads, sc, c8, css, mpad);                                           \
+                       (int)heads, sc, c8, css, mpad, (int)L);                                   \
     break;
     IRC_ATTX(1) IRC_ATTX(2) IRC_ATTX(3) IRC_ATTX(4)
 #undef IRC_ATTX
@@ -537,24 +575,21 @@ extern "C" int irc_attention(int dtype, const void* qkv, const int64_t* mask, vo
               "attention: L=%lld too long for LDS staging", (long long)L);
   if (B == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
-  if (dtype == 0 && dh == 64 && L % 32 == 0 && L <= 128) {  // production shape: MFMA
-    const int64_t waves = B * heads * (L / 32);
+  if (dtype == 0 && dh == 64 && L <= 128) {  // production shape: MFMA (any L <= 128)
+    const int64_t waves = B * heads * ((L + 31) / 32);
     const dim3 grid((unsigned)((waves + 3) / 4));
     const float sc = 0.125f;  // 1/sqrt(64)
     prof_begin(st);
-    switch (L / 32) {
-      case 1: hipLaunchKernelGGL(enc::attention_mfma_kernel<1>, grid, dim3(256), 0, st,
-                                 (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B,
-                                 (int)H, (int)heads, sc); break;
-      case 2: hipLaunchKernelGGL(enc::attention_mfma_kernel<2>, grid, dim3(256), 0, st,
-                                 (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B,
-                                 (int)H, (int)heads, sc); break;
-      case 3: hipLaunchKernelGGL(enc::attention_mfma_kernel<3>, grid, dim3(256), 0, st,
-                                 (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B,
-                                 (int)H, (int)heads, sc); break;
-      default: hipLaunchKernelGGL(enc::attention_mfma_kernel<4>, grid, dim3(256), 0, st,
-                                  (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B,
-                                  (int)H, (int)heads, sc); break;
+    switch ((L + 31) / 32) {
+#define IRC_ATTB(NJ)                                                                             \
+  case NJ:                                                                                       \
+    hipLaunchKernelGGL(enc::attention_mfma_kernel<NJ>, grid, dim3(256), 0, st,                   \
+                       (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B, (int)H,   \
+                       (int)heads, sc, (unsigned char*)nullptr, (unsigned char*)nullptr,         \
+                       (int64_t)0, (int)L);                                                      \
+    break;
+      IRC_ATTB(1) IRC_ATTB(2) IRC_ATTB(3) IRC_ATTB(4)
+#undef IRC_ATTB
     }
     // algorithmic bytes: QKV read once + ctx written
     prof_end("attention", st, (double)B * L * (3 * H + H) * 2.0);

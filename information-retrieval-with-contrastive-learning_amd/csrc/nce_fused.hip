@@ -252,29 +252,36 @@ __global__ __launch_bounds__(NT) void fwd_partial_kernel(Args a) {
   }
 }
 
-// lse[r], loss_row[r] for the computed rows: partials combined in chunk order.
-__global__ void fwd_combine_kernel(Args a, float* __restrict__ lse, float* __restrict__ loss_row) {
-  const int lr = blockIdx.x * blockDim.x + threadIdx.x;
+// lse[r], loss_row[r] for the computed rows: one wave per row, lane l combining
+// chunks l, l + 64, ... in order, then a fixed xor tree (deterministic).
+__global__ __launch_bounds__(256) void fwd_combine_kernel(Args a, float* __restrict__ lse,
+                                                          float* __restrict__ loss_row) {
+  const int lr = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (lr >= (full_range(a) ? 2 * a.N : local_rows(a))) return;
   const int r = full_range(a) ? lr : abs_of(a, lr);
   const int n2 = 2 * a.N;
-  const int chunks_q = a.K > 0 ? a.chunks_q : 0;
-  float m = -INFINITY;
-  for (int c = 0; c < a.chunks_b; ++c) m = fmaxf(m, a.part_b[(int64_t)c * n2 + r].x);
+  const int cb = a.chunks_b, cq = a.K > 0 ? a.chunks_q : 0;
   const int n = r % a.N;
-  for (int c = 0; c < chunks_q; ++c) m = fmaxf(m, a.part_q[(int64_t)c * a.N + n].x);
+  auto part = [&](int c) {
+    return c < cb ? a.part_b[(int64_t)c * n2 + r] : a.part_q[(int64_t)(c - cb) * a.N + n];
+  };
+  float m = -INFINITY;
+  for (int c = lane; c < cb + cq; c += 64) m = fmaxf(m, part(c).x);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
   float s = 0.f;
-  for (int c = 0; c < a.chunks_b; ++c) {
-    const float2 p = a.part_b[(int64_t)c * n2 + r];
+  for (int c = lane; c < cb + cq; c += 64) {
+    const float2 p = part(c);
     if (p.x != -INFINITY) s += p.y * __expf(p.x - m);
   }
-  for (int c = 0; c < chunks_q; ++c) {
-    const float2 p = a.part_q[(int64_t)c * a.N + n];
-    if (p.x != -INFINITY) s += p.y * __expf(p.x - m);
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) {
+    const float l = m + logf(s);
+    lse[r] = l;
+    loss_row[r] = l - a.pos[r];
   }
-  const float l = m + logf(s);
-  lse[r] = l;
-  loss_row[r] = l - a.pos[r];
 }
 
 // ---- backward: dF partial of one (128-row group, column chunk) -----------------
@@ -375,10 +382,18 @@ __global__ void bwd_reduce_kernel(const float* __restrict__ dpart, int rows, int
   const int row = (int)(e4 * 4 / D);
   const f32x4* p = reinterpret_cast<const f32x4*>(dpart) + e4;
   const int64_t cs = (int64_t)rows * D / 4;
-  f32x4 s = (f32x4)0.f;
-  for (int c = 0; c < chunks_b; ++c) s += p[c * cs];
-  if (row < q_rows)
-    for (int c = 0; c < chunks_q; ++c) s += p[(chunks_b + c) * cs];
+  const int nc = chunks_b + (row < q_rows ? chunks_q : 0);
+  // 8 independent sums (chunk c into sum c % 8, in chunk order), then added in a
+  // fixed order: deterministic, and 8 loads in flight per thread
+  f32x4 s8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s8[j] = (f32x4)0.f;
+  int c = 0;
+  for (; c + 8 <= nc; c += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s8[j] += p[(c + j) * cs];
+  for (int j = 0; c + j < nc; ++j) s8[j] += p[(c + j) * cs];
+  const f32x4 s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
   reinterpret_cast<f32x4*>(dF)[e4] = s;
 }
 
@@ -395,6 +410,7 @@ int pick_chunk(int64_t N, int64_t D, int64_t K, int64_t rows_b, int64_t rows_q, 
   const int64_t tb = (2 * N + 31) / 32, tq = (K + 31) / 32;
   const int64_t groups = ((rows_b + 127) / 128) * tb + ((rows_q + 127) / 128) * tq;
   int64_t c = (groups + 1023) / 1024;
+  if (c < 2) c = 2;  // >= 2 tiles per workgroup: the row block's loads amortised
   if (bwd) {
     const int64_t part1 = (rows_b * tb + rows_q * tq) * D * 4;
     const int64_t cb = (part1 + (48ll << 20) - 1) / (48ll << 20);
@@ -483,8 +499,8 @@ extern "C" int irc_nce_fused_fwd(const float* F, const float* queue, int64_t N, 
     IRC_NCEF(1) IRC_NCEF(2) IRC_NCEF(3) IRC_NCEF(4) IRC_NCEF(5) IRC_NCEF(6) IRC_NCEF(7) IRC_NCEF(8)
 #undef IRC_NCEF
   }
-  hipLaunchKernelGGL(ncef::fwd_combine_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
-                     st, a, lse, loss_row);
+  hipLaunchKernelGGL(ncef::fwd_combine_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st,
+                     a, lse, loss_row);
   prof_end("nce_fused", st, 2.0 * rows * D * (2.0 * N) + 2.0 * (rows / 2) * D * K);
   return check_launch("nce_fused_fwd");
 }

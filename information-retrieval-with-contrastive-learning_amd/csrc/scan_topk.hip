@@ -31,6 +31,13 @@
 #ifndef IRC_SCAN_SEL_STOP
 #define IRC_SCAN_SEL_STOP -1  // diagnostic builds: the final select returns at stage N
 #endif
+// 1: the DMA of tile it + NBUF is issued into tile it's ring slot as soon as every
+// wave holds tile it's A fragments in registers (one extra barrier), so NBUF tiles
+// are in flight during the MFMAs and the epilogue instead of NBUF - 1 (0: the
+// round-2 order, the next DMA at the top of each iteration).
+#ifndef IRC_SCAN_EARLY_ISSUE
+#define IRC_SCAN_EARLY_ISSUE 1
+#endif
 #ifndef IRC_SCAN_GENERAL_SELECT
 #define IRC_SCAN_GENERAL_SELECT 0  // A/B builds: 1 = region selects without select_fast
 #endif
@@ -50,9 +57,21 @@ __device__ uint64_t dbg_stamps[4][32];
       *p_ = t_;                                                                          \
     }                                                                                    \
   } while (0)
+// every block's start / end of the filter launch (LTOP or KEYS-with-threshold)
+__device__ uint64_t dbg_blk[2 * 8192];
+#define BLK_STAMP(i)                                                                     \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 8192 && (MODE == LTOP || thr != nullptr)) {     \
+      volatile uint64_t* p_ = &dbg_blk[2 * blockIdx.x + (i)];                            \
+      *p_ = __builtin_amdgcn_s_memrealtime();                                            \
+    }                                                                                    \
+  } while (0)
 #else
 #define STAMP(slot, i) \
   do {                 \
+  } while (0)
+#define BLK_STAMP(i) \
+  do {               \
   } while (0)
 #endif
 
@@ -142,6 +161,7 @@ void scan_tile_kernel(
   const int q = qblock * (NQ * 32) + g * 32 + r32;
 
   STAMP(thr == nullptr ? 2 : 3, 0);
+  BLK_STAMP(0);
   const int ntiles_total = (NS + TD - 1) / TD;
   const int t_begin = worker * tiles_per_worker;
   int t_end = t_begin + tiles_per_worker;
@@ -180,8 +200,9 @@ void scan_tile_kernel(
     }
   };
 
+  constexpr int PRE = IRC_SCAN_EARLY_ISSUE ? G::NBUF : G::NBUF - 1;  // tiles issued up front
 #pragma unroll
-  for (int bb = 0; bb < G::NBUF - 1; ++bb)
+  for (int bb = 0; bb < PRE; ++bb)
     if (bb < my_tiles) issue_tile(t_begin + bb, bb);
 
   // Stationary B fragments: lane holds chunk 2c + h of its query row (of its
@@ -231,18 +252,23 @@ void scan_tile_kernel(
 
   for (int it = 0; it < my_tiles; ++it) {
     const int tile = t_begin + it;
-    if (it + G::NBUF - 1 < my_tiles) issue_tile(tile + G::NBUF - 1, (it + G::NBUF - 1) % G::NBUF);
+    if (!IRC_SCAN_EARLY_ISSUE && it + G::NBUF - 1 < my_tiles)
+      issue_tile(tile + G::NBUF - 1, (it + G::NBUF - 1) % G::NBUF);
     const int after = my_tiles - 1 - it;
     const int ahead = after < G::NBUF - 1 ? after : G::NBUF - 1;
+    // survivor stores younger than tile it's DMA: those of the iterations after
+    // the one that issued it (PRE of them)
     int extra = 0;
 #pragma unroll
-    for (int t = 0; t < G::NBUF - 1; ++t) extra += (int)((nst_hist >> (8 * t)) & 0xff);
+    for (int t = 0; t < PRE; ++t) extra += (int)((nst_hist >> (8 * t)) & 0xff);
     extra = extra < 15 ? extra : 15;  // smaller = safe
     wait_vmcnt_n(__builtin_amdgcn_readfirstlane(ahead == 0 ? 0 : ahead * PW + extra));
     wg_barrier();  // every wave's share of the tile has landed
 
 #ifdef IRC_SCAN_DMA_ONLY  // diagnostic build: the corpus stream alone
     wg_barrier();
+    if (IRC_SCAN_EARLY_ISSUE && it + G::NBUF < my_tiles)
+      issue_tile(tile + G::NBUF, it % G::NBUF);
     continue;
 #endif
     const char* tb = smem + (it % G::NBUF) * G::TILE_BYTES + kh * (D * EB / KS);
@@ -254,6 +280,12 @@ void scan_tile_kernel(
 #pragma unroll
       for (int c = 0; c < NCW; ++c)
         af[c] = *reinterpret_cast<const u16x8*>(tb + lo[c & 7] + 256 * (c >> 3));
+      if (IRC_SCAN_EARLY_ISSUE) {
+        // the slot is free once every wave's fragment reads have returned
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        wg_barrier();
+        if (it + G::NBUF < my_tiles) issue_tile(tile + G::NBUF, it % G::NBUF);
+      }
 #pragma unroll
       for (int c = 0; c < NCW; ++c) {
         if constexpr (EB == 2) {
@@ -373,7 +405,7 @@ void scan_tile_kernel(
 #pragma unroll
       for (int jj = 0; jj < JPW; ++jj) pm |= (uint32_t)(!(fin[jj] < ltf)) << jj;
       while (__ballot(pm != 0)) {
-#ifdef IRC_SCAN_STAMPS  // diagnostic: LTOP rounds (wave 0 of blocks < 256)
+#if defined(IRC_SCAN_STAMPS) && !defined(IRC_SCAN_NO_ROUNDS)  // diagnostic: LTOP rounds (wave 0 of blocks < 256)
         if (wave == 0 && lane == 0 && blockIdx.x < 256)
           atomicAdd((unsigned long long*)&dbg_stamps[3][28], 1ull);
 #endif
@@ -423,7 +455,10 @@ void scan_tile_kernel(
       }
     }
     nst_hist = (nst_hist << 8) | (uint64_t)(nst < 255 ? nst : 255);
-    wg_barrier();  // all reads of this buffer (and of xbuf) done before reuse
+    // all reads of this buffer (and of xbuf) done before reuse; with the early issue
+    // the slot was released above and the next iteration's two barriers precede any
+    // xbuf write
+    if (!IRC_SCAN_EARLY_ISSUE) wg_barrier();
   }
 
   if (MODE == LTOP) {
@@ -437,6 +472,7 @@ void scan_tile_kernel(
       dst[1] = (u64x2){lt2, lt3};
     }
     STAMP(3, 1);
+    BLK_STAMP(1);
     return;
   }
   if (MODE != SCORES) {  // flush the shift buffer (newest first; order is irrelevant)
@@ -448,6 +484,7 @@ void scan_tile_kernel(
   if (MODE != SCORES && q < Qpad)
     counts[((int64_t)worker * Qpad + q) * (2 * KS) + slice] = nsurv;
   STAMP(thr == nullptr ? 2 : 3, 1);
+  BLK_STAMP(1);
 }
 
 // ----------------------------------------------------------------- selection
@@ -2100,6 +2137,20 @@ extern "C" int irc_scan_dbg_stamps(uint64_t* out /* [4][32] */) {
 #ifdef IRC_SCAN_STAMPS
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(dbg_stamps), sizeof(dbg_stamps)) == hipSuccess ? 0 : -1;
+#else
+  (void)out;
+  return -1;
+#endif
+}
+
+// Diagnostic builds only: per-block start / end stamps of the last filter launch
+// (out: 2 * 8192 uint64, s_memrealtime ticks at 100 MHz; zeroed after the copy).
+extern "C" int irc_scan_dbg_blocks(uint64_t* out) {
+#ifdef IRC_SCAN_STAMPS
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(dbg_blk), sizeof(dbg_blk)) != hipSuccess) return -1;
+  static uint64_t zero[2 * 8192];
+  return hipMemcpyToSymbol(HIP_SYMBOL(dbg_blk), zero, sizeof(dbg_blk)) == hipSuccess ? 0 : -1;
 #else
   (void)out;
   return -1;

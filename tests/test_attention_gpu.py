@@ -2,8 +2,9 @@
 in eval mode (modeling_bert, reached from contrastive_module.py:39):
 softmax(Q K^T / sqrt(dh) + (1 - mask) * finfo.min) V over the fused [B*L, 3H] QKV rows.
 
-bf16 with head dim 64 and L % 32 == 0 (L <= 128) runs the MFMA kernel; other
-shapes / fp32 run the VALU kernel.  Tolerance: bf16 inputs and bf16-rounded
+bf16 with head dim 64 and L <= 128 runs the MFMA kernel (L not a multiple of 32,
+e.g. a joint-padded batch's L = 72: clamped key rows with a pad bias, zero V rows,
+query rows past L never stored); other shapes / fp32 run the VALU kernel.  Tolerance: bf16 inputs and bf16-rounded
 probabilities -> 2e-2 absolute on O(1) outputs; fp32 -> 1e-5.
 """
 import pytest
@@ -33,7 +34,7 @@ def _case(B, L, H, heads, dtype, seed, all_masked_row=False):
     return qkv, mask
 
 
-@pytest.mark.parametrize("L", [32, 64, 96, 128])
+@pytest.mark.parametrize("L", [1, 17, 32, 40, 64, 72, 96, 100, 128])
 def test_attention_mfma_bf16(gpu, L):
     from irc_amd import ops
 

@@ -184,14 +184,15 @@ def test_layernorm_mx_equals_quantised_layernorm(gpu, H):
     assert torch.equal(ym.codes, ref.codes) and torch.equal(ym.scales, ref.scales)
 
 
-def test_attention_mx_equals_quantised_attention(gpu):
+@pytest.mark.parametrize("L", [64, 72, 17])
+def test_attention_mx_equals_quantised_attention(gpu, L):
     from irc_amd import ops
 
-    g = torch.Generator().manual_seed(17)
-    B, L, H, heads = 9, 64, 768, 12
+    g = torch.Generator().manual_seed(17 + L)
+    B, H, heads = 9, 768, 12
     qkv = torch.randn(B * L, 3 * H, generator=g).bfloat16().to(gpu)
     mask = torch.ones(B, L, dtype=torch.int64)
-    mask[3, 40:] = 0
+    mask[3, min(40, L - 1):] = 0
     mask[5, 1:] = 0
     mask = mask.to(gpu)
     ctx = ops.attention(qkv, mask, B, L, H, heads)
