@@ -273,6 +273,19 @@ __device__ __forceinline__ void stage_tile(const PArgs& g, const unsigned short*
   stage_half<BK_>(B, g.ldb, n0 + 128 * grp, g.N, k0, base + 2 * SA + grp * SB, wq, lane);
 }
 
+// 1: group 1 issues its half of K-tile kt + 1 at the start of its M section of
+// K-tile kt - 1 instead of its L section of K-tile kt (the buffer is free from the
+// barrier between them), so its DMA, like group 0's, has a whole K-tile of sections
+// to land before group 0 reads it; 0: the round-2 order (one section); 1: the MX
+// kernel only (default); 2: every kernel.  The per-lane DMA addresses are then
+// re-derived per call (kept live across the M section they spill 12-28 VGPRs).
+// Measured on MI355X (profiles/r03_gemm_j_*): MX qkv / FFN1 (MX out) / FFN2 101 /
+// 184 / 119 us against 110 / 194 / 135; the bf16 forms gain nothing on qkv / FFN2
+// and lose on FFN1 + GELU (237 vs 200 us) and 4096^3 (127 vs 108 us).
+#ifndef IRC_PP_G1_EARLY
+#define IRC_PP_G1_EARLY 1
+#endif
+
 // The ping-pong K loop of one 256x256 output tile over nk K-tiles from kbeg.
 // K-tile kt lives in LDS buffer (kt + par) & 1, the buffers `pitch` bytes apart.
 // staged: K-tile 0's DMA was already issued by the caller.  pub != null: thread 0
@@ -287,6 +300,8 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
                                          f32x4 (&acc)[8][4], int grp, int wq, int lane, int* pub,
                                          int pub_val) {
   constexpr int SA = slot_bytes(AK), SB = slot_bytes(BK_);
+  constexpr bool G1E = IRC_PP_G1_EARLY != 0 && (F8 == 2 || IRC_PP_G1_EARLY == 2);
+  constexpr bool RD = F8 == 2 || G1E;  // DMA addresses re-derived per call (register budget)
   const int wn = wq;  // 64-column slab of the tile
   const int bh = wn >> 1, bcol = 64 * (wn & 1);
 #pragma unroll
@@ -299,21 +314,31 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
     if constexpr (F8 == 2) stage_scales(g, m0, n0, kbeg / BK, lds + MX_SC_OFF + par * 2048, grp, wq, lane);
     wait_vmcnt<0>();
     wg_barrier();
-    if (grp == 1) wg_barrier();  // group 1 runs one section behind
+    if (grp == 1) {  // group 1 runs one section behind
+      if (G1E && nk > 1) {
+        // its half of K-tile 1 now: group 1 issues K-tile kt + 1 in its M section of
+        // kt - 1 (below), so its DMA has two sections to land, as group 0's has
+        stage_tile<AK, BK_, RD>(g, A, B, m0, n0, kbeg + BK, lds + (par ^ 1) * pitch, grp, wq, lane);
+        if constexpr (F8 == 2)
+          stage_scales(g, m0, n0, kbeg / BK + 1, lds + MX_SC_OFF + (par ^ 1) * 2048, grp, wq, lane);
+      }
+      wg_barrier();
+    }
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = (kt + par) & 1;
-      // ---- L section: next tile's DMA, this tile's fragments
+      // ---- L section: next tile's DMA (group 0; group 1 with IRC_PP_G1_EARLY = 0),
+      // this tile's fragments
 #ifdef IRC_PP_DIAG_NODMA  // diagnostic build: only K-tile 0 is loaded (MFMA + LDS-read rate)
       if (kt + 1 < nk && kt < 0) {
 #else
-      if (kt + 1 < nk) {
+      if (kt + 1 < nk && (grp == 0 || !G1E)) {
 #endif
 #ifdef IRC_MX_NO_REDERIVE  // A/B build: DMA addresses kept live as in the bf16 loop
         stage_tile<AK, BK_, false>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch,
                                    grp, wq, lane);
 #else
-        stage_tile<AK, BK_, F8 == 2>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch,
-                                     grp, wq, lane);
+        stage_tile<AK, BK_, RD>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch,
+                                grp, wq, lane);
 #endif
         if constexpr (F8 == 2)
           stage_scales(g, m0, n0, kbeg / BK + kt + 1, lds + MX_SC_OFF + (cur ^ 1) * 2048, grp, wq,
@@ -356,6 +381,16 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
       if (grp == 1) wait_vmcnt<0>();  // group 0 reads this DMA in the next section
       wg_barrier();
       // ---- M section
+#ifndef IRC_PP_DIAG_NODMA
+      // group 1: its half of K-tile kt + 2 into this tile's buffer, which both groups
+      // finished reading at the barrier above
+      if (G1E && grp == 1 && kt + 2 < nk) {
+        stage_tile<AK, BK_, RD>(g, A, B, m0, n0, kbeg + (kt + 2) * BK, lds + cur * pitch, grp, wq,
+                                lane);
+        if constexpr (F8 == 2)
+          stage_scales(g, m0, n0, kbeg / BK + kt + 2, lds + MX_SC_OFF + cur * 2048, grp, wq, lane);
+      }
+#endif
       __builtin_amdgcn_s_setprio(1);
       if constexpr (F8 == 2) {
 #pragma unroll

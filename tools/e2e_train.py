@@ -6,7 +6,7 @@ before moving tokenisation to the GPU.
 
     python tools/e2e_train.py [--steps 30] [--workers 6]
 
-Synthetic corpus: 20k documents x 3-8 sentences of 8-30 words; each word is
+Synthetic corpus: 20k documents x 3-8 sentences of 8-26 words (--max-words); each word is
 1-3 syllables from a vocabulary that holds the syllables as words and as
 '##' continuation pieces, so WordPiece does real greedy longest-match splits
 (the offline image has no bert-base-uncased vocab)."""
@@ -44,13 +44,14 @@ def make_vocab(path, size=30522):
     return syl
 
 
-def make_corpus(path, syl, n_docs=20000):
+def make_corpus(path, syl, n_docs=20000, max_words=20):
     rng = np.random.default_rng(1)
     docs = []
     for _ in range(n_docs):
         sents = []
         for _ in range(rng.integers(3, 9)):
-            words = ["".join(rng.choice(syl, rng.integers(1, 4))) for _ in range(rng.integers(8, 31))]
+            words = ["".join(rng.choice(syl, rng.integers(1, 4)))
+                     for _ in range(rng.integers(8, max_words + 1))]
             sents.append(" ".join(words).capitalize() + ".")
         docs.append(sents)
     with open(path, "wb") as f:
@@ -63,11 +64,14 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--workers", type=int, default=6)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--max-words", type=int, default=26,
+                    help="words per sentence 8..max (26: a joint batch of 512 pads to L ~ 64, the C2 "
+                         "bench sequence length; 20: L ~ 52; 30: L ~ 72)")
     args = ap.parse_args()
     tmp = tempfile.mkdtemp()
     vocab = os.path.join(tmp, "vocab.txt")
     syl = make_vocab(vocab)
-    docs = make_corpus(os.path.join(tmp, "docs_sentence.pkl"), syl)
+    docs = make_corpus(os.path.join(tmp, "docs_sentence.pkl"), syl, max_words=args.max_words)
 
     from irc_amd.tokenizer import load_tokenizer
 

@@ -3,12 +3,20 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_attention_gpu.py tests/test_fp8_encoder_gpu.py \
+timeout -k 10 900 python -u -m pytest tests/test_gemm_gpu.py tests/test_attention_gpu.py tests/test_fp8_encoder_gpu.py \
   tests/test_configs_gpu.py tests/test_model_gpu.py tests/test_train_gpu.py tests/test_main_gpu.py \
   tests/test_oracle_golden.py -m gpu -q -rfE -s --timeout 300 --timeout-method thread > gpurun_out/pytest_j.log 2>&1
 prc=$?
 grep -E "passed|failed|^FAILED|C5 fp8|fused|Error" gpurun_out/pytest_j.log | tail -30
 [ $prc -eq 0 ] || [ $prc -eq 1 ] || exit $prc
+V=information-retrieval-with-contrastive-learning_amd/irc_amd/lib/variants
+for v in base g1off; do
+  if [ $v = base ]; then L=; else L=$V/$v.so; fi
+  echo "== gemm $v"
+  IRC_LIB_PATH=$L timeout -k 10 200 python tools/gemm_bench.py --only qkv,attn_out+res,ffn1+gelu,ffn2+res,square4k > gpurun_out/gemm_j_$v.txt 2>&1 || { tail -3 gpurun_out/gemm_j_$v.txt; exit 1; }
+  IRC_LIB_PATH=$L timeout -k 10 200 python tools/gemm_bench.py --mx >> gpurun_out/gemm_j_$v.txt 2>&1 || { tail -3 gpurun_out/gemm_j_$v.txt; exit 1; }
+  grep -v amdgpu gpurun_out/gemm_j_$v.txt
+done
 timeout -k 10 200 python tools/nce_bench.py > gpurun_out/nce_j.txt 2>&1 || { tail -3 gpurun_out/nce_j.txt; exit 1; }
 grep -v amdgpu gpurun_out/nce_j.txt
 timeout -k 10 300 python tools/encode_bench.py > gpurun_out/encode_j.txt 2>&1 || { tail -3 gpurun_out/encode_j.txt; exit 1; }
