@@ -171,7 +171,8 @@ def _live_events(lib, name, fn, n):
 
 def run_train(args, rank, world, dev, weights="bf16", cfg=None):
     """weights "fp8": config C5 -- the frozen encoder's nn.Linear layers on e4m3
-    (irc_gemm_fp8, per-channel weight / per-token input scales); same step.
+    (irc_gemm_mx: MX-fp8, e4m3 codes with one E8M0 scale per 32 k, inputs quantised by
+    their producing LayerNorm / attention / GELU epilogues); same step.
     cfg: c2_config() (default) or c4_config() (BERT-large encoder)."""
     from irc_amd import _lib
     from src.model import build_model, get_optimizer
@@ -732,7 +733,8 @@ def main():
         if train8 is not None:
             line["train_fp8"] = dict(train8, workload=(
                 "C5: fp8 (e4m3) frozen-encoder weights, d=768: the C2 step with every BERT-base "
-                "nn.Linear on irc_gemm_fp8 (per-channel weight / per-token input scales)"))
+                "nn.Linear on irc_gemm_mx (MX-fp8: e4m3 codes, one E8M0 scale per 32 k; inputs "
+                "quantised by their producing LayerNorm / attention / GELU epilogues)"))
         if scan is not None:
             line["retrieval"] = scan
         if scan_c3 is not None:

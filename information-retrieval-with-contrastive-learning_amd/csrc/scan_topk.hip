@@ -78,15 +78,19 @@ __device__ uint64_t dbg_blk[2 * 8192];
 // Tile geometry for embeddings of D elements of EB bytes (2: bf16, 1: fp8 e4m3).
 // The chunk XOR is confined to the low bits that divide a k-slice's chunk count,
 // so the per-slice read offsets stay base + immediate.
-template <int D, int EB = 2>
+// KSX = k-slices (waves sharing one 32-query group): 1 for D <= 512, 2 above, and 4
+// for the single-pass scan of at most 64 queries at D = 768 / 1024 (LTOP_KS4).
+template <int D, int EB = 2, int KSX = (D > 512 ? 2 : 1)>
 struct Geo {
-  static constexpr int KS = D > 512 ? 2 : 1;
+  static constexpr int KS = KSX;
   static constexpr int CH = D * EB / 16;             // 16-byte chunks per row
   static constexpr int LOWBIT = (CH / KS) & (-(CH / KS));
   static constexpr int SWZ = (LOWBIT < 16 ? LOWBIT : 16) - 1;
   static constexpr int TILE_BYTES = TD * D * EB;
   static constexpr int GLDS_PER_TILE = TD * CH / 64;  // wave-instructions per tile
-  static constexpr int XBUF_BYTES = (D > 512) ? 4 * 4096 : 0;  // KS=2 exchange (NQ <= 4)
+  // k-slice exchange: KS = 2, NQ <= 4 (8 floats per lane per wave); KS = 4, NQ <= 2
+  // (the butterfly's 8-float rounds)
+  static constexpr int XBUF_BYTES = (KSX > 1) ? 4 * 4096 : 0;
   // ring depth: 3 x 48 KB for bf16 D=768; fp8 tiles are half as large, so the
   // ring goes deeper (same bytes in flight)
   static constexpr int NBMAX = EB == 1 ? 5 : 3;
@@ -139,8 +143,8 @@ void scan_tile_kernel(
     int Qpad, int GY, int NS, int stride, int tiles_per_worker, uint32_t idx_base,
     const uint64_t* __restrict__ thr, uint64_t* __restrict__ keys, uint32_t* __restrict__ counts,
     int64_t cap, float* __restrict__ scores_out) {
-  using G = Geo<D, EB>;
-  static_assert(G::KS == KS, "k-slices");
+  using G = Geo<D, EB, KS>;
+  static_assert(KS != 4 || (MODE == LTOP && NQ <= 2), "four k-slices: single-pass scan only");
   constexpr int NW = NQ * KS;
   constexpr int KKW = G::KK / KS;  // k-steps per wave
   constexpr int NCW = KKW * EB / 2;  // 16-byte fragment chunks per wave per tile
@@ -305,7 +309,47 @@ void scan_tile_kernel(
     wg_barrier();
     continue;
 #endif
-    if (KS == 2) {
+    if (KS == 4) {
+      // Butterfly reduce-scatter of the four k-slice partial sums: round 1 with
+      // wave kh ^ 2 (keep half kh >> 1 of the 16 registers, send the other), round 2
+      // with wave kh ^ 1 (keep quarter kh & 1 of that half).  Every wave's registers
+      // end as fl(fl(s0 + s2) + fl(s1 + s3)) whatever its kh (fp32 addition is
+      // commutative), the order rescore_docs reproduces.  Round 2 writes into the
+      // slot this wave alone read in round 1, so it needs no barrier before it.
+      float* s1 = xbuf + ((g * 4 + kh) * 64 + lane) * 8;
+      float* s2 = xbuf + ((g * 4 + (kh ^ 2)) * 64 + lane) * 8;
+      float* s3 = xbuf + ((g * 4 + (kh ^ 3)) * 64 + lane) * 8;  // wave kh ^ 1's round-2 slot
+      f32x4 o0, o1, k0, k1;
+      if ((kh >> 1) == 0) {
+        o0 = (f32x4){acc[8], acc[9], acc[10], acc[11]};
+        o1 = (f32x4){acc[12], acc[13], acc[14], acc[15]};
+        k0 = (f32x4){acc[0], acc[1], acc[2], acc[3]};
+        k1 = (f32x4){acc[4], acc[5], acc[6], acc[7]};
+      } else {
+        o0 = (f32x4){acc[0], acc[1], acc[2], acc[3]};
+        o1 = (f32x4){acc[4], acc[5], acc[6], acc[7]};
+        k0 = (f32x4){acc[8], acc[9], acc[10], acc[11]};
+        k1 = (f32x4){acc[12], acc[13], acc[14], acc[15]};
+      }
+      reinterpret_cast<f32x4*>(s1)[0] = o0;
+      reinterpret_cast<f32x4*>(s1)[1] = o1;
+#ifndef IRC_SCAN_XCHG_NOWAIT
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the raw barrier does not wait
+#endif
+      wg_barrier();
+      k0 += reinterpret_cast<const f32x4*>(s2)[0];
+      k1 += reinterpret_cast<const f32x4*>(s2)[1];
+      const f32x4 keep = (kh & 1) ? k1 : k0;
+      reinterpret_cast<f32x4*>(s2)[0] = (kh & 1) ? k0 : k1;
+#ifndef IRC_SCAN_XCHG_NOWAIT
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+      wg_barrier();
+      const f32x4 fq = keep + reinterpret_cast<const f32x4*>(s3)[0];
+      // the finished quarter kh (rows of registers 4 kh .. 4 kh + 3) in registers 0-3
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = fq[e];
+    } else if (KS == 2) {
       // exchange: wave kh sends the half it does NOT finish, adds the partner's.
       float* xo = xbuf + ((g * 2 + kh) * 64 + lane) * 8;
       float* xi = xbuf + ((g * 2 + (kh ^ 1)) * 64 + lane) * 8;
@@ -347,6 +391,7 @@ void scan_tile_kernel(
       for (int jj = 0; jj < 8; ++jj) fin[jj] = acc[jj + 8];
       joff = 8;
     }
+    if (KS == 4) joff = 4 * kh;  // the exchange left quarter kh in registers 0-3
     // Survivors wait in a per-lane 4-key shift buffer and leave 4 at a time: a
     // store is older than the DMAs issued after it and vmcnt retires in order,
     // so every store episode delays a later tile's wait by its write-ack
@@ -462,9 +507,34 @@ void scan_tile_kernel(
   }
 
   if (MODE == LTOP) {
-    // dense lists: keys[((q * G_total + worker) * 2KS + slice) * 4 + i], cap = lists
-    // per query (G_total * 2KS); every list written, empty slots 0
-    if (q < Q) {
+    // dense lists: keys[((q * G_total + worker) * NL + slice) * 4 + i], cap = lists
+    // per query (G_total * NL); every list written, empty slots 0.  KS = 4: the two
+    // half-lanes' lists of one (query, k-slice) are merged first (top 4 of 8; every
+    // doc either list dropped is below the merged last key), so NL = 4 as for KS = 2
+    // and each list covers tile rows [8 kh, 8 kh + 8).
+    if constexpr (KS == 4) {
+      const uint64_t p0 = __shfl_xor(lt0, 32, 64), p1 = __shfl_xor(lt1, 32, 64);
+      const uint64_t p2 = __shfl_xor(lt2, 32, 64), p3 = __shfl_xor(lt3, 32, 64);
+      const uint64_t pv[4] = {p0, p1, p2, p3};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint64_t key = pv[i];
+        if (key > lt3) {
+          lt3 = key;
+          uint64_t t;
+          if (lt3 > lt2) { t = lt2; lt2 = lt3; lt3 = t; }
+          if (lt2 > lt1) { t = lt1; lt1 = lt2; lt2 = t; }
+          if (lt1 > lt0) { t = lt0; lt0 = lt1; lt1 = t; }
+        }
+      }
+      if (q < Q && h == 0) {
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+        u64x2* dst = reinterpret_cast<u64x2*>(
+            keys + (((int64_t)q * cap + (int64_t)worker * 4 + kh) * LT_M));
+        dst[0] = (u64x2){lt0, lt1};
+        dst[1] = (u64x2){lt2, lt3};
+      }
+    } else if (q < Q) {
       typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
       u64x2* dst = reinterpret_cast<u64x2*>(
           keys + (((int64_t)q * cap + (int64_t)worker * (2 * KS) + slice) * LT_M));
@@ -1473,12 +1543,12 @@ __device__ uint64_t dense_kth(const uint64_t (&v)[U], const uint64_t* xk, uint32
 // k-slice partial sums added -- bit-identical (an MFMA row's result does not
 // depend on the other rows).  Lane (r32, h) returns rows (j & 3) + 8 (j >> 2) + 4 h
 // of column 0 in acc[j] (lanes 0 and 32 hold the query's column).
-template <int D, int EB>
+template <int D, int EB, int KS>
 __device__ __forceinline__ f32x16 rescore_docs(const unsigned char* qlds,
                                                const unsigned char* __restrict__ docs,
                                                const uint32_t* dl, int n, int lane) {
-  using G = Geo<D, EB>;
-  constexpr int KS = G::KS;
+  using G = Geo<D, EB, KS>;
+  f32x16 part[KS == 4 ? 4 : 1];
   constexpr int NCW = (G::KK / KS) * EB / 2;
   const int r32 = lane & 31, h = lane >> 5;
   const bool live = r32 < n;
@@ -1508,16 +1578,36 @@ __device__ __forceinline__ f32x16 rescore_docs(const unsigned char* qlds,
         acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a2[1], b2[1], acc, 0, 0, 0);
       }
     }
-    if (kh == 0) tot = acc;
-    else tot += acc;  // the filter's exchange: fl(half 0 + half 1), commutative
+    if constexpr (KS == 4) {
+      part[kh] = acc;
+    } else {
+      if (kh == 0) tot = acc;
+      else tot += acc;  // the filter's exchange: fl(half 0 + half 1), commutative
+    }
   }
+  if constexpr (KS == 4) tot = (part[0] + part[2]) + (part[1] + part[3]);  // the butterfly's order
   return tot;
 }
 
-template <int D, int EB>
+// Tile rows covered by list `sl` of a worker (slice kh * 2 + h for KS <= 2: rows
+// (j & 3) + 8 (j >> 2) + 4 h, j in kh's share of the 16 registers; KS = 4: the merged
+// half-lane lists, rows [8 sl, 8 sl + 8)).
+template <int KS>
+__device__ __forceinline__ uint32_t list_rows(int sl) {
+  if constexpr (KS == 4) {
+    return 0xFFu << (8 * sl);
+  } else {
+    const int kh = sl >> 1, hh = sl & 1;
+    constexpr int JPW = 16 / KS;
+    uint32_t rows = 0;
+    for (int j = kh * JPW; j < (kh + 1) * JPW; ++j) rows |= 1u << ((j & 3) + 8 * (j >> 2) + 4 * hh);
+    return rows;
+  }
+}
+
+template <int D, int EB, int KS>
 __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
-  using G = Geo<D, EB>;
-  constexpr int NSL = 2 * G::KS;
+  constexpr int NSL = KS == 4 ? 4 : 2 * KS;  // lists per worker
   constexpr int U = SEL_STAGE / SEL_NT;
   constexpr int MAXW = SEL_STAGE / (LT_M * 2);  // workers (NSL >= 2)
   __shared__ uint32_t hbuf[2 * SEL_NW * 256];
@@ -1556,13 +1646,8 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int i = tid + u * SEL_NT;
-    if ((i & (LT_M - 1)) == LT_M - 1 && i < M4 && v[u] != 0 && v[u] >= kth) {
-      const int sl = (i / LT_M) % NSL, kh = sl >> 1, hh = sl & 1;
-      constexpr int JPW = 16 / G::KS;
-      uint32_t rows = 0;
-      for (int j = kh * JPW; j < (kh + 1) * JPW; ++j) rows |= 1u << ((j & 3) + 8 * (j >> 2) + 4 * hh);
-      atomicOr(&vflag[(i / LT_M) / NSL], rows);
-    }
+    if ((i & (LT_M - 1)) == LT_M - 1 && i < M4 && v[u] != 0 && v[u] >= kth)
+      atomicOr(&vflag[(i / LT_M) / NSL], list_rows<KS>((i / LT_M) % NSL));
   }
   __syncthreads();
   for (int w = tid; w < nworkers; w += SEL_NT)
@@ -1583,12 +1668,8 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // truncated lists: replaced by the rescan of their rows
       const int i = tid + u * SEL_NT;
-      if (i < M4 && vflag[(i / LT_M) / NSL] != 0) {
-        const int sl = (i / LT_M) % NSL, kh = sl >> 1, hh = sl & 1;
-        constexpr int JPW = 16 / G::KS;
-        const int j0 = kh * JPW;  // any row of the slice identifies it
-        if ((vflag[(i / LT_M) / NSL] >> ((j0 & 3) + 8 * (j0 >> 2) + 4 * hh)) & 1u) v[u] = 0;
-      }
+      // the lists' row sets are disjoint: any overlap with the flags marks this one
+      if (i < M4 && (vflag[(i / LT_M) / NSL] & list_rows<KS>((i / LT_M) % NSL)) != 0) v[u] = 0;
     }
     uint64_t thr = kth;
     const int ntiles = (a.NS + TD - 1) / TD;
@@ -1645,7 +1726,7 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
         const int c = c0 + wave * TD;
         if (c < nd) {
           const int n = nd - c < TD ? nd - c : TD;
-          const f32x16 sc = rescore_docs<D, EB>(qlds, a.docs, dl + c, n, lane);
+          const f32x16 sc = rescore_docs<D, EB, KS>(qlds, a.docs, dl + c, n, lane);
           if ((lane & 31) == 0) {
             const int h = lane >> 5;
             uint64_t kk[16];
@@ -1808,9 +1889,22 @@ static int pick_nq(int64_t D, int64_t Q) {
   return p;
 }
 
-template <int D, int EB>
+template <int D, int EB, int KS = (D > 512 ? 2 : 1)>
 static size_t tile_lds_bytes() {
-  return (size_t)Geo<D, EB>::NBUF * Geo<D, EB>::TILE_BYTES + Geo<D, EB>::XBUF_BYTES;
+  using G = Geo<D, EB, KS>;
+  return (size_t)G::NBUF * G::TILE_BYTES + G::XBUF_BYTES;
+}
+
+// IRC_SCAN_LTOP_KS4=1 selects four k-slices in the single-pass scan (read once; off by default).
+// Four k-slices (D = 768 / 1024 bf16, Q <= 64) give each wave half the DMA issue,
+// MFMA chain and list insertions of a tile, and put two waves on every SIMD at
+// Q > 32 (C3 shard measurements in DESIGN.md §4).
+static bool ltop_ks4() {
+  static const bool v = [] {
+    const char* e = getenv("IRC_SCAN_LTOP_KS4");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 template <int EB>
@@ -1928,6 +2022,12 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
            k <= SEL_NT;
   if (p.ltop) {
     p.two_phase = false;
+    // four k-slices: same LDS (ring + a 16 KB exchange) and the same 4 lists per
+    // worker and query (the half-lane lists are merged), so g_f / ls stand
+    if (eb == 2 && (D == 768 || D == 1024) && p.nq <= 2 && ltop_ks4()) {
+      p.ks = 4;
+      p.nw = p.nq * 4;
+    }
     const size_t lb = (size_t)p.qpad * p.ls * LT_M * 8;
     if (lb > key_bytes) key_bytes = lb;
   }
@@ -1940,13 +2040,12 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   return p;
 }
 
-template <int D, int NQ, int MODE, int EB>
+template <int D, int NQ, int MODE, int EB, int KS = (D > 512 ? 2 : 1)>
 static void launch_tile(const Plan& p, int g, const unsigned char* qs, const unsigned char* docs,
                         int Q, int64_t NS, int64_t stride, int tpw, uint32_t idx_base,
                         const uint64_t* thr, uint64_t* keys, uint32_t* counts, int64_t cap,
                         float* scores, hipStream_t st) {
-  const size_t lds = tile_lds_bytes<D, EB>();
-  constexpr int KS = D > 512 ? 2 : 1;
+  const size_t lds = tile_lds_bytes<D, EB, KS>();
   static_assert(NQ * KS <= 8 || KS == 1, "wave budget");
   hipLaunchKernelGGL((scan_tile_kernel<D, NQ, KS, MODE, EB>), dim3(g * p.gy), dim3(NQ * KS * 64),
                      lds, st, qs, docs, Q, p.qpad, p.gy, (int)NS, (int)stride, tpw, idx_base, thr,
@@ -1961,7 +2060,12 @@ static int dispatch_tile_eb(int64_t D, const Plan& p, int g, const unsigned char
 #define IRC_SCAN_ARGS p, g, qs, docs, Q, NS, stride, tpw, idx_base, thr, keys, counts, cap, scores, st
 #define IRC_SCAN_CASE(DD)                                              \
   case DD:                                                             \
-    if (p.nq == 1) launch_tile<DD, 1, MODE, EB>(IRC_SCAN_ARGS);        \
+    if (p.ks == 4) {                                                   \
+      if constexpr (MODE == LTOP && EB == 2 && (DD == 768 || DD == 1024)) { \
+        if (p.nq == 1) launch_tile<DD, 1, MODE, EB, 4>(IRC_SCAN_ARGS); \
+        else launch_tile<DD, 2, MODE, EB, 4>(IRC_SCAN_ARGS);           \
+      }                                                                \
+    } else if (p.nq == 1) launch_tile<DD, 1, MODE, EB>(IRC_SCAN_ARGS); \
     else if (p.nq == 2) launch_tile<DD, 2, MODE, EB>(IRC_SCAN_ARGS);   \
     else if (p.nq == 4) launch_tile<DD, 4, MODE, EB>(IRC_SCAN_ARGS);   \
     else launch_tile<DD, (DD > 512 ? 4 : 8), MODE, EB>(IRC_SCAN_ARGS); \
@@ -1999,10 +2103,17 @@ static int dispatch_tile(int eb, int64_t D, const Plan& p, int g, const void* qs
 }
 
 template <int EB>
-static void launch_dense_eb(int64_t D, int Q, const DenseArgs& a, hipStream_t st) {
+static void launch_dense_eb(int64_t D, int ks, int Q, const DenseArgs& a, hipStream_t st) {
 #define IRC_DENSE_CASE(DD)                                                                 \
   case DD:                                                                                 \
-    hipLaunchKernelGGL((select_dense_kernel<DD, EB>), dim3((unsigned)Q), dim3(SEL_NT), 0, st, a); \
+    if constexpr (EB == 2 && (DD == 768 || DD == 1024)) {                                  \
+      if (ks == 4) {                                                                       \
+        hipLaunchKernelGGL((select_dense_kernel<DD, EB, 4>), dim3((unsigned)Q), dim3(SEL_NT), 0, st, a); \
+        break;                                                                             \
+      }                                                                                    \
+    }                                                                                      \
+    hipLaunchKernelGGL((select_dense_kernel<DD, EB, (DD > 512 ? 2 : 1)>), dim3((unsigned)Q), \
+                       dim3(SEL_NT), 0, st, a);                                            \
     break;
   switch (D) {
     IRC_DENSE_CASE(64)
@@ -2015,9 +2126,9 @@ static void launch_dense_eb(int64_t D, int Q, const DenseArgs& a, hipStream_t st
   }
 #undef IRC_DENSE_CASE
 }
-static void launch_dense(int eb, int64_t D, int Q, const DenseArgs& a, hipStream_t st) {
-  if (eb == 1) launch_dense_eb<1>(D, Q, a, st);
-  else launch_dense_eb<2>(D, Q, a, st);
+static void launch_dense(int eb, int64_t D, int ks, int Q, const DenseArgs& a, hipStream_t st) {
+  if (eb == 1) launch_dense_eb<1>(D, ks, Q, a, st);
+  else launch_dense_eb<2>(D, ks, Q, a, st);
 }
 
 static bool supported_d(int64_t D) {
@@ -2071,7 +2182,7 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
     DenseArgs da{keys, static_cast<const unsigned char*>(queries),
                  static_cast<const unsigned char*>(docs), p.ls, (int)N, p.tpw_f, base, (int)k, smul,
                  out_score, out_idx};
-    launch_dense(eb, D, (int)Q, da, st);
+    launch_dense(eb, D, p.ks, (int)Q, da, st);
     return check_launch("select_dense_kernel");
   }
   if (p.two_phase) {

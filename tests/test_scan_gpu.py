@@ -65,6 +65,13 @@ def test_golden_ties(gpu):
     (16, 60000, 128, 100, 0),   # two-phase (sampled threshold) path
     (64, 40000, 768, 1024, 3),  # maximum k
     (8, 20000, 128, 1, 0),      # k = 1
+    # single-pass scan with four k-slices (D = 768 / 1024, Q <= 64): one and two
+    # 32-query groups, merged half-lane lists, ragged tails, k up to 256
+    (1, 50011, 768, 100, 0),
+    (33, 40000, 768, 100, 2),
+    (64, 30007, 768, 256, 4),
+    (7, 20000, 1024, 200, 5),
+    (40, 25000, 1024, 64, 0),
     # Q >= 128: filter on the ping-pong GEMM kernel (regions = 256-doc tiles)
     (128, 60000, 768, 100, 0),  # two-phase, C2 dims
     (200, 30000, 256, 1024, 7),  # maximum k, ragged Q
