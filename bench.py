@@ -104,11 +104,12 @@ def _prof(lib, name):
     return tot.value / 1e3, cnt.value, work.value  # seconds, launches, work
 
 
-def _alg_bytes(lib, traffic):
-    """Algorithmic HBM bytes per bf16 GEMM launch of the last profiled pass (operands
-    read once, C written once, residual read once: gemm.hip gemm_alg_bytes) and the
-    PMC traffic's ratio to them (same dispatch set: the bench part's GEMM launches)."""
-    _, n, b = _prof(lib, "gemm_bf16_bytes")
+def _alg_bytes(lib, traffic, name="gemm_bf16_bytes"):
+    """Algorithmic HBM bytes per GEMM launch of the last profiled pass (operands
+    read once, C written once, residual read once: gemm.hip gemm_alg_bytes; MX-fp8:
+    codes + E8M0 scales, fp8_linear.hip irc_gemm_mx) and the PMC traffic's ratio to
+    them (same dispatch set: the bench part's GEMM launches)."""
+    _, n, b = _prof(lib, name)
     per = b / n if n else None
     return {"alg_bytes_per_launch": per,
             "traffic_over_alg": (traffic / per) if (traffic and per) else None}
@@ -239,7 +240,8 @@ def run_train(args, rank, world, dev, weights="bf16", cfg=None):
         torch.cuda.synchronize()
     lib.irc_prof_enable(0)
     g_s, g_n, g_flops = _prof(lib, gname)
-    g_bytes = _alg_bytes(lib, _pmc_traffic(gname) if weights == "bf16" else None)
+    ptag = gname if weights == "bf16" else "gemm_mx"
+    g_bytes = _alg_bytes(lib, _pmc_traffic(ptag), gname + "_bytes")
     flops_pair = 2 * model.bert_model.flops_per_sequence(TRAIN_L) + _lstm_flops_per_pair(cfg)
     pairs = TRAIN_B * args.steps * world
     achieved = g_flops / g_s / 1e12 if g_s > 0 else None
@@ -252,18 +254,19 @@ def run_train(args, rank, world, dev, weights="bf16", cfg=None):
         "step_tflops": pairs * flops_pair / dt / 1e12,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": gpeak,
                      "unit": "TFLOP/s", "frac": achieved / gpeak if achieved else None,
-                     "traffic": _pmc_traffic(gname) if weights == "bf16" else None,
-                     "traffic_source": _pmc_source(gname) if weights == "bf16" else None,
+                     "traffic": _pmc_traffic(ptag),
+                     "traffic_source": _pmc_source(ptag),
                      "kernel": ("bf16 GEMM kernels (gemm_big_kernel / gemm_pp_kernel / "
                                 "gemm_kernel; all GEMM launches of a single-stream pass of "
                                 "the same steps)") if weights == "bf16" else
-                               ("e4m3 GEMM (gemm_pp_kernel F8, v_mfma_scale_f32_16x16x128_"
-                                "f8f6f4) of the frozen encoder's linear layers, single-stream "
-                                "pass; the heads' bf16 GEMMs are not in this figure"),
+                               ("MX-fp8 GEMM (gemm_pp_kernel F8 = 2: e4m3 codes, E8M0 scales "
+                                "per 32 k applied by v_mfma_scale_f32_16x16x128_f8f6f4) of the "
+                                "frozen encoder's linear layers, single-stream pass; the heads' "
+                                "bf16 GEMMs are not in this figure"),
                      "launches_per_step": g_n / args.steps,
                      "gemm_ms_per_step": g_s * 1e3 / args.steps,
                      "alg_flops_per_step": g_flops / args.steps,
-                     **(g_bytes if weights == "bf16" else {}),
+                     **g_bytes,
                      "live_overlapped": {
                          "achieved": live_flops / live_s / 1e12 if live_s > 0 else None,
                          "note": "timed region itself: BERT GEMMs share the chip with the "

@@ -165,7 +165,15 @@ extern "C" int irc_gemm_mx(const void* A8, int64_t lda, const void* sa, int64_t 
   hipStream_t st = as_stream(stream);
   if (on) prof_begin(st);
   gpp::run_mx(epi, a, st);
-  if (on) prof_end("gemm_fp8", st, 2.0 * M * N * K);
+  if (on) {
+    prof_end("gemm_fp8", st, 2.0 * M * N * K);
+    // algorithmic bytes: both operands' codes and E8M0 scales once, C once (bf16, or
+    // MX codes + scales), the residual once
+    const double mn = (double)M * N;
+    prof_work("gemm_fp8_bytes", (double)(M + N) * K * (1.0 + 1.0 / 32) +
+                                    (cx ? mn * (1.0 + 1.0 / 32) : 2.0 * mn) +
+                                    (epi == 3 ? 2.0 * mn : 0.0));
+  }
   return check_launch("gemm_mx");
 }
 

@@ -144,7 +144,8 @@ void scan_tile_kernel(
     const uint64_t* __restrict__ thr, uint64_t* __restrict__ keys, uint32_t* __restrict__ counts,
     int64_t cap, float* __restrict__ scores_out) {
   using G = Geo<D, EB, KS>;
-  static_assert(KS != 4 || (MODE == LTOP && NQ <= 2), "four k-slices: single-pass scan only");
+  static_assert(KS != 4 || ((MODE == LTOP || MODE == SCORES) && NQ <= 2),
+                "four k-slices: the single-pass scan (and scan_scores on the same plan) only");
   constexpr int NW = NQ * KS;
   constexpr int KKW = G::KK / KS;  // k-steps per wave
   constexpr int NCW = KKW * EB / 2;  // 16-byte fragment chunks per wave per tile
@@ -363,6 +364,10 @@ void scan_tile_kernel(
       }
       reinterpret_cast<f32x4*>(xo)[0] = s0;
       reinterpret_cast<f32x4*>(xo)[1] = s1;
+      // the raw barrier does not wait for LDS writes: without this wait the partner
+      // wave can read the slot before the write lands (seen on MI355X with the
+      // four-slice exchange, whose round 2 also overwrites a slot another wave wrote)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       wg_barrier();
       const f32x4 t0 = reinterpret_cast<const f32x4*>(xi)[0];
       const f32x4 t1 = reinterpret_cast<const f32x4*>(xi)[1];
@@ -1895,14 +1900,16 @@ static size_t tile_lds_bytes() {
   return (size_t)G::NBUF * G::TILE_BYTES + G::XBUF_BYTES;
 }
 
-// IRC_SCAN_LTOP_KS4=1 selects four k-slices in the single-pass scan (read once; off by default).
-// Four k-slices (D = 768 / 1024 bf16, Q <= 64) give each wave half the DMA issue,
-// MFMA chain and list insertions of a tile, and put two waves on every SIMD at
-// Q > 32 (C3 shard measurements in DESIGN.md §4).
-static bool ltop_ks4() {
-  static const bool v = [] {
+// IRC_SCAN_LTOP_KS4 (read once): four k-slices in the single-pass scan for one
+// 32-query group (Q <= 32; default 1), also for two (Q <= 64; 2), or never (0).
+// Four slices give each wave half the DMA issue, MFMA chain and list insertions of a
+// tile.  C3 shard (250k x 768) filter at Q = 1 / 16 / 32: 78.5 / 85.0 / 86.0 ->
+// 74.3 / 79.7 / 79.1 us; C2: 38.7 / 43.3 / 44.4 -> 34.5 / 37.8 / 38.0 us.  Two groups
+// (8 waves): no gain (C3 Q = 33 / 64: 90.7 / 94.0 -> 90.2 / 95.6 us), so off there.
+static int ltop_ks4() {
+  static const int v = [] {
     const char* e = getenv("IRC_SCAN_LTOP_KS4");
-    return e && e[0] == '1';
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
@@ -2024,7 +2031,7 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
     p.two_phase = false;
     // four k-slices: same LDS (ring + a 16 KB exchange) and the same 4 lists per
     // worker and query (the half-lane lists are merged), so g_f / ls stand
-    if (eb == 2 && (D == 768 || D == 1024) && p.nq <= 2 && ltop_ks4()) {
+    if (eb == 2 && (D == 768 || D == 1024) && p.nq <= ltop_ks4()) {
       p.ks = 4;
       p.nw = p.nq * 4;
     }
@@ -2061,9 +2068,13 @@ static int dispatch_tile_eb(int64_t D, const Plan& p, int g, const unsigned char
 #define IRC_SCAN_CASE(DD)                                              \
   case DD:                                                             \
     if (p.ks == 4) {                                                   \
-      if constexpr (MODE == LTOP && EB == 2 && (DD == 768 || DD == 1024)) { \
+      if constexpr ((MODE == LTOP || MODE == SCORES) && EB == 2 &&     \
+                    (DD == 768 || DD == 1024)) {                       \
         if (p.nq == 1) launch_tile<DD, 1, MODE, EB, 4>(IRC_SCAN_ARGS); \
         else launch_tile<DD, 2, MODE, EB, 4>(IRC_SCAN_ARGS);           \
+      } else {                                                         \
+        set_error("scan: four k-slices planned for an unsupported mode"); \
+        return IRC_E_INVALID;                                          \
       }                                                                \
     } else if (p.nq == 1) launch_tile<DD, 1, MODE, EB>(IRC_SCAN_ARGS); \
     else if (p.nq == 2) launch_tile<DD, 2, MODE, EB>(IRC_SCAN_ARGS);   \

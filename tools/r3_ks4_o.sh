@@ -1,5 +1,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
+export IRC_SCAN_LTOP_KS4=1
 mkdir -p gpurun_out
 V=information-retrieval-with-contrastive-learning_amd/irc_amd/lib/variants
 for c in "7 20000 1024 200 5" "1 50011 768 100 0" "33 40000 768 100 2"; do
