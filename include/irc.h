@@ -128,6 +128,12 @@ int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M,
  * the results are bit-identical in every mode (env IRC_GEMM_PERSIST sets the
  * initial mode).  Returns the previous mode. */
 int irc_gemm_set_persistent(int mode);
+/* K loop of the 256 x 384 / 256 x 256 big-tile bf16 GEMM (QKV, out-proj, FFN2, the
+ * LSTM input projections): 1 = a 4-slot ring of 32-deep K-tiles with three in flight
+ * (the default), 0 = two 64-deep slots.  Same MFMAs in the same k order, so the
+ * results are bit-identical (env IRC_BIG_RING sets the initial value).  Returns the
+ * previous setting. */
+int irc_gemm_set_big_ring(int on);
 
 /* ------------------------------------------------------------- BERT encoder
  * Frozen BERT forward pieces (contrastive_module.py:36-41 -> HF BertModel):

@@ -24,6 +24,8 @@
 // in that XCD's L2).
 #include "gemm_pp.h"
 
+#include <atomic>
+
 namespace irc {
 namespace gemm {
 
@@ -494,9 +496,45 @@ __device__ __forceinline__ void stage_part(const unsigned short* __restrict__ X,
     glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
   }
 }
+// Ring form (RING = true): 32-deep K-tiles in 4 LDS slots (64-byte rows, 40 KB a
+// slot at 256 x 384), three in flight: K-tile kt + 3 is issued into the slot K-tile
+// kt - 1 used, right after the one barrier of iteration kt (every wave is past its
+// reads of kt - 1 there), and waited for by a counted vmcnt three iterations later,
+// so the DMA has three K-tiles of MFMAs to land instead of one (the 2-slot form waits
+// vmcnt(0) at the end of every 64-deep K-tile: FFN2 181 -> 126 us with no DMA at all,
+// profiles/r03_big_q_*).  Chunk c of row r sits in slot c ^ ((r >> 2) & 3), so the 8
+// lanes of each ds_read_b128 phase (rows r0 .. r0 + 7) hit 8 distinct 16-byte bank
+// slots.  Same MFMAs in the same k order as the 2-slot form: bit-identical results.
+constexpr int BK4 = 32, ROW4 = BK4 * 2, NST = 4;
+template <int ROWS>
+__device__ __forceinline__ void stage4(const unsigned short* __restrict__ X, int64_t ld, int r0,
+                                       int nrows, int k0, char* lds_tile, int wave, int lane) {
+  constexpr int CH = ROWS * 4;  // 16-byte chunks (4 per 64-byte row)
+  static_assert(CH % NT == 0, "whole passes");
+#pragma unroll
+  for (int i = 0; i < CH / NT; ++i) {
+    const int p = (i * NW + wave) * 64 + lane;  // lane-linear LDS chunk
+    const int row = p >> 2;
+    const int c = (p & 3) ^ ((row >> 2) & 3);
+    int gr = r0 + row;
+    gr = gr < nrows ? gr : nrows - 1;
+    glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
+  }
+}
 }  // namespace big
 
-template <typename TO, int EPI, int WNB>
+// IRC_BIG_RING=0 selects the 2-slot 64-deep loop of gemm_big_kernel (A/B; read on
+// first use); irc_gemm_set_big_ring switches it at run time (the tests compare both).
+inline std::atomic<int>& big_ring_mode() {
+  static std::atomic<int> on{[] {
+    const char* e = getenv("IRC_BIG_RING");
+    return (e && e[0] == '1') ? 1 : 0;
+  }()};
+  return on;
+}
+inline bool big_ring() { return big_ring_mode().load(std::memory_order_relaxed) != 0; }
+
+template <typename TO, int EPI, int WNB, bool RING = false>
 __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
   using big::BK;
   using big::NT;
@@ -531,6 +569,53 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 #pragma unroll
     for (int j = 0; j < WNB; ++j) acc[i][j] = (f32x16)0.0f;
 
+  if constexpr (RING) {
+    using big::BK4;
+    using big::ROW4;
+    constexpr int A4 = BM * ROW4, STG4 = A4 + BN * ROW4;
+    static_assert(big::NST * STG4 <= 2 * STAGE, "ring fits the 2-slot allocation");
+    constexpr int PPT = (BM * 4 + BN * 4) / NT;  // DMA wave-instructions per K-tile per wave
+    const int nk = g.K / BK4;
+#pragma unroll
+    for (int s0 = 0; s0 < big::NST - 1; ++s0)
+      if (s0 < nk) {
+        big::stage4<BM>(A, g.lda, m0, g.M, s0 * BK4, lds + s0 * STG4, wave, lane);
+        big::stage4<BN>(B, g.ldb, n0, g.N, s0 * BK4, lds + s0 * STG4 + A4, wave, lane);
+      }
+    const int sw4 = (r32 >> 2) & 3;
+    for (int kt = 0; kt < nk; ++kt) {
+      // K-tiles kt + 1, kt + 2 may still be in flight (issued after kt)
+      const int after = nk - 1 - kt;
+      if (after >= 2) wait_vmcnt<2 * PPT>();
+      else if (after == 1) wait_vmcnt<PPT>();
+      else wait_vmcnt<0>();
+      wg_barrier();  // every wave's share of kt landed; every wave done reading kt - 1
+      if (kt + 3 < nk) {
+        char* nxt = lds + ((kt + 3) & 3) * STG4;
+        big::stage4<BM>(A, g.lda, m0, g.M, (kt + 3) * BK4, nxt, wave, lane);
+        big::stage4<BN>(B, g.ldb, n0, g.N, (kt + 3) * BK4, nxt + A4, wave, lane);
+      }
+      const char* la = lds + (kt & 3) * STG4;
+      const char* lb = la + A4;
+#pragma unroll
+      for (int kk = 0; kk < BK4 / 16; ++kk) {
+        const int coff = ((2 * kk + h) ^ sw4) * 16;
+        bf16x8 fa[4], fb[WNB];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 32 + r32) * ROW4 + coff);
+#pragma unroll
+        for (int j = 0; j < WNB; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8*>(lb + (wn * 32 * WNB + j * 32 + r32) * ROW4 + coff);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < WNB; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // the epilogue's staging rows overlap the ring
+  } else {
   const int nk = g.K / BK;
   big::stage<BM>(A, g.lda, m0, g.M, 0, lds, wave, lane);
   big::stage<BN>(B, g.ldb, n0, g.N, 0, lds + A_BYTES, wave, lane);
@@ -583,6 +668,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
     wait_vmcnt<0>();
     __syncthreads();
   }
+  }  // 2-slot form
 
 #ifdef IRC_PP_DIAG_NOEPI  // diagnostic build: main loop only (every accumulator kept live)
   {
@@ -777,8 +863,13 @@ static int launch_big(const Args& g, int batch, int wnb, hipStream_t st) {
   const int bn = 128 * wnb;
   const int tiles = ((g.M + big::BM - 1) / big::BM) * ((g.N + bn - 1) / bn);
   prof_begin(st);
-  if (wnb == 3)
+  const bool ring = big_ring() && g.K % big::BK4 == 0;
+  if (wnb == 3 && ring)
+    hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 3, true>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
+  else if (wnb == 3)
     hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 3>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
+  else if (ring)
+    hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 2, true>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
   else
     hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 2>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
   prof_end("gemm_bf16", st, 2.0 * g.M * g.N * g.K * batch);
@@ -872,6 +963,12 @@ extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue,
     if (sp > s) s = sp;
   }
   return s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
+}
+
+// 4-slot ring (1, the default) or 2-slot loop (0) of the 256-row big-tile GEMM;
+// returns the previous setting.
+extern "C" int irc_gemm_set_big_ring(int on) {
+  return irc::gemm::big_ring_mode().exchange(on ? 1 : 0);
 }
 
 // dtype codes: 0 = bf16, 1 = fp32

@@ -25,6 +25,13 @@ def _code(t: torch.Tensor) -> int:
         raise TypeError(f"irc kernels take bf16 or fp32, got {t.dtype}") from None
 
 
+def gemm_set_big_ring(on) -> int:
+    """K loop of the big-tile bf16 GEMM (irc_gemm_set_big_ring): True = 4-slot ring of
+    32-deep K-tiles (the default), False = two 64-deep slots.  Bit-identical results.
+    Returns the previous setting."""
+    return int(_lib.load().irc_gemm_set_big_ring(1 if on else 0))
+
+
 def gemm_set_persistent(mode) -> int:
     """Persistent tile loop of the 256x256 bf16 GEMM (irc_gemm_set_persistent): 0 off
     (the default), 1 / True dynamic tiles with the next tile's first K-tile prestaged

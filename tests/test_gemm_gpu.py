@@ -162,6 +162,34 @@ def test_big_tile_accumulate_fp32(gpu):
     assert (out.cpu() - ref).abs().max().item() <= 2e-3 * K ** 0.5
 
 
+@pytest.mark.parametrize("epi", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(32768, 2304, 768), (32768, 768, 3072), (32668, 768, 192),
+                                   (32700, 2304, 64)])
+def test_big_tile_ring_bitwise(gpu, epi, M, N, K):
+    """The big-tile kernel's 4-slot ring of 32-deep K-tiles (three in flight) against
+    its 2-slot 64-deep loop: the same MFMAs in the same k order, so the outputs are
+    equal bit for bit -- on the BERT-base QKV / FFN2 shapes (the shapes irc_gemm
+    sends to the 256 x 384 kernel: whole waves of its tiles), with ragged M, K = 192
+    (six ring K-tiles) and K = 64 (two: fewer than the ring's prefetch depth)."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(M + N + K + epi)
+    a = torch.randn((M, K), generator=g).to(torch.bfloat16).to(gpu)
+    b = torch.randn((N, K), generator=g).to(torch.bfloat16).to(gpu)
+    bias = torch.randn((N,), generator=g).to(gpu) if epi in (1, 2, 3) else None
+    res = torch.randn((M, N), generator=g).to(torch.bfloat16).to(gpu) if epi == 3 else None
+    outs = []
+    prev = ops.gemm_set_big_ring(True)
+    try:
+        for ring in (True, False):
+            ops.gemm_set_big_ring(ring)
+            outs.append(ops.gemm(a, b, bias=bias, epilogue=epi, residual=res))
+        torch.cuda.synchronize()
+    finally:
+        ops.gemm_set_big_ring(prev)
+    assert torch.equal(outs[0], outs[1])
+
+
 # ---- the 256x256 ping-pong path (gemm_pp.hip): shapes with >= 32 output tiles
 @pytest.mark.parametrize("trans_a,b_is_nk", [(False, True), (False, False), (True, True),
                                              (True, False)])
