@@ -523,8 +523,10 @@ __device__ __forceinline__ void stage4(const unsigned short* __restrict__ X, int
 }
 }  // namespace big
 
-// IRC_BIG_RING=0 selects the 2-slot 64-deep loop of gemm_big_kernel (A/B; read on
-// first use); irc_gemm_set_big_ring switches it at run time (the tests compare both).
+// IRC_BIG_RING=1 selects the 4-slot ring of gemm_big_kernel (A/B; read on first use;
+// default off: within noise of the 2-slot loop on every BERT shape and 1.4% slower on
+// the C2 step, profiles/r03_ring_r_*); irc_gemm_set_big_ring switches it at run time
+// (the tests compare both bit for bit).
 inline std::atomic<int>& big_ring_mode() {
   static std::atomic<int> on{[] {
     const char* e = getenv("IRC_BIG_RING");
@@ -965,8 +967,9 @@ extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue,
   return s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
 }
 
-// 4-slot ring (1, the default) or 2-slot loop (0) of the 256-row big-tile GEMM;
-// returns the previous setting.
+// 4-slot ring (1) or 2-slot loop (0, the default: the ring measured no faster on
+// the BERT shapes, profiles/r03_ring_r_*) of the 256-row big-tile GEMM; returns the
+// previous setting.
 extern "C" int irc_gemm_set_big_ring(int on) {
   return irc::gemm::big_ring_mode().exchange(on ? 1 : 0);
 }

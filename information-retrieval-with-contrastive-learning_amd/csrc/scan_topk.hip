@@ -1537,6 +1537,9 @@ __device__ uint64_t dense_kth(const uint64_t (&v)[U], const uint64_t* xk, uint32
     kr = s_misc[1];
     const bool done = s_misc[3] || lo == 0;
     __syncthreads();  // s_misc is rewritten by the next pass (or the next call)
+#ifdef IRC_SCAN_STAMPS  // diagnostic: radix passes of block 0's last dense_kth
+    if (blockIdx.x == 0 && tid == 0) *(volatile uint64_t*)&dbg_stamps[2][24] = (uint64_t)pass + 1;
+#endif
     if (done) break;
     hi = lo - 1;
   }
@@ -1631,6 +1634,7 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int M4 = a.LS * LT_M;
   const uint64_t* L = a.lists + (int64_t)q * M4;
+  STAMP(2, 16);
   uint64_t v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -1646,6 +1650,7 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
   }
   uint32_t M = 0;
   uint64_t kth = dense_kth<U>(v, xk, 0, a.k, hbuf, s_mm, s_cnt, s_misc, &M);
+  STAMP(2, 17);
   // lists whose last slot could have pushed out a winner -> the tile rows they
   // cover (slice kh * 2 + h: rows (j & 3) + 8 (j >> 2) + 4 h, j in kh's half)
 #pragma unroll
@@ -1659,6 +1664,7 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
     if (vflag[w]) vw[atomicAdd(&s_nv, 1u)] = (uint16_t)w;
   __syncthreads();
   const int nv = (int)s_nv;
+  STAMP(2, 18);
   if (nv > 0 && tid == 0) {
     atomicAdd(&g_dense_rescans[0], 1ull);
     atomicAdd(&g_dense_rescans[1], (unsigned long long)nv);
@@ -1753,6 +1759,7 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
     }
     kth = dense_kth<U>(v, xk, s_xn, a.k, hbuf, s_mm, s_cnt, s_misc, &M);
   }
+  STAMP(2, 19);
   // collect the exactly min(M, k) keys >= kth, then place them by rank
   const uint32_t xn = s_xn;
 #pragma unroll
@@ -1788,6 +1795,7 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
       a.out_idx[(int64_t)q * k + pos] = id;
     }
   }
+  STAMP(2, 20);
 }
 
 // The 256-thread select_kernel is the default: measured on MI355X (100k x 768,

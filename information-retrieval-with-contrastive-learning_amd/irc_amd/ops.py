@@ -27,7 +27,8 @@ def _code(t: torch.Tensor) -> int:
 
 def gemm_set_big_ring(on) -> int:
     """K loop of the big-tile bf16 GEMM (irc_gemm_set_big_ring): True = 4-slot ring of
-    32-deep K-tiles (the default), False = two 64-deep slots.  Bit-identical results.
+    32-deep K-tiles, False = two 64-deep slots (the default; the ring measured no
+    faster on MI355X).  Bit-identical results.
     Returns the previous setting."""
     return int(_lib.load().irc_gemm_set_big_ring(1 if on else 0))
 
