@@ -1453,6 +1453,16 @@ __device__ uint64_t dense_kth(const uint64_t (&v)[U], const uint64_t* xk, uint32
     mn = x < mn ? x : mn;
     mx = x > mx ? x : mx;
   }
+  // Lower bound of the k-th key that is tighter than the minimum: the smallest of the
+  // threads' own maxima.  Those are distinct keys, so once at least k threads hold a
+  // key, k keys are >= it.  The radix passes then start at the top bit in which it and
+  // the maximum differ -- on the global [min, max] the first digit put most keys in a
+  // few bins, and their LDS atomics serialised (pass 0 4.3 us of the 12 us select at
+  // Q = 1, profiles/r03_dense_t.txt; 1.6 us and one pass instead of two after it,
+  // r03_dense_u.txt).  Keys below the window's prefix are below the k-th key and are
+  // not counted: the same exact k-th key.
+  const uint64_t tmax = c ? mx : ~0ull;
+  const uint32_t nthr = (uint32_t)__popcll(__ballot(c != 0));
   uint32_t* h0 = hbuf;
   uint32_t* h1 = hbuf + SEL_NW * 256;
   for (int i = tid; i < SEL_NW * 256; i += SEL_NT) h0[i] = 0;
@@ -1460,23 +1470,31 @@ __device__ uint64_t dense_kth(const uint64_t (&v)[U], const uint64_t* xk, uint32
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   mn = wave_min_u64(mn);
   mx = wave_max_u64(mx);
+  const uint64_t lbw = wave_min_u64(tmax);
   if (lane == 0) {
     s_mm[wave] = mn;
     s_mm[SEL_NW + wave] = mx;
+    s_mm[2 * SEL_NW + wave] = lbw;
     s_cnt[wave] = c;
+    s_cnt[SEL_NW + wave] = nthr;
   }
   __syncthreads();
-  uint32_t M = 0;
+  uint32_t M = 0, nt = 0;
   mn = s_mm[0];
   mx = s_mm[SEL_NW];
+  uint64_t lb = s_mm[2 * SEL_NW];
 #pragma unroll
   for (int w = 0; w < SEL_NW; ++w) {
     M += s_cnt[w];
+    nt += s_cnt[SEL_NW + w];
     mn = s_mm[w] < mn ? s_mm[w] : mn;
     mx = s_mm[SEL_NW + w] > mx ? s_mm[SEL_NW + w] : mx;
+    lb = s_mm[2 * SEL_NW + w] < lb ? s_mm[2 * SEL_NW + w] : lb;
   }
   *total = M;
+  STAMP(2, 25);
   if (M <= (uint32_t)k) return 0;
+  if (nt >= (uint32_t)k) mn = lb;  // else the global minimum
   const int top = 63 - __builtin_clzll((mn ^ mx) | 1ull);
   uint64_t pmask = top >= 63 ? 0ull : (~0ull << (top + 1));
   uint64_t prefix = mn & pmask;
@@ -1539,6 +1557,7 @@ __device__ uint64_t dense_kth(const uint64_t (&v)[U], const uint64_t* xk, uint32
     __syncthreads();  // s_misc is rewritten by the next pass (or the next call)
 #ifdef IRC_SCAN_STAMPS  // diagnostic: radix passes of block 0's last dense_kth
     if (blockIdx.x == 0 && tid == 0) *(volatile uint64_t*)&dbg_stamps[2][24] = (uint64_t)pass + 1;
+    if (pass < 2) STAMP(2, 26 + pass);
 #endif
     if (done) break;
     hi = lo - 1;
@@ -1619,10 +1638,10 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
   constexpr int U = SEL_STAGE / SEL_NT;
   constexpr int MAXW = SEL_STAGE / (LT_M * 2);  // workers (NSL >= 2)
   __shared__ uint32_t hbuf[2 * SEL_NW * 256];
-  __shared__ uint64_t cand[SEL_MAXK];
+  __shared__ __attribute__((aligned(16))) uint64_t cand[SEL_MAXK];
   __shared__ uint64_t xk[SD_XCAP];
-  __shared__ uint64_t s_mm[2 * SEL_NW];
-  __shared__ uint32_t s_cnt[SEL_NW];
+  __shared__ uint64_t s_mm[3 * SEL_NW];
+  __shared__ uint32_t s_cnt[2 * SEL_NW];
   __shared__ uint32_t s_misc[4];
   __shared__ uint32_t s_xn, s_coll, s_nv;
   __shared__ uint32_t vflag[MAXW];  // per worker: tile rows of its truncated lists
@@ -1760,17 +1779,29 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
     kth = dense_kth<U>(v, xk, s_xn, a.k, hbuf, s_mm, s_cnt, s_misc, &M);
   }
   STAMP(2, 19);
-  // collect the exactly min(M, k) keys >= kth, then place them by rank
+  // collect the exactly min(M, k) keys >= kth, then place them by rank.  The wave's
+  // U ballots are counted first, so it takes its cand range with ONE LDS atomic (a
+  // returning atomic per ballot serialised 16 round trips: ~1.3 us of the 12 us select
+  // at Q = 1, profiles/r03_dense_s.txt); the order inside cand is irrelevant (ranked).
   const uint32_t xn = s_xn;
+  {
+    uint64_t bal[U];
+    uint32_t tot = 0;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const bool take = v[u] != 0 && v[u] >= kth;
-    const uint64_t bal = __ballot(take);
-    if (bal != 0) {
+    for (int u = 0; u < U; ++u) {
+      bal[u] = __ballot(v[u] != 0 && v[u] >= kth);
+      tot += (uint32_t)__popcll(bal[u]);
+    }
+    if (tot != 0) {  // wave-uniform
       uint32_t b0 = 0;
-      if (lane == 0) b0 = atomicAdd(&s_coll, (uint32_t)__popcll(bal));
+      if (lane == 0) b0 = atomicAdd(&s_coll, tot);
       b0 = __shfl(b0, 0, 64);
-      if (take) cand[b0 + __popcll(bal & ((1ull << lane) - 1))] = v[u];
+      const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if ((bal[u] >> lane) & 1ull) cand[b0 + __popcll(bal[u] & below)] = v[u];
+        b0 += (uint32_t)__popcll(bal[u]);
+      }
     }
   }
   for (uint32_t i = tid; i < xn; i += SEL_NT)
@@ -1785,8 +1816,18 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
       int pos = i;
       if (i < cnt) {
         const uint64_t key = cand[i];
-        int rank = 0;
-        for (int j = 0; j < cnt; ++j) rank += (int)(cand[j] > key);
+        // rank = keys above this one: 16-byte broadcast reads, 8 keys per step in
+        // flight (the one-key loop was LDS-latency bound, ~2 us at k = 100)
+        int rank = 0, j = 0;
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        for (; j + 8 <= cnt; j += 8) {
+          u64x2 c[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) c[t] = *reinterpret_cast<const u64x2*>(&cand[j + 2 * t]);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) rank += (int)(c[t][0] > key) + (int)(c[t][1] > key);
+        }
+        for (; j < cnt; ++j) rank += (int)(cand[j] > key);
         pos = rank;
         sc = unorderable_f32((uint32_t)(key >> 32)) * a.smul;
         id = (int64_t)(uint32_t)(~(uint32_t)key);

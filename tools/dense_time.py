@@ -1,7 +1,8 @@
 """Diagnostic (library built with -DIRC_SCAN_STAMPS, loaded via IRC_LIB_PATH): phase
 times of select_dense_kernel's block 0 (query 0) on a C3-sized shard, per Q.
-Stamps are s_memrealtime (100 MHz): 16 start, 17 first dense_kth done, 18 truncated
-lists flagged, 19 rescan done, 20 results written; [24] radix passes."""
+Stamps are s_memrealtime (100 MHz): 16 start, 25 keys loaded + min/max/count, 26/27
+radix passes 0/1 done, 17 first dense_kth done, 18 truncated lists flagged, 19 rescan
+done, 20 results written; [24] radix passes."""
 import argparse
 import ctypes
 import os
@@ -36,11 +37,12 @@ def main():
             torch.cuda.synchronize()
             lib.irc_scan_dbg_stamps(buf.ctypes.data_as(ctypes.c_void_p))
             st = buf[2].astype(np.int64)
-            rows.append([(st[i] - st[16]) * 10 / 1000 for i in (17, 18, 19, 20)] + [st[24]])
+            rows.append([(st[i] - st[16]) * 10 / 1000 for i in (25, 26, 27, 17, 18, 19, 20)] + [st[24]])
         r = np.array(rows[2:])
         med = np.median(r, axis=0)
-        print(f"Q={q}: select_dense block 0 (us from start): kth {med[0]:.2f}  flags {med[1]:.2f}  "
-              f"rescan {med[2]:.2f}  end {med[3]:.2f}  radix passes {med[4]:.0f}", flush=True)
+        print(f"Q={q}: select_dense block 0 (us from start): loads+minmax {med[0]:.2f}  pass0 {med[1]:.2f}  "
+              f"pass1 {med[2]:.2f}  kth {med[3]:.2f}  flags {med[4]:.2f}  "
+              f"rescan {med[5]:.2f}  end {med[6]:.2f}  radix passes {med[7]:.0f}", flush=True)
 
 
 if __name__ == "__main__":
