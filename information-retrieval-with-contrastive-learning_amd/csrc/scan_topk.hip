@@ -773,11 +773,16 @@ __device__ __forceinline__ void select_fast(const Src& src, int q, int k, int mo
       mx = v[u] > mx ? v[u] : mx;
     }
   }
+  // the smallest of the threads' own maxima: a lower bound of the k-th key once
+  // min(M, SEL_NT) >= k threads hold a key (distinct keys) -- the radix window starts
+  // there instead of at the minimum (as in dense_kth: fewer keys per first-pass bin)
+  const uint64_t lbw = wave_min_u64((uint32_t)tid < M ? mx : ~0ull);
   mn = wave_min_u64(mn);
   mx = wave_max_u64(mx);
   if (lane == 0) {
     s_mm[wave] = mn;
     s_mm[SEL_NW + wave] = mx;
+    s_mm[2 * SEL_NW + wave] = lbw;
   }
   __syncthreads();
   STAMP(mode, 2);
@@ -787,11 +792,14 @@ __device__ __forceinline__ void select_fast(const Src& src, int q, int k, int mo
   if (M > (uint32_t)k) {
     mn = s_mm[0];
     mx = s_mm[SEL_NW];
+    uint64_t lb = s_mm[2 * SEL_NW];
 #pragma unroll
     for (int w = 1; w < SEL_NW; ++w) {
       mn = s_mm[w] < mn ? s_mm[w] : mn;
       mx = s_mm[SEL_NW + w] > mx ? s_mm[SEL_NW + w] : mx;
+      lb = s_mm[2 * SEL_NW + w] < lb ? s_mm[2 * SEL_NW + w] : lb;
     }
+    if ((M < (uint32_t)SEL_NT ? M : (uint32_t)SEL_NT) >= (uint32_t)k) mn = lb;
     const int top = 63 - __builtin_clzll((mn ^ mx) | 1ull);
     uint64_t pmask = top >= 63 ? 0ull : (~0ull << (top + 1));
     uint64_t prefix = mn & pmask;
@@ -859,16 +867,26 @@ __device__ __forceinline__ void select_fast(const Src& src, int q, int k, int mo
   }
   STAMP(mode, 12);
   if (IRC_SCAN_SEL_STOP == 3 && mode == SEL_FINAL) return;
-  // collect the exactly min(M, k) keys >= kth: one LDS atomic per wave and slot
+  // collect the exactly min(M, k) keys >= kth: one LDS atomic per wave (its U
+  // ballots counted first; a returning atomic per slot serialised U round trips)
+  {
+    uint64_t bal[U];
+    uint32_t tot = 0;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const bool take = tid + u * SEL_NT < M && v[u] >= kth;
-    const uint64_t bal = __ballot(take);
-    if (bal != 0) {
+    for (int u = 0; u < U; ++u) {
+      bal[u] = __ballot(tid + u * SEL_NT < M && v[u] >= kth);
+      tot += (uint32_t)__popcll(bal[u]);
+    }
+    if (tot != 0) {  // wave-uniform
       uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(s_coll, (uint32_t)__popcll(bal));
+      if (lane == 0) base = atomicAdd(s_coll, tot);
       base = __shfl(base, 0, 64);
-      if (take) cand[base + __popcll(bal & ((1ull << lane) - 1))] = v[u];
+      const uint64_t below = (1ull << lane) - 1;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if ((bal[u] >> lane) & 1ull) cand[base + __popcll(bal[u] & below)] = v[u];
+        base += (uint32_t)__popcll(bal[u]);
+      }
     }
   }
   __syncthreads();
@@ -885,9 +903,14 @@ __device__ __forceinline__ void select_fast(const Src& src, int q, int k, int mo
         const uint64_t key = cand[i];
         int rank = 0;
         int j = 0;
-        for (; j + 4 <= cnt; j += 4)
-          rank += (int)(cand[j] > key) + (int)(cand[j + 1] > key) + (int)(cand[j + 2] > key) +
-                  (int)(cand[j + 3] > key);
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        for (; j + 8 <= cnt; j += 8) {  // 16-byte broadcast reads, 8 keys in flight
+          u64x2 c[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) c[t] = *reinterpret_cast<const u64x2*>(&cand[j + 2 * t]);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) rank += (int)(c[t][0] > key) + (int)(c[t][1] > key);
+        }
         for (; j < cnt; ++j) rank += (int)(cand[j] > key);
         pos = rank;
         sc = unorderable_f32((uint32_t)(key >> 32)) * smul;
@@ -927,11 +950,11 @@ __device__ __forceinline__ void select_body(Src src, int k, int mode,
                                                          int64_t* __restrict__ out_idx,
                                                          float smul) {
   __shared__ uint32_t hist[SEL_NW][256];
-  __shared__ uint64_t cand[SEL_MAXK];
+  __shared__ __attribute__((aligned(16))) uint64_t cand[SEL_MAXK];
   __shared__ uint64_t stage[SEL_STAGE];
   __shared__ uint16_t rid[SEL_STAGE];
   __shared__ uint32_t roff[SEL_MAXR];
-  __shared__ uint64_t s_mm[2][SEL_NW];
+  __shared__ uint64_t s_mm[3][SEL_NW];  // min, max, threads' lower bound (select_fast)
   __shared__ uint32_t s_wsum[SEL_NW];
   __shared__ uint32_t s_misc[4];  // 0: total count, 1: kr, 2: selected digit, 3: staging ctr
   __shared__ uint32_t s_coll;     // collect counter
