@@ -240,7 +240,9 @@ def run_train(args, rank, world, dev, weights="bf16", cfg=None):
         torch.cuda.synchronize()
     lib.irc_prof_enable(0)
     g_s, g_n, g_flops = _prof(lib, gname)
-    ptag = gname if weights == "bf16" else "gemm_mx"
+    large = "large" in str((cfg or {}).get("bert", {}).get("name", ""))
+    # PMC traffic of THIS leg's GEMMs (profiles/pmc_<tag>.json; null when absent)
+    ptag = ("gemm_bf16_c4" if large else gname) if weights == "bf16" else "gemm_mx"
     g_bytes = _alg_bytes(lib, _pmc_traffic(ptag), gname + "_bytes")
     flops_pair = 2 * model.bert_model.flops_per_sequence(TRAIN_L) + _lstm_flops_per_pair(cfg)
     pairs = TRAIN_B * args.steps * world

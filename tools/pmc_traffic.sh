@@ -26,6 +26,8 @@ summ scan_c2 $OUT/scan_c2_FETCH_SIZE $OUT/scan_c2_WRITE_SIZE \
   --note "C2 scan filter (100k x 768 bf16 docs, 256 queries), bench.py --part scan_c2" || exit 1
 summ train $OUT/train_FETCH_SIZE $OUT/train_WRITE_SIZE "$GEMM" gemm_bf16 --out $OUT \
   --note "all bf16 GEMM dispatches of bench.py --part train (BERT-base frozen fwd + BiLSTM head)" || exit 1
+summ train_c4 $OUT/train_c4_FETCH_SIZE $OUT/train_c4_WRITE_SIZE "$GEMM" gemm_bf16_c4 --out $OUT \
+  --note "all bf16 GEMM dispatches of bench.py --part train_c4 (BERT-large frozen fwd + BiLSTM head)" || exit 1
 summ bert $OUT/bert_FETCH_SIZE $OUT/bert_WRITE_SIZE "$GEMM" gemm_bf16_bert --out $OUT \
   --note "all bf16 GEMM dispatches of bench.py --part bert (trainable BERT-base fwd+bwd)" || exit 1
 exit 0
