@@ -598,6 +598,60 @@ def cpu_baseline_scan(budget_s):
                       f"k={SCAN_K}): torch CPU fp32 matmul over 64k-doc chunks + topk merge"}
 
 
+def _r(x, n=4):
+    return None if x is None else float(f"{x:.{n}g}")
+
+
+def _leg_summary(name, d):
+    """The few numbers of one leg that a reader checks first (value, step time, roofline
+    fraction, Q sweep); the full leg goes to the detail file."""
+    if name.startswith("train"):
+        r = d.get("roofline") or {}
+        return {"pairs_per_s": _r(d.get("pairs_per_s"), 5), "ms_per_step": _r(d.get("ms_per_step")),
+                "gemm_frac": _r(r.get("frac"), 3), "gemm_ms_per_step": _r(r.get("gemm_ms_per_step")),
+                "traffic_over_alg": _r(r.get("traffic_over_alg"), 3),
+                "step_tflops": _r(d.get("step_tflops"))}
+    if name == "sparse_tfidf":
+        c = d.get("cpu_baseline") or {}
+        return {"queries_per_s": _r(d.get("value"), 5), "cpu_queries_per_s": _r(c.get("value"))}
+    r, c = d.get("roofline") or {}, d.get("call_level") or {}
+    out = {"queries_per_s": _r(d.get("value"), 5), "Q": d.get("queries"),
+           "docs_per_gpu": d.get("docs_per_gpu"), "bound": r.get("bound"),
+           "filter_frac": _r(r.get("frac"), 3), "filter_us": _r(r.get("kernel_avg_us")),
+           "call_us": _r(c.get("serial_us_per_call")), "call_hbm_frac": _r(c.get("serial_hbm_frac"), 3)}
+    if d.get("q_sweep_local"):
+        out["sweep_call_us"] = {str(x["Q"]): _r(x["call_us"]) for x in d["q_sweep_local"]}
+        out["sweep_call_frac"] = {str(x["Q"]): _r(x["call_hbm_frac"], 3) for x in d["q_sweep_local"]}
+    return out
+
+
+# summary order: the training legs last (nearest the end of the output)
+LEGS = ("sparse_tfidf", "retrieval_fp8", "retrieval_c4", "retrieval_c3", "retrieval",
+        "train_bert", "train_c4", "train_fp8", "train")
+
+
+def _compact(line):
+    """The printed line keeps the contract keys and one short summary per leg, placed
+    last so that a reader holding only the output's tail still sees every leg; the
+    full per-leg objects (Q sweeps, traffic sources, notes) go to bench_detail.json
+    (gpurun_out/ when present, else the working directory) and are named in the line."""
+    legs = {k: line[k] for k in LEGS if k in line}
+    if not legs:
+        return line
+    detail = os.path.join(ROOT, "gpurun_out") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) \
+        else os.getcwd()
+    path = os.path.join(detail, "bench_detail.json")
+    try:
+        with open(path, "w") as f:
+            json.dump(line, f)
+    except OSError:
+        path = None
+    out = {k: v for k, v in line.items() if k not in LEGS}
+    out["detail_file"] = path and os.path.relpath(path, ROOT)
+    out["legs"] = {k: _leg_summary(k, legs[k]) for k in LEGS if k in legs}
+    return out
+
+
 def _free_port():
     import socket
 
@@ -727,7 +781,7 @@ def main():
         }
         if train is not None:
             line["train"] = {k: train[k] for k in ("pairs_per_s", "ms_per_step", "step_tflops",
-                                                   "flops_per_pair", "loss_last")}
+                                                   "flops_per_pair", "loss_last", "roofline")}
         if bert is not None:
             line["train_bert"] = bert
         if train_c4 is not None:
@@ -759,7 +813,7 @@ def main():
             scan_fp8["workload"] = (f"C5 retrieval shard: {FP8_N_PER_GPU} e4m3 docs/GPU "
                                     f"(5M over 8 GPUs), {C5_Q} queries, top-{SCAN_K}")
             line["retrieval_fp8"] = scan_fp8
-        print(json.dumps(line), flush=True)
+        print(json.dumps(_compact(line)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

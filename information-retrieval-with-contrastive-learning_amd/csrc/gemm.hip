@@ -447,8 +447,8 @@ inline int split_count(int TIbytes, int out_f32, int epi, int64_t M, int64_t N, 
 // Both tiles move global -> LDS by global_load_lds_dwordx4 (no VGPR staging),
 // double buffered (2 x 80 KB at WNB=3): tile k+1 is in flight while tile k is
 // consumed.  LDS rows are 128 B (64 k); the 16-byte chunk c of row r is stored at
-// chunk c ^ (r & 7) so the row-wise ds_read_b128 fragment reads are conflict
-// free -- applied on the SOURCE address, since the DMA destination is
+// chunk c ^ ((r >> 1) & 7) (big::chunk_key) so the row-wise ds_read_b128 fragment reads
+// are conflict free -- applied on the SOURCE address, since the DMA destination is
 // lane-linear.  Rows past M / N load a clamped valid row and are never stored.
 // Requires K % 64 == 0, lda/ldb % 8 == 0 and 16-byte aligned bases.
 // Algorithmic HBM bytes of one bf16 GEMM launch: both operands read once, C written
@@ -466,6 +466,22 @@ namespace big {
 constexpr int BM = 256, BK = 64, NW = 8, NT = NW * 64;
 constexpr int ROW_BYTES = BK * 2;  // 128
 
+// The 16-byte chunk c of tile row r sits in slot c ^ chunk_key(r).  ds_read_b128 serves a
+// wave in four 16-lane groups ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, +32), and two
+// 128-byte rows share one 256-byte bank line, so a group's 16 reads are conflict free iff
+// its 8 even and 8 odd rows each get 8 distinct slots.  (r >> 1) & 7 does that for every
+// fragment row set used here (row offsets are multiples of 16); the round-2 key r & 7
+// repeats inside every group (rows r, r + 8 / r + 24) and made every fragment read 2-way
+// conflicted: 47-49% of the LDS-array cycles (profiles/r03_lds_y_before.txt).
+// -DIRC_BIG_OLD_SWZ builds the old key for the A/B (same bytes, same MFMAs: bit-identical).
+__device__ __forceinline__ int chunk_key(int r) {
+#ifdef IRC_BIG_OLD_SWZ
+  return r & 7;
+#else
+  return (r >> 1) & 7;
+#endif
+}
+
 // rows [0, nrows_tile) of one operand tile: nrows_tile*8 16-byte chunks, NT per pass
 template <int ROWS>
 __device__ __forceinline__ void stage(const unsigned short* __restrict__ X, int64_t ld, int r0,
@@ -475,7 +491,7 @@ __device__ __forceinline__ void stage(const unsigned short* __restrict__ X, int6
   for (int i = 0; i < PASSES; ++i) {
     const int p = (i * NW + wave) * 64 + lane;  // 16-byte LDS chunk index (lane-linear)
     const int row = p >> 3;
-    const int c = (p & 7) ^ (row & 7);          // logical k-chunk stored at this slot
+    const int c = (p & 7) ^ chunk_key(row);     // logical k-chunk stored at this slot
     int gr = r0 + row;
     gr = gr < nrows ? gr : nrows - 1;
     glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
@@ -490,7 +506,7 @@ __device__ __forceinline__ void stage_part(const unsigned short* __restrict__ X,
   for (int i = P0; i < P1; ++i) {
     const int p = (i * NW + wave) * 64 + lane;
     const int row = p >> 3;
-    const int c = (p & 7) ^ (row & 7);
+    const int c = (p & 7) ^ chunk_key(row);
     int gr = r0 + row;
     gr = gr < nrows ? gr : nrows - 1;
     glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
@@ -623,7 +639,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
   big::stage<BN>(B, g.ldb, n0, g.N, 0, lds + A_BYTES, wave, lane);
   wait_vmcnt<0>();
   __syncthreads();
-  const int swz = r32 & 7;
+  const int swz = big::chunk_key(r32);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
 #ifdef IRC_PP_DIAG_NODMA  // diagnostic build: only K-tile 0 is loaded

@@ -657,8 +657,7 @@ __device__ __forceinline__ void epilogue_scan(const PArgs& g, const f32x4 (&acc)
     thf[threadIdx.x] = q >= g.M ? __builtin_huge_valf()
                                 : (hi == 0 ? -__builtin_huge_valf() : unorderable_f32(hi));
   }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  wg_barrier();
+  lds_barrier();
   after_init();
 #ifdef IRC_PP_SCAN_NOEPI  // diagnostic build: main loop + counters only
   if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
@@ -722,8 +721,7 @@ __device__ __forceinline__ void epilogue_scan(const PArgs& g, const f32x4 (&acc)
     }
   }
   PSTAMP(3);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  wg_barrier();
+  lds_barrier();
   PSTAMP(4);
   if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
     g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = cnt[threadIdx.x];

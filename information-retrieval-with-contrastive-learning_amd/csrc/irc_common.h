@@ -126,8 +126,23 @@ __device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, in
 // Raw workgroup barrier that does NOT drain vmcnt (so LDS-DMA prefetches stay in
 // flight across it); the empty asm statements stop the compiler moving memory
 // operations across the barrier.
+// RULE: s_barrier does not wait for this wave's own LDS accesses either.  A barrier
+// that publishes LDS writes to other waves (or frees LDS that other waves will
+// overwrite after reading it) must be lds_barrier() below, which waits lgkmcnt(0)
+// first; wg_barrier() alone is only for barriers that order DMA (vmcnt, waited
+// explicitly before it) or whose LDS traffic was already waited for.  A raw barrier
+// at an LDS exchange returned stale partial sums on MI355X (the scan's k-slice
+// butterfly, round 3).
 __device__ __forceinline__ void wg_barrier() {
   asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Barrier at an LDS exchange: this wave's LDS writes have landed and its LDS reads
+// have returned before any wave passes (vmcnt is left alone, so LDS-DMA stays in flight).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }

@@ -287,8 +287,7 @@ void scan_tile_kernel(
         af[c] = *reinterpret_cast<const u16x8*>(tb + lo[c & 7] + 256 * (c >> 3));
       if (IRC_SCAN_EARLY_ISSUE) {
         // the slot is free once every wave's fragment reads have returned
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        wg_barrier();
+        lds_barrier();
         if (it + G::NBUF < my_tiles) issue_tile(tile + G::NBUF, it % G::NBUF);
       }
 #pragma unroll
@@ -367,8 +366,7 @@ void scan_tile_kernel(
       // the raw barrier does not wait for LDS writes: without this wait the partner
       // wave can read the slot before the write lands (seen on MI355X with the
       // four-slice exchange, whose round 2 also overwrites a slot another wave wrote)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wg_barrier();
+      lds_barrier();
       const f32x4 t0 = reinterpret_cast<const f32x4*>(xi)[0];
       const f32x4 t1 = reinterpret_cast<const f32x4*>(xi)[1];
       if (kh == 0) {

@@ -158,8 +158,10 @@ def test_c2_train_step_full_size(gpu):
 
 
 def test_c5_fp8_step_loss_vs_fp32(gpu):
-    """C5: the C2 step with every frozen-encoder nn.Linear on e4m3 (per-channel
-    weight, per-token input scales).  Its InfoNCE loss against the fp32-mode step
+    """C5: the C2 step with every frozen-encoder nn.Linear on MX-fp8 (irc_gemm_mx: e4m3
+    codes with one E8M0 scale per 32 consecutive k of a row, for weights and inputs;
+    inputs quantised by their producing LayerNorm / attention / GELU epilogues,
+    irc_amd/bert.py set_weight_format("fp8")).  Its InfoNCE loss against the fp32-mode step
     on the same inputs and initial weights: the fp8 quantisation of 72 GEMM inputs
     perturbs the features (pooled cosine ~0.998, tests/test_fp8_encoder_gpu.py), so
     the bound is looser than bf16's 1e-3; the measured delta is printed."""

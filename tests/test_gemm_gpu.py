@@ -190,6 +190,29 @@ def test_big_tile_ring_bitwise(gpu, epi, M, N, K):
     assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("ring", [False, True])
+@pytest.mark.parametrize("M,N,K", [(32768, 2304, 768), (32768, 768, 3072), (4000, 2100, 640)])
+def test_big_tile_chunk_key_exact(gpu, ring, M, N, K):
+    """The big-tile kernel's LDS chunk key ((r >> 1) & 7 since round 4): small-integer
+    operands make every product and partial sum exact in fp32, so the output must equal
+    the torch product bit for bit -- a chunk stored under one key and read under another
+    (a wrong row, k-chunk or slot) changes the result.  Both the 2-slot and the ring
+    form, on the BERT QKV / FFN2 shapes (256 x 384 tiles) and a ragged 256 x 256 case."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randint(-8, 9, (M, K), generator=g).to(torch.bfloat16)
+    b = torch.randint(-8, 9, (N, K), generator=g).to(torch.bfloat16)
+    prev = ops.gemm_set_big_ring(ring)
+    try:
+        out = ops.gemm(a.to(gpu), b.to(gpu), out_dtype=torch.float32)
+        torch.cuda.synchronize()
+    finally:
+        ops.gemm_set_big_ring(prev)
+    ref = (a.to(gpu).float() @ b.to(gpu).float().t())  # |sum| <= 64 * K < 2^24: exact
+    assert torch.equal(out, ref)
+
+
 # ---- the 256x256 ping-pong path (gemm_pp.hip): shapes with >= 32 output tiles
 @pytest.mark.parametrize("trans_a,b_is_nk", [(False, True), (False, False), (True, True),
                                              (True, False)])

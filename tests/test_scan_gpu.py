@@ -178,6 +178,21 @@ def test_full_c2_size_properties(gpu):
     # idempotence: a second call returns the same bits
     s2, i2 = retrieval.scan_topk(q, d, k)
     assert torch.equal(i, i2) and torch.equal(s, s2)
+    # the oracle at full size, margin-aware, on 6 rows spread over the query batch:
+    # the fp32 restatement of closest_docs (O.scan_topk, evaluation.py:110-112) over the
+    # same bf16 embeddings; the lists agree except where two docs' true scores are
+    # within the accumulation-order tolerance of the oracle's k-th score
+    rows = [0, 1, 97, 128, 200, 255]
+    dn = d.float().cpu().numpy()
+    qn = q[rows].float().cpu().numpy()
+    ri, rs = O.scan_topk(qn, dn, k)
+    exact = qn.astype(np.float64) @ dn.astype(np.float64).T
+    tol = 1e-5  # fp32 accumulation-order difference on unit vectors, D = 768
+    sc, ic = s[rows].cpu().numpy(), i[rows].cpu().numpy()
+    for t in range(len(rows)):
+        np.testing.assert_allclose(sc[t], exact[t, ic[t]], atol=tol)
+        for doc in set(ic[t].tolist()) ^ set(ri[t].tolist()):
+            assert abs(exact[t, doc] - rs[t, -1]) <= 2 * tol, (rows[t], doc)
 
 
 @pytest.mark.parametrize("Q,D,fp8", [(1, 768, False), (16, 768, False), (64, 256, False),

@@ -1,11 +1,11 @@
-# For the round-4 change (gemm_big chunk key (r >> 1) & 7 with an IRC_BIG_OLD_SWZ A/B build).
+# Round 4: A/B of the gemm_big chunk key (new (r >> 1) & 7 vs variants/oldswz.so).
 # gemm_big chunk key (r >> 1) & 7 vs the round-2 r & 7: GEMM / encoder / config tests, LDS
 # counters, BERT-shape A/B and the C2 / C4 step A/B on one box.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/swz
 V=$GRAFT_REPO_ROOT/information-retrieval-with-contrastive-learning_amd/irc_amd/lib/variants/oldswz.so
-timeout -k 10 500 python -u -m pytest tests/test_gemm_gpu.py tests/test_encoder_gpu.py tests/test_bert_train_gpu.py tests/test_lstm_mfma_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/swz/tests.log 2>&1 || { tail -30 gpurun_out/swz/tests.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gemm_gpu.py tests/test_encoder_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/swz/tests.log 2>&1 || { tail -30 gpurun_out/swz/tests.log; exit 1; }
 tail -1 gpurun_out/swz/tests.log
 SH=qkv,attn_out+res,ffn2+res,lstm_xp_l0,lstm_xp_l12
 for r in 1; do
@@ -29,3 +29,7 @@ cd /tmp
 timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/swz/pmc/p1 -o run -- \
   python3 $GRAFT_REPO_ROOT/tools/gemm_bench.py --iters 3 --only qkv,attn_out+res,ffn2+res > $GRAFT_REPO_ROOT/gpurun_out/swz/pmc.log 2>&1 || exit 1
 cd "$GRAFT_REPO_ROOT" && python3 tools/pmc_table.py gpurun_out/swz/pmc gemm_big
+cd /tmp
+IRC_LIB_PATH=$V timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/swz/pmc_old/p1 -o run -- \
+  python3 $GRAFT_REPO_ROOT/tools/gemm_bench.py --iters 3 --only qkv,attn_out+res,ffn2+res > $GRAFT_REPO_ROOT/gpurun_out/swz/pmc_old.log 2>&1 || exit 1
+cd "$GRAFT_REPO_ROOT" && echo "== OLD" && python3 tools/pmc_table.py gpurun_out/swz/pmc_old gemm_big
