@@ -743,7 +743,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
         for (int e = 0; e < 16; ++e) {
           const int rl = (e & 3) + 8 * (e >> 2) + 4 * h;
           float v = acc[i][j][e] * g.alpha + bv[j];
-          if (EPI == EPI_BIAS_GELU) v = gelu_fast(v);
+          if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
           st[rl * PITCH + j * 32 + r32] = v;
         }
       __builtin_amdgcn_wave_barrier();

@@ -508,8 +508,13 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
               v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * alpha + bv[j];
           }
           if (!slab && EPI == EPI_BIAS_GELU) {
-            v[0] = gelu_f2(v[0]);
-            v[1] = gelu_f2(v[1]);
+            if constexpr (sizeof(TO) == 2 || F8 == 2) {  // bf16 / MX output
+              v[0] = gelu_lite2(v[0]);
+              v[1] = gelu_lite2(v[1]);
+            } else {
+              v[0] = gelu_f2(v[0]);
+              v[1] = gelu_f2(v[1]);
+            }
           }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {

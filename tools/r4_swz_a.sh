@@ -33,3 +33,4 @@ cd /tmp
 IRC_LIB_PATH=$V timeout -s KILL 90 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/swz/pmc_old/p1 -o run -- \
   python3 $GRAFT_REPO_ROOT/tools/gemm_bench.py --iters 3 --only qkv,attn_out+res,ffn2+res > $GRAFT_REPO_ROOT/gpurun_out/swz/pmc_old.log 2>&1 || exit 1
 cd "$GRAFT_REPO_ROOT" && echo "== OLD" && python3 tools/pmc_table.py gpurun_out/swz/pmc_old gemm_big
+cd "$GRAFT_REPO_ROOT" && timeout -k 10 200 python tools/torch_gemm_ref.py > gpurun_out/swz/torch_ref.txt 2>&1; grep -v amdgpu.ids gpurun_out/swz/torch_ref.txt
