@@ -73,6 +73,16 @@ int irc_topk_merge(const float* in_score, const int64_t* in_idx, int64_t P, int6
 int irc_scan_scores(const void* queries, const void* docs, int64_t Q, int64_t N, int64_t D,
                     float* out, irc_stream_t stream);
 
+/* Smallest query batch Q for which irc_scan_topk / irc_scan_topk_fp8 run the
+ * single-pass GEMM filter (Q in [q, 256]: the 4 largest keys of every (256-doc tile,
+ * query) kept in the filter's epilogue, then an exact select over those lists that
+ * rescans any tile whose 4th key reaches the k-th; no threshold sample pass).  q > 256
+ * selects the sampled-threshold pipeline for every Q.  Same top-k either way (exact);
+ * env IRC_SCAN_PPL_MINQ sets the initial value (default 65), IRC_SCAN_PPL=0 turns it
+ * off.  Returns the previous value.  Replaces nothing in the reference: it selects
+ * between two exact implementations of evaluation.py:110-112 / tfidf_doc_ranker.py:60-75. */
+int irc_scan_set_ppl_min_q(int q);
+
 /* fp8 (e4m3fn) corpus scan: the same exact top-k as irc_scan_topk over e4m3
  * queries [Q][D] and docs [N][D] (16-byte aligned rows), products exact, fp32
  * accumulation; returned scores are the raw dot products times score_scale (a
@@ -129,8 +139,8 @@ int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M,
  * initial mode).  Returns the previous mode. */
 int irc_gemm_set_persistent(int mode);
 /* K loop of the 256 x 384 / 256 x 256 big-tile bf16 GEMM (QKV, out-proj, FFN2, the
- * LSTM input projections): 1 = a 4-slot ring of 32-deep K-tiles with three in flight
- * (the default), 0 = two 64-deep slots.  Same MFMAs in the same k order, so the
+ * LSTM input projections): 1 = a 4-slot ring of 32-deep K-tiles with three in flight,
+ * 0 = two 64-deep slots (the default).  Same MFMAs in the same k order, so the
  * results are bit-identical (env IRC_BIG_RING sets the initial value).  Returns the
  * previous setting. */
 int irc_gemm_set_big_ring(int on);

@@ -732,6 +732,111 @@ __device__ __forceinline__ void epilogue_scan(const PArgs& g, const f32x4 (&acc)
     g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = cnt[threadIdx.x];
 }
 
+// Single-pass filter epilogue (g.lists != null, no threshold): the 4 largest keys of
+// every (query, 256-doc tile), exact, for select_dense (scan_topk.hip), which rescans
+// a tile whose 4th key reaches the k-th key of all lists (the tile may hold more
+// winners).  Four passes of 64 queries: the owning group stages its 64 x 256 fp32
+// scores in LDS (row-major, 1 KB rows; column c of row r at c ^ 32 (r & 1), so the
+// readers' ds_read_b128 lane groups -- 4 rows, 4 chunks each -- cover 64 distinct
+// banks), then thread t takes query t >> 3 and the 32 docs {4 (t & 7) + 32 c + e}:
+// the top 4 of its docs by insertion in increasing doc order (strict >, so a tie keeps
+// the lower index), then three xor-shuffle rounds with its 7 neighbours (bitonic
+// 4 + 4 -> 4 under (score desc, doc asc)).  Ragged docs (>= N) never enter; padded
+// query rows (>= M) are not stored.  LDS [0, 64 KB) < PBUF, so a persistent caller's
+// prestage into buffer 1 may run meanwhile.
+__device__ __forceinline__ bool top_better(float va, int ia, float vb, int ib) {
+  return va > vb || (va == vb && ia < ib);
+}
+__device__ __forceinline__ void top_cswap(float& va, int& ia, float& vb, int& ib) {
+  const bool sw = top_better(vb, ib, va, ia);
+  const float tv = sw ? vb : va, uv = sw ? va : vb;
+  const int ti = sw ? ib : ia, ui = sw ? ia : ib;
+  va = tv; ia = ti; vb = uv; ib = ui;
+}
+template <typename Fn>
+__device__ __forceinline__ void epilogue_scan_lists(const PArgs& g, const f32x4 (&acc)[8][4],
+                                                    char* lds, int m0, int n0, int tn, int grp,
+                                                    int wn, int lane, Fn after_init) {
+  float* S = reinterpret_cast<float*>(lds);
+  after_init();
+  const int tid = threadIdx.x;
+  const int rq = tid >> 3, seg = tid & 7, flip = rq & 1;
+  const int nval = g.N - n0;  // docs of this tile
+  const float NEG = -__builtin_huge_valf();
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (grp == (p >> 1)) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 16 * ii + 4 * (lane >> 4) + e;
+            const int c = (64 * wn + 16 * j + (lane & 15)) ^ ((e & 1) << 5);
+            S[r * 256 + c] = acc[4 * (p & 1) + ii][j][e];
+          }
+    }
+    lds_barrier();
+    float tv[4] = {NEG, NEG, NEG, NEG};
+    int ti[4] = {0x7fffffff, 0x7fffffff, 0x7fffffff, 0x7fffffff};
+    const float* row = S + rq * 256 + 4 * seg;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(row + 32 * (c ^ flip));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int pos = 4 * seg + 32 * c + e;
+        const float x = pos < nval ? v[e] : NEG;
+        if (x > tv[3]) {
+          const bool c0 = x > tv[0], c1 = x > tv[1], c2 = x > tv[2];
+          tv[3] = c2 ? tv[2] : x;
+          ti[3] = c2 ? ti[2] : pos;
+          tv[2] = c1 ? tv[1] : (c2 ? x : tv[2]);
+          ti[2] = c1 ? ti[1] : (c2 ? pos : ti[2]);
+          tv[1] = c0 ? tv[0] : (c1 ? x : tv[1]);
+          ti[1] = c0 ? ti[0] : (c1 ? pos : ti[1]);
+          tv[0] = c0 ? x : tv[0];
+          ti[0] = c0 ? pos : ti[0];
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      float bv[4];
+      int bi[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bv[r] = __shfl_xor(tv[r], m, 64);
+        bi[r] = __shfl_xor(ti[r], m, 64);
+      }
+      // max of own (desc) and partner reversed (asc): a bitonic sequence holding the top 4
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (top_better(bv[3 - r], bi[3 - r], tv[r], ti[r])) {
+          tv[r] = bv[3 - r];
+          ti[r] = bi[3 - r];
+        }
+      }
+      top_cswap(tv[0], ti[0], tv[2], ti[2]);
+      top_cswap(tv[1], ti[1], tv[3], ti[3]);
+      top_cswap(tv[0], ti[0], tv[1], ti[1]);
+      top_cswap(tv[2], ti[2], tv[3], ti[3]);
+    }
+    const int q = m0 + 64 * p + rq;
+    if (seg == 0 && q < g.M) {
+      uint64_t kk[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        kk[r] = tv[r] == NEG ? 0ull : make_key(tv[r], g.idx_base + (uint32_t)(n0 + ti[r]));
+      uint64_t* dst = g.lists + ((int64_t)q * g.ls + tn) * 4;
+      reinterpret_cast<ulonglong2*>(dst)[0] = make_ulonglong2(kk[0], kk[1]);
+      reinterpret_cast<ulonglong2*>(dst)[1] = make_ulonglong2(kk[2], kk[3]);
+    }
+    lds_barrier();  // every reader is done with S before the next pass writes it
+  }
+}
+
 template <bool AK, bool BK_, typename TO, int EPI, int F8 = 0>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
@@ -774,7 +879,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   const int rbase0 = m0 + 128 * grp;
   const int cbase = n0 + 64 * wn;
   if constexpr (EPI == EPI_SCAN) {
-    epilogue_scan(g, acc, lds, m0, n0, tn, grp, wn, lane, [] {});
+    if (g.lists != nullptr)
+      epilogue_scan_lists(g, acc, lds, m0, n0, tn, grp, wn, lane, [] {});
+    else
+      epilogue_scan(g, acc, lds, m0, n0, tn, grp, wn, lane, [] {});
     return;
   }
 #ifdef IRC_PP_DIAG_NOEPI  // diagnostic build: main loop only (a guarded store of the sum of
@@ -914,7 +1022,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_pers_kernel(PArgs g, uint32_t* 
                             wq, ln);
     };
     if constexpr (EPI == EPI_SCAN) {
-      epilogue_scan(g, acc, lds, m0, n0, tn, grp, wq, ln, prestage);
+      if (g.lists != nullptr)
+        epilogue_scan_lists(g, acc, lds, m0, n0, tn, grp, wq, ln, prestage);
+      else
+        epilogue_scan(g, acc, lds, m0, n0, tn, grp, wq, ln, prestage);
     } else {
       prestage();
       epilogue_vec<TO, EPI, F8>(g, acc, lds, m0, n0, 0, grp, wq, wave, ln);

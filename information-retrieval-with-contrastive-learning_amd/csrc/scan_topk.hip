@@ -21,6 +21,7 @@
 #include <math.h>
 #include <stdio.h>
 
+#include <atomic>
 #include <cmath>
 
 #include "gemm_pp.h"
@@ -1637,12 +1638,65 @@ __device__ __forceinline__ f32x16 rescore_docs(const unsigned char* qlds,
   return tot;
 }
 
+// Score of doc dl[lane] (lanes 0-31, lane < n) against the query in qlds, as the GEMM
+// filter (gemm_pp_kernel<EPI_SCAN>, the single-pass form at Q in (64, 256]) computes
+// it: the same MFMA (v_mfma_f32_16x16x32_bf16; e4m3: v_mfma_scale_f32_16x16x128_f8f6f4
+// with unit scales), the same per-lane k chunks and the same K-tile order from a zero
+// accumulator -- bit-identical, since an output element depends only on its own row
+// and column.  All 16 A rows carry the query; docs 0-15 / 16-31 are the B columns of
+// two accumulators, and lane l reads element 0 (row 4 (l >> 4) of column l & 15) of
+// the block that holds doc l.
+template <int D, int EB>
+__device__ __forceinline__ float rescore_docs_pp(const unsigned char* qlds,
+                                                 const unsigned char* __restrict__ docs,
+                                                 const uint32_t* dl, int n, int lane) {
+  const int c = lane & 15, q4 = (lane >> 4) & 3;
+  const bool l0 = c < n, l1 = 16 + c < n;
+  const unsigned char* d0 = docs + (int64_t)(l0 ? dl[c] : 0u) * D * EB;
+  const unsigned char* d1 = docs + (int64_t)(l1 ? dl[16 + c] : 0u) * D * EB;
+  f32x4 acc0 = (f32x4)0.0f, acc1 = (f32x4)0.0f;
+  if constexpr (EB == 2) {
+#pragma unroll 4
+    for (int kt = 0; kt < D / 64; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int off = (kt * 64 + 32 * s + 8 * q4) * 2;
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(qlds + off);
+        const bf16x8 b0 = l0 ? *reinterpret_cast<const bf16x8*>(d0 + off) : (bf16x8)0;
+        const bf16x8 b1 = l1 ? *reinterpret_cast<const bf16x8*>(d1 + off) : (bf16x8)0;
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b1, acc1, 0, 0, 0);
+      }
+  } else {
+    typedef int v8i32_t __attribute__((ext_vector_type(8)));
+#pragma unroll 2
+    for (int kt = 0; kt < D / 128; ++kt) {
+      const int o0 = kt * 128 + 16 * q4, o1 = o0 + 64;
+      const u16x8 a2[2] = {*reinterpret_cast<const u16x8*>(qlds + o0),
+                           *reinterpret_cast<const u16x8*>(qlds + o1)};
+      const u16x8 z = (u16x8)0;
+      const u16x8 b02[2] = {l0 ? *reinterpret_cast<const u16x8*>(d0 + o0) : z,
+                            l0 ? *reinterpret_cast<const u16x8*>(d0 + o1) : z};
+      const u16x8 b12[2] = {l1 ? *reinterpret_cast<const u16x8*>(d1 + o0) : z,
+                            l1 ? *reinterpret_cast<const u16x8*>(d1 + o1) : z};
+      const v8i32_t av = __builtin_bit_cast(v8i32_t, a2);
+      acc0 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+          av, __builtin_bit_cast(v8i32_t, b02), acc0, 0, 0, 0, 127, 0, 127);
+      acc1 = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+          av, __builtin_bit_cast(v8i32_t, b12), acc1, 0, 0, 0, 127, 0, 127);
+    }
+  }
+  return lane < 16 ? acc0[0] : acc1[0];
+}
+
 // Tile rows covered by list `sl` of a worker (slice kh * 2 + h for KS <= 2: rows
 // (j & 3) + 8 (j >> 2) + 4 h, j in kh's share of the 16 registers; KS = 4: the merged
 // half-lane lists, rows [8 sl, 8 sl + 8)).
 template <int KS>
 __device__ __forceinline__ uint32_t list_rows(int sl) {
-  if constexpr (KS == 4) {
+  if constexpr (KS == 0) {  // GEMM-filter lists: one per 256-doc tile, every row
+    return 0xFFFFFFFFu;
+  } else if constexpr (KS == 4) {
     return 0xFFu << (8 * sl);
   } else {
     const int kh = sl >> 1, hh = sl & 1;
@@ -1653,11 +1707,13 @@ __device__ __forceinline__ uint32_t list_rows(int sl) {
   }
 }
 
+// KS = 0: the lists of the GEMM filter's single-pass form (one list per 256-doc
+// tile = worker of tpw = 8 TD-tiles; rescans with rescore_docs_pp).
 template <int D, int EB, int KS>
 __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
-  constexpr int NSL = KS == 4 ? 4 : 2 * KS;  // lists per worker
+  constexpr int NSL = KS == 0 ? 1 : (KS == 4 ? 4 : 2 * KS);  // lists per worker
   constexpr int U = SEL_STAGE / SEL_NT;
-  constexpr int MAXW = SEL_STAGE / (LT_M * 2);  // workers (NSL >= 2)
+  constexpr int MAXW = SEL_STAGE / (LT_M * NSL);  // workers
   __shared__ uint32_t hbuf[2 * SEL_NW * 256];
   __shared__ __attribute__((aligned(16))) uint64_t cand[SEL_MAXK];
   __shared__ uint64_t xk[SD_XCAP];
@@ -1775,7 +1831,19 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
           __syncthreads();
         }
         const int c = c0 + wave * TD;
-        if (c < nd) {
+        if constexpr (KS == 0) {
+          if (c < nd) {  // wave-uniform
+            const int n = nd - c < TD ? nd - c : TD;
+            const float sc = rescore_docs_pp<D, EB>(qlds, a.docs, dl + c, n, lane);
+            const uint64_t kk = lane < n ? make_key(sc, a.idx_base + dl[c + lane]) : 0ull;
+            const bool keep = kk != 0 && kk >= thr;
+            const uint64_t bal = __ballot(keep);
+            uint32_t o = 0;
+            if (lane == 0 && bal) o = atomicAdd(&s_xn, (uint32_t)__popcll(bal));
+            o = __shfl(o, 0, 64);
+            if (keep) xk[o + __popcll(bal & ((1ull << lane) - 1))] = kk;
+          }
+        } else if (c < nd) {
           const int n = nd - c < TD ? nd - c : TD;
           const f32x16 sc = rescore_docs<D, EB, KS>(qlds, a.docs, dl + c, n, lane);
           if ((lane & 31) == 0) {
@@ -1905,6 +1973,9 @@ struct Plan {
   int ls;  // lists per query
   // filter pass on the ping-pong GEMM (Q >= pp_min_q): regions = 256-doc tiles
   bool pp;
+  // single pass on the ping-pong GEMM (Q in [ppl_min_q, 256]): lists of the 4 largest
+  // keys per (256-doc tile, query), select_dense<KS = 0>; no sample, no threshold
+  bool ppl;
   int pp_G, pp_qpad;
   int64_t pp_cap;
   size_t off_thr, off_cnt, off_keys, bytes;
@@ -1953,6 +2024,20 @@ static int ltop_max_q() {
   }();
   return v;
 }
+
+// IRC_SCAN_PPL=0 disables the single-pass GEMM filter; IRC_SCAN_PPL_MINQ (default 65)
+// is its smallest Q (its largest is 256, one query tile).
+// irc_scan_set_ppl_min_q changes it at run time (the tests compare both pipelines).
+static std::atomic<int>& ppl_min_q_ref() {
+  static std::atomic<int> v{[] {
+    const char* e = getenv("IRC_SCAN_PPL");
+    if (e && e[0] == '0') return 1 << 30;
+    const char* m = getenv("IRC_SCAN_PPL_MINQ");
+    return m ? atoi(m) : 65;
+  }()};
+  return v;
+}
+static int ppl_min_q() { return ppl_min_q_ref().load(std::memory_order_relaxed); }
 
 static int pick_ks(int64_t D) { return D > 512 ? 2 : 1; }  // <= 128 fragment VGPRs/wave
 
@@ -2093,9 +2178,18 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
     if (pc > cnt_bytes) cnt_bytes = pc;
     if (pp_keys > key_bytes) key_bytes = pp_keys;
   }
+  // the single-pass GEMM filter: one query tile, every tile's list in one select stage
+  p.ppl = Q >= ppl_min_q() && Q <= 256 && N >= 256 && (eb == 2 || D % 128 == 0) &&
+          (int64_t)p.pp_G * LT_M <= SEL_STAGE && k <= SEL_NT;
+  if (p.ppl) {
+    p.pp = false;
+    p.two_phase = false;
+    const size_t lb = (size_t)Q * p.pp_G * LT_M * 8;
+    if (lb > key_bytes) key_bytes = lb;
+  }
   // LTOP where the GEMM filter does not run and all lists fit one select stage
   p.ls = p.g_f * 2 * p.ks;
-  p.ltop = !p.pp && ltop_enabled() && Q <= ltop_max_q() && (int64_t)p.ls * LT_M <= SEL_STAGE &&
+  p.ltop = !p.pp && !p.ppl && ltop_enabled() && Q <= ltop_max_q() && (int64_t)p.ls * LT_M <= SEL_STAGE &&
            k <= SEL_NT;
   if (p.ltop) {
     p.two_phase = false;
@@ -2187,6 +2281,11 @@ template <int EB>
 static void launch_dense_eb(int64_t D, int ks, int Q, const DenseArgs& a, hipStream_t st) {
 #define IRC_DENSE_CASE(DD)                                                                 \
   case DD:                                                                                 \
+    if (ks == 0) {                                                                         \
+      if constexpr (EB == 2 || DD % 128 == 0)                                              \
+        hipLaunchKernelGGL((select_dense_kernel<DD, EB, 0>), dim3((unsigned)Q), dim3(SEL_NT), 0, st, a); \
+      break;                                                                               \
+    }                                                                                      \
     if constexpr (EB == 2 && (DD == 768 || DD == 1024)) {                                  \
       if (ks == 4) {                                                                       \
         hipLaunchKernelGGL((select_dense_kernel<DD, EB, 4>), dim3((unsigned)Q), dim3(SEL_NT), 0, st, a); \
@@ -2265,6 +2364,35 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
                  out_score, out_idx};
     launch_dense(eb, D, p.ks, (int)Q, da, st);
     return check_launch("select_dense_kernel");
+  }
+  if (p.ppl) {
+    // single pass: the GEMM filter keeps the 4 largest keys of every (256-doc tile,
+    // query); select_dense takes the k-th of all lists and rescans the tiles whose
+    // 4th key reaches it
+    gpp::PArgs a{};
+    a.A = static_cast<const unsigned short*>(queries);
+    a.B = static_cast<const unsigned short*>(docs);
+    a.M = (int)Q;
+    a.N = (int)N;
+    a.K = (int)(D * eb / 2);  // 2-byte units
+    a.kchunk = a.K;
+    a.lda = a.K;
+    a.ldb = a.K;
+    a.alpha = 1.f;
+    a.qpad = p.pp_qpad;
+    a.stride = 1;
+    a.idx_base = base;
+    a.lists = keys;
+    a.ls = p.pp_G;
+    prof_begin(st);
+    gpp::run_scan(a, st, eb == 1);
+    prof_end("scan_filter", st, alg_bytes);
+    if ((rc = check_launch("gemm_pp_kernel(scan lists)"))) return rc;
+    DenseArgs da{keys, static_cast<const unsigned char*>(queries),
+                 static_cast<const unsigned char*>(docs), p.pp_G, (int)N, 256 / TD, base, (int)k,
+                 smul, out_score, out_idx};
+    launch_dense(eb, D, 0, (int)Q, da, st);
+    return check_launch("select_dense_kernel(gemm lists)");
   }
   if (p.two_phase) {
     rc = dispatch_tile<GMAX>(eb, D, p, p.g_s, queries, docs, (int)Q, p.S, p.stride, p.tpw_s,
@@ -2363,6 +2491,10 @@ extern "C" int irc_scan_rescan_stats(uint64_t* out, int reset) {
   }
   return IRC_OK;
 }
+
+// Smallest query batch of the single-pass GEMM filter (Q in [q, 256]); > 256 turns it
+// off (the sampled-threshold pipeline then runs).  Returns the previous value.
+extern "C" int irc_scan_set_ppl_min_q(int q) { return ppl_min_q_ref().exchange(q); }
 
 extern "C" int64_t irc_scan_topk_workspace(int64_t Q, int64_t N, int64_t D, int64_t k) {
   if (Q <= 0 || N <= 0 || k <= 0) return 256;
@@ -2477,7 +2609,7 @@ extern "C" int irc_scan_scores(const void* queries, const void* docs, int64_t Q,
               "scan_scores: queries and docs must be 16-byte aligned");
   if (Q == 0 || N == 0) return IRC_OK;
   Plan p = make_plan(Q, N, D, 1, 2);
-  if (p.pp) {
+  if (p.pp || p.ppl) {
     // same MFMA arithmetic as irc_scan_topk's filter on this path
     gpp::PArgs a{};
     a.A = static_cast<const unsigned short*>(queries);
@@ -2509,7 +2641,7 @@ extern "C" int irc_scan_scores_fp8(const void* queries, const void* docs, int64_
               "scan_scores_fp8: queries and docs must be 16-byte aligned");
   if (Q == 0 || N == 0) return IRC_OK;
   Plan p = make_plan(Q, N, D, 1, 1);
-  if (p.pp) {
+  if (p.pp || p.ppl) {
     // same MFMA arithmetic as irc_scan_topk_fp8's filter on this path
     gpp::PArgs a{};
     a.A = static_cast<const unsigned short*>(queries);

@@ -111,6 +111,13 @@ def scan_scores_fp8(queries: torch.Tensor, docs: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def set_single_pass_min_q(q: int) -> int:
+    """Smallest query batch of the single-pass GEMM filter (irc_scan_set_ppl_min_q:
+    Q in [q, 256]; q > 256 selects the sampled-threshold pipeline).  Both are exact.
+    Returns the previous value."""
+    return int(_lib.load().irc_scan_set_ppl_min_q(int(q)))
+
+
 def rescan_stats(reset: bool = True):
     """(queries whose single-pass select rescanned, workers rescanned) since the
     last reset -- synchronises the device (tests / diagnostics)."""

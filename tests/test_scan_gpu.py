@@ -196,7 +196,8 @@ def test_full_c2_size_properties(gpu):
 
 
 @pytest.mark.parametrize("Q,D,fp8", [(1, 768, False), (16, 768, False), (64, 256, False),
-                                      (40, 768, True)])
+                                      (40, 768, True), (128, 768, False), (256, 768, False),
+                                      (200, 768, True)])
 def test_clustered_corpus_rescan_properties(gpu, Q, D, fp8):
     """A block of 600 consecutive docs aligned with the queries: ~25 winners per
     worker there, so the single-pass scan's 4-key lists overflow and
@@ -293,7 +294,8 @@ def test_graphed_search_many_survives_workspace_growth(gpu):
 
 
 @pytest.mark.parametrize("Q,D,fp8", [(1, 768, False), (16, 768, False), (64, 1024, False),
-                                      (32, 768, True)])
+                                      (32, 768, True), (128, 768, False), (256, 768, False),
+                                      (256, 1024, False), (200, 768, True)])
 def test_rescan_bit_exact_vs_oracle_on_grid(gpu, Q, D, fp8):
     """the single-pass scan's rescan path pinned to
     the oracle.  Integer-grid corpus (every score exact in fp32 in any order) with
@@ -312,6 +314,8 @@ def test_rescan_bit_exact_vs_oracle_on_grid(gpu, Q, D, fp8):
     docs = rng.integers(-2, 3, (N, D))
     docs[lo:lo + 600] = base + rng.integers(-3, 4, (600, D))
     qs = base + rng.integers(-3, 4, (Q, D))
+    # Q > 64: the single-pass GEMM filter (4-key lists per 256-doc tile, rescans
+    # with its own 16x16x32 MFMA sequence)
     d = (docs / step).astype(np.float32)
     q = (qs / step).astype(np.float32)
     retrieval.rescan_stats(reset=True)
@@ -329,3 +333,40 @@ def test_rescan_bit_exact_vs_oracle_on_grid(gpu, Q, D, fp8):
     np.testing.assert_array_equal(i.cpu().numpy(), ri)
     np.testing.assert_array_equal(s.cpu().numpy(), rs)
     assert ((ri >= lo + 3) & (ri < lo + 603)).all()
+
+
+@pytest.mark.parametrize("Q,fp8", [(192, False), (256, False), (256, True)])
+def test_single_pass_gemm_filter_equals_sampled_pipeline(gpu, Q, fp8):
+    """Q >= 192 runs the GEMM filter either way: the single-pass form (lists + select
+    with rescans) and the sampled-threshold form (sample pass, threshold select,
+    threshold epilogue, region select) score with the same MFMAs, so their results
+    are equal bit for bit -- on a Gaussian corpus and on the adversarial sorted one
+    (huge tie groups: every tile's list truncated)."""
+    from irc_amd import retrieval
+
+    g = torch.Generator().manual_seed(Q)
+    N, D, k = 50_000, 768, 100
+    q = torch.nn.functional.normalize(torch.randn(Q, D, generator=g))
+    d = torch.nn.functional.normalize(torch.randn(N, D, generator=g))
+    ds = torch.zeros(N, D)
+    ds[:, 0] = (torch.arange(N) % 256) / 128.0 - 1.0
+    qs = torch.zeros(Q, D)
+    qs[:, 0] = 1.0
+    qs[::2, 1] = 0.5
+    for qq, dd in ((q, d), (qs, ds)):
+        outs = []
+        prev = retrieval.set_single_pass_min_q(65)
+        try:
+            for mq in (65, 1 << 20):
+                retrieval.set_single_pass_min_q(mq)
+                if fp8:
+                    q8 = retrieval.quantize_fp8(qq.to(gpu))
+                    d8 = retrieval.quantize_fp8(dd.to(gpu))
+                    outs.append(retrieval.scan_topk_fp8(q8, d8, k, 11, 1.0 / 256))
+                else:
+                    outs.append(retrieval.scan_topk(qq.bfloat16().to(gpu),
+                                                    dd.bfloat16().to(gpu), k, 11))
+            torch.cuda.synchronize()
+        finally:
+            retrieval.set_single_pass_min_q(prev)
+        assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][0], outs[1][0])
