@@ -28,9 +28,10 @@ struct PArgs {
   int qpad;
   int stride;
   uint32_t idx_base;
-  // single-pass scan filter (EPI_SCAN with lists != null, no threshold): the 4
-  // largest keys of each (256-doc tile tn, query q) go to lists[(q * ls + tn) * 4 + i],
-  // in descending order, 0 for empty slots (select_dense reads them)
+  // scan filter lists (EPI_SCAN with lists != null, no threshold): the 4 largest keys
+  // of each (256-doc tile tn, query q) go to lists[(q * ls + tn) * 4 + i], in
+  // descending order, 0 for empty slots (the single pass: select_dense reads them;
+  // the threshold sample: lists_kth_kernel)
   uint64_t* lists;
   int ls;
   // fp8 linear layers (F8, non-scan epilogues): C = alpha * (A8 . B8^T) * sa[row]

@@ -742,7 +742,8 @@ __device__ __forceinline__ void epilogue_scan(const PArgs& g, const f32x4 (&acc)
 // the top 4 of its docs by insertion in increasing doc order (strict >, so a tie keeps
 // the lower index), then three xor-shuffle rounds with its 7 neighbours (bitonic
 // 4 + 4 -> 4 under (score desc, doc asc)).  Ragged docs (>= N) never enter; padded
-// query rows (>= M) are not stored.  LDS [0, 64 KB) < PBUF, so a persistent caller's
+// query rows (>= M) are not stored.  Doc d's global index is idx_base + d * stride
+// (stride > 1: the threshold sample of the sampled pipeline, B rows ldb apart).  LDS [0, 64 KB) < PBUF, so a persistent caller's
 // prestage into buffer 1 may run meanwhile.
 __device__ __forceinline__ bool top_better(float va, int ia, float vb, int ib) {
   return va > vb || (va == vb && ia < ib);
@@ -828,7 +829,8 @@ __device__ __forceinline__ void epilogue_scan_lists(const PArgs& g, const f32x4 
       uint64_t kk[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        kk[r] = tv[r] == NEG ? 0ull : make_key(tv[r], g.idx_base + (uint32_t)(n0 + ti[r]));
+        kk[r] = tv[r] == NEG ? 0ull
+                             : make_key(tv[r], g.idx_base + (uint32_t)(n0 + ti[r]) * (uint32_t)g.stride);
       uint64_t* dst = g.lists + ((int64_t)q * g.ls + tn) * 4;
       reinterpret_cast<ulonglong2*>(dst)[0] = make_ulonglong2(kk[0], kk[1]);
       reinterpret_cast<ulonglong2*>(dst)[1] = make_ulonglong2(kk[2], kk[3]);

@@ -1954,6 +1954,31 @@ static void launch_select(const RegionSource& src, int Q, int k, int mode, uint6
                          src, k, mode, thr, out_score, out_idx, smul);
 }
 
+// Threshold of the sampled pipeline from the GEMM kernel's sample lists (the 4
+// largest keys of every (256-doc sample tile, query)): thr[q] = the exact k-th largest
+// nonzero key of the query's LS * 4 list keys -- real keys of k distinct docs, so a
+// lower bound of the true k-th key -- or 0 (admit everything) when there are <= k.
+__global__ __launch_bounds__(SEL_NT) void lists_kth_kernel(const uint64_t* __restrict__ lists,
+                                                           int LS, int k, uint64_t* thr) {
+  constexpr int U = SEL_STAGE / SEL_NT;
+  __shared__ uint32_t hbuf[2 * SEL_NW * 256];
+  __shared__ uint64_t s_mm[3 * SEL_NW];
+  __shared__ uint32_t s_cnt[2 * SEL_NW];
+  __shared__ uint32_t s_misc[4];
+  const int q = blockIdx.x, tid = threadIdx.x;
+  const int M4 = LS * LT_M;
+  const uint64_t* L = lists + (int64_t)q * M4;
+  uint64_t v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = tid + u * SEL_NT;
+    v[u] = i < M4 ? L[i] : 0ull;
+  }
+  uint32_t M = 0;
+  const uint64_t kth = dense_kth<U>(v, nullptr, 0, k, hbuf, s_mm, s_cnt, s_misc, &M);
+  if (tid == 0) thr[q] = kth;
+}
+
 // ------------------------------------------------------------------ planning
 struct Plan {
   int nw;  // waves = nq * ks
@@ -1976,6 +2001,7 @@ struct Plan {
   // single pass on the ping-pong GEMM (Q in [ppl_min_q, 256]): lists of the 4 largest
   // keys per (256-doc tile, query), select_dense<KS = 0>; no sample, no threshold
   bool ppl;
+  int pp_sG;  // 256-doc tiles of the threshold sample on the GEMM kernel (pp two-phase)
   int pp_G, pp_qpad;
   int64_t pp_cap;
   size_t off_thr, off_cnt, off_keys, bytes;
@@ -2038,6 +2064,16 @@ static std::atomic<int>& ppl_min_q_ref() {
   return v;
 }
 static int ppl_min_q() { return ppl_min_q_ref().load(std::memory_order_relaxed); }
+
+// IRC_SCAN_PP_SAMPLE=0: the sampled pipeline's threshold pass stays on the tile kernel
+// (GMAX) where the filter runs on the GEMM kernel (A/B; default: the GEMM kernel).
+static bool pp_sample_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("IRC_SCAN_PP_SAMPLE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
 
 static int pick_ks(int64_t D) { return D > 512 ? 2 : 1; }  // <= 128 fragment VGPRs/wave
 
@@ -2173,6 +2209,11 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   // the GEMM-kernel filter: bf16, or fp8 with 128-byte K-tiles (D % 128 == 0)
   p.pp = (eb == 2 || D % 128 == 0) && Q >= pp_min_q() && N >= 256 &&
          pp_keys <= pp_max_bytes() && p.pp_G <= SEL_MAXR;
+  p.pp_sG = (int)((p.S + 255) / 256);
+  if (p.pp && p.two_phase) {  // the GEMM sample's lists share the survivor key buffer
+    const size_t sb = (size_t)Q * p.pp_sG * LT_M * 8;
+    if (sb > key_bytes) key_bytes = sb;
+  }
   if (p.pp) {
     const size_t pc = (size_t)p.pp_G * p.pp_qpad * 4;
     if (pc > cnt_bytes) cnt_bytes = pc;
@@ -2394,7 +2435,32 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
     launch_dense(eb, D, 0, (int)Q, da, st);
     return check_launch("select_dense_kernel(gemm lists)");
   }
-  if (p.two_phase) {
+  if (p.two_phase && p.pp && pp_sample_enabled() && p.pp_sG * LT_M <= SEL_STAGE) {
+    // threshold sample on the GEMM kernel: the sample docs (every stride-th row) as B
+    // with row stride ldb = stride * D, the 4 largest keys per (256-doc sample tile,
+    // query) kept, thr[q] = their k-th.  (The tile kernel's GMAX pass ran at ~0.05 of
+    // the MFMA peak at Q = 2048: 699 us of a 3.3 ms C4 call, profiles/r03_scan_p_kernels.txt.)
+    gpp::PArgs a{};
+    a.A = static_cast<const unsigned short*>(queries);
+    a.B = static_cast<const unsigned short*>(docs);
+    a.M = (int)Q;
+    a.N = (int)p.S;
+    a.K = (int)(D * eb / 2);  // 2-byte units
+    a.kchunk = a.K;
+    a.lda = a.K;
+    a.ldb = (int64_t)a.K * p.stride;
+    a.alpha = 1.f;
+    a.qpad = p.pp_qpad;
+    a.stride = (int)p.stride;
+    a.idx_base = base;
+    a.lists = keys;
+    a.ls = p.pp_sG;
+    gpp::run_scan(a, st, eb == 1);
+    if ((rc = check_launch("gemm_pp_kernel(scan sample)"))) return rc;
+    hipLaunchKernelGGL(lists_kth_kernel, dim3((unsigned)Q), dim3(SEL_NT), 0, st, keys, p.pp_sG,
+                       (int)k, thr);
+    if ((rc = check_launch("lists_kth_kernel"))) return rc;
+  } else if (p.two_phase) {
     rc = dispatch_tile<GMAX>(eb, D, p, p.g_s, queries, docs, (int)Q, p.S, p.stride, p.tpw_s,
                              base, nullptr, keys, cnt, p.cap_s, nullptr, st);
     if (rc) return rc;

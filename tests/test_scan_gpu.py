@@ -108,6 +108,17 @@ def test_adversarial_sorted_corpus_gemm_filter(gpu):
     _check_sorted_corpus(gpu, q, N, D, k)
 
 
+def test_adversarial_sorted_corpus_gemm_sample(gpu):
+    """Q = 300 (two query tiles): the sampled pipeline with its threshold sample on the
+    GEMM kernel (4-key lists per 256-doc sample tile, k-th of the lists): whole
+    regions survive the threshold, the selection must still be exact."""
+    N, D, k = 50000, 128, 100
+    q = np.zeros((300, D), np.float32)
+    q[:, 0] = 1.0
+    q[::3, 1] = 0.5
+    _check_sorted_corpus(gpu, q, N, D, k)
+
+
 def _check_sorted_corpus(gpu, q, N, D, k):
     from irc_amd import retrieval
 

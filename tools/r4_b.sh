@@ -8,6 +8,13 @@ timeout -k 10 600 python -u -m pytest tests/test_scan_gpu.py tests/test_scan_fp8
 tail -2 gpurun_out/r4b/tests.log
 timeout -k 10 300 python tools/scan_ppl_ab.py > gpurun_out/r4b/ppl_ab.txt 2>&1 || { tail -20 gpurun_out/r4b/ppl_ab.txt; exit 1; }
 grep -v amdgpu.ids gpurun_out/r4b/ppl_ab.txt
+for fp8 in "" "--fp8"; do
+  for smp in 1 0; do
+    D=1024; [ -n "$fp8" ] && D=768
+    IRC_SCAN_PP_SAMPLE=$smp timeout -k 10 200 python tools/scan_call_prof.py --n 625000 --d $D --q 2048 $fp8 > gpurun_out/r4b/c45_$smp$fp8.txt 2>&1 || exit 1
+    echo "pp_sample=$smp $(grep -v amdgpu.ids gpurun_out/r4b/c45_$smp$fp8.txt)"
+  done
+done
 SH=qkv,attn_out+res,ffn1+gelu,ffn1+bias,ffn2+res,lstm_xp_l0,square4k
 timeout -k 10 200 python tools/gemm_bench.py --only $SH > gpurun_out/r4b/gemm_new.txt 2>&1 || exit 1
 IRC_LIB_PATH=$V timeout -k 10 200 python tools/gemm_bench.py --only $SH > gpurun_out/r4b/gemm_old.txt 2>&1 || exit 1
