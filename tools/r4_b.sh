@@ -4,7 +4,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r4b
 V=$GRAFT_REPO_ROOT/information-retrieval-with-contrastive-learning_amd/irc_amd/lib/variants/oldswz.so
-timeout -k 10 600 python -u -m pytest tests/test_scan_gpu.py tests/test_scan_fp8_gpu.py tests/test_gemm_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r4b/tests.log 2>&1 || { tail -40 gpurun_out/r4b/tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_scan_gpu.py tests/test_scan_fp8_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r4b/tests.log 2>&1 || { tail -40 gpurun_out/r4b/tests.log; exit 1; }
 tail -2 gpurun_out/r4b/tests.log
 timeout -k 10 300 python tools/scan_ppl_ab.py > gpurun_out/r4b/ppl_ab.txt 2>&1 || { tail -20 gpurun_out/r4b/ppl_ab.txt; exit 1; }
 grep -v amdgpu.ids gpurun_out/r4b/ppl_ab.txt
@@ -16,7 +16,7 @@ for fp8 in "" "--fp8"; do
   done
 done
 SH=qkv,attn_out+res,ffn1+gelu,ffn1+bias,ffn2+res,lstm_xp_l0,square4k
-timeout -k 10 200 python tools/gemm_bench.py --only $SH > gpurun_out/r4b/gemm_new.txt 2>&1 || exit 1
+timeout -k 10 200 python tools/gemm_bench.py --only $SH --duo ab > gpurun_out/r4b/gemm_new.txt 2>&1 || exit 1
 IRC_LIB_PATH=$V timeout -k 10 200 python tools/gemm_bench.py --only $SH > gpurun_out/r4b/gemm_old.txt 2>&1 || exit 1
 for f in gemm_new gemm_old; do echo "== $f"; grep -v amdgpu.ids gpurun_out/r4b/$f.txt; done
 timeout -k 10 200 python tools/torch_gemm_ref.py > gpurun_out/r4b/torch_ref.txt 2>&1; grep -v amdgpu.ids gpurun_out/r4b/torch_ref.txt
