@@ -366,7 +366,9 @@ __global__ __launch_bounds__(NT) void gemm_kernel(Args g) {
         const int row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (row >= g.M) continue;
         float v = acc[i][j][e] * g.alpha + bv;
-        if (EPI == EPI_BIAS_GELU) v = gelu_erf(v);
+        // bf16 outputs: the same GELU as every other bf16 epilogue (the kernel choice
+        // must not change the result beyond fp32 reassociation)
+        if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_erf(v);
         if (EPI == EPI_BIAS_GELU_SAVE) {
           TO* pre = const_cast<TO*>(R) + (int64_t)row * g.ldr + col;
           if constexpr (sizeof(TO) == 2)
@@ -835,7 +837,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
         const int row = m0 + wm * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (row >= g.M) continue;
         float v = acc[i][j][e] * g.alpha + bv;
-        if (EPI == EPI_BIAS_GELU) v = gelu_fast(v);
+        if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
         if (EPI == EPI_BIAS_GELU_SAVE) {
           TO* pre = const_cast<TO*>(R) + (int64_t)row * g.ldr + col;
           if constexpr (sizeof(TO) == 2)

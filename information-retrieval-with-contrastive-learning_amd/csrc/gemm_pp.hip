@@ -918,7 +918,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
         const int row = rbase0 + 16 * i + 4 * (lane >> 4) + e;
         if (row >= g.M) continue;
         float v = acc[i][j][e] * g.alpha + bvv;
-        if (EPI == EPI_BIAS_GELU) v = gelu_f(v);
+        if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_f(v);
         if (EPI == EPI_BIAS_GELU_SAVE) {
           TO* pre = const_cast<TO*>(R) + (int64_t)row * g.ldr + col;
           if constexpr (sizeof(TO) == 2)
