@@ -144,13 +144,6 @@ int irc_gemm_set_persistent(int mode);
  * results are bit-identical (env IRC_BIG_RING sets the initial value).  Returns the
  * previous setting. */
 int irc_gemm_set_big_ring(int on);
-/* Experimental: 1 routes the bf16-output GEMMs with A [M][K], B [N][K] (one batch,
- * epilogues 0-4, aligned, K % 32 == 0, >= 4 tiles per CU) to a two-workgroups-per-CU
- * kernel of 128 x 256 tiles, whose epilogues overlap the partner workgroup's MFMAs;
- * 0 (the default) keeps the one-workgroup-per-CU kernels.  Same operation (the
- * nn.Linear calls of contrastive_module.py:39 -> HF BertModel); results agree within
- * fp32 reassociation.  Env IRC_GEMM_DUO sets the initial value.  Returns the previous. */
-int irc_gemm_set_duo(int on);
 
 /* ------------------------------------------------------------- BERT encoder
  * Frozen BERT forward pieces (contrastive_module.py:36-41 -> HF BertModel):

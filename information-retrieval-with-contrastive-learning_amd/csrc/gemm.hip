@@ -966,16 +966,6 @@ static int gemm_group_m() {
   return gm;
 }
 
-// IRC_GEMM_DUO=1 (or irc_gemm_set_duo) routes the bf16-out NT GEMMs that qualify to the
-// two-workgroups-per-CU kernel (gemm_duo.hip; experimental, off by default).
-static std::atomic<int>& duo_mode() {
-  static std::atomic<int> m{[] {
-    const char* e = getenv("IRC_GEMM_DUO");
-    return (e && e[0] == '1') ? 1 : 0;
-  }()};
-  return m;
-}
-
 // IRC_GEMM_PP=0 disables the ping-pong path (A/B experiments; read once).
 static bool pp_enabled() {
   static const bool on = [] {
@@ -994,10 +984,6 @@ extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue,
   }
   return s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
 }
-
-// Two-workgroups-per-CU GEMM (gemm_duo.hip) for the shapes that qualify (1) or not (0,
-// the default); returns the previous setting.
-extern "C" int irc_gemm_set_duo(int on) { return duo_mode().exchange(on ? 1 : 0); }
 
 // 4-slot ring (1) or 2-slot loop (0, the default: the ring measured no faster on
 // the BERT shapes, profiles/r03_ring_r_*) of the 256-row big-tile GEMM; returns the
@@ -1046,18 +1032,6 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
                gemm_group_m()};
   hipStream_t st = as_stream(stream);
   const int nb = (int)batch;
-  if (in_dtype == 0 && duo_mode().load(std::memory_order_relaxed) &&
-      gpp::duo_qualifies(a_layout, b_layout, epilogue, out_dtype, accumulate, M, N, K, A, lda, B,
-                         ldb, C, ldc, R, ldr, batch)) {
-    prof_begin(st);
-    gpp::duo_run(epilogue, static_cast<const unsigned short*>(A), lda,
-                 static_cast<const unsigned short*>(B), ldb, static_cast<unsigned short*>(C), ldc,
-                 bias, static_cast<const unsigned short*>(R), ldr, (int)M, (int)N, (int)K, alpha,
-                 st);
-    prof_end("gemm_bf16", st, 2.0 * M * N * K * batch);
-    prof_work("gemm_bf16_bytes", gemm::gemm_alg_bytes(0, epilogue, 0, M, N, K, batch));
-    return check_launch("gemm_duo_kernel");
-  }
   if (in_dtype == 0 && pp_enabled()) {
     int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch);
     if (sp > 1 && (workspace == nullptr ||

@@ -69,13 +69,5 @@ void run_fp8(int epi, const PArgs& a, hipStream_t st);
 // GELU / residual); bf16 C, or MX-fp8 C when a.cx != null (epilogues 1, 2 only)
 void run_mx(int epi, const PArgs& a, hipStream_t st);
 
-// Two-workgroups-per-CU bf16 GEMM (gemm_duo.hip; experimental, irc_gemm_set_duo)
-bool duo_qualifies(int la, int lb, int epi, int out_f32, int accumulate, int64_t M, int64_t N,
-                   int64_t K, const void* A, int64_t lda, const void* B, int64_t ldb,
-                   const void* C, int64_t ldc, const void* R, int64_t ldr, int64_t batch);
-void duo_run(int epi, const unsigned short* A, int64_t lda, const unsigned short* B, int64_t ldb,
-             unsigned short* C, int64_t ldc, const float* bias, const unsigned short* R,
-             int64_t ldr, int M, int N, int K, float alpha, hipStream_t st);
-
 }  // namespace gpp
 }  // namespace irc

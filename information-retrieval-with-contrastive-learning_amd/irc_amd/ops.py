@@ -33,12 +33,6 @@ def gemm_set_big_ring(on) -> int:
     return int(_lib.load().irc_gemm_set_big_ring(1 if on else 0))
 
 
-def gemm_set_duo(on) -> int:
-    """Experimental two-workgroups-per-CU kernel for the bf16 NT GEMMs that qualify
-    (irc_gemm_set_duo).  Returns the previous setting."""
-    return int(_lib.load().irc_gemm_set_duo(1 if on else 0))
-
-
 def gemm_set_persistent(mode) -> int:
     """Persistent tile loop of the 256x256 bf16 GEMM (irc_gemm_set_persistent): 0 off
     (the default), 1 / True dynamic tiles with the next tile's first K-tile prestaged

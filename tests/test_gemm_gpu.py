@@ -242,34 +242,6 @@ def test_gelu_bf16_epilogue_matches_exact_erf_gelu(gpu, M, N):
     assert (ulps[big] == 0).float().mean().item() >= 0.95
 
 
-@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
-@pytest.mark.parametrize("M,N,K", [(4096, 3072, 768), (16384, 2048, 1024), (20000, 2304, 96)])
-def test_duo_kernel_exact(gpu, epi, M, N, K):
-    """The experimental two-workgroups-per-CU kernel (irc_gemm_set_duo): small-integer
-    operands, bias and residual make every product and sum exact in fp32, so its output
-    must equal the default kernels' bit for bit (GELU: the same gelu_lite2 of the same
-    exact pre-activation), on the BERT FFN1 shape, a K = 1024 shape and a ragged M with
-    K = 96 (>= 4 tiles of 128 x 256 per CU: the shapes the kernel takes)."""
-    from irc_amd import ops
-
-    g = torch.Generator().manual_seed(M + N + K + epi)
-    a = torch.randint(-4, 5, (M, K), generator=g).to(torch.bfloat16).to(gpu)
-    b = torch.randint(-4, 5, (N, K), generator=g).to(torch.bfloat16).to(gpu)
-    bias = (torch.randint(-8, 9, (N,), generator=g).float() / 4).to(gpu) if epi in (1, 2, 3) else None
-    res = torch.randint(-8, 9, (M, N), generator=g).to(torch.bfloat16).to(gpu) if epi in (3, 4) else None
-    outs = []
-    prev = ops.gemm_set_duo(False)
-    try:
-        for duo in (False, True):
-            ops.gemm_set_duo(duo)
-            outs.append(ops.gemm(a, b, bias=bias, epilogue=epi, residual=res,
-                                 out_dtype=torch.bfloat16))
-        torch.cuda.synchronize()
-    finally:
-        ops.gemm_set_duo(prev)
-    assert torch.equal(outs[0], outs[1])
-
-
 # ---- the 256x256 ping-pong path (gemm_pp.hip): shapes with >= 32 output tiles
 @pytest.mark.parametrize("trans_a,b_is_nk", [(False, True), (False, False), (True, True),
                                              (True, False)])

@@ -46,7 +46,6 @@ def main():
     ap.add_argument("--layouts", action="store_true")
     ap.add_argument("--only", default="", help="comma-separated shape names")
     ap.add_argument("--mx", action="store_true", help="MX-fp8 GEMMs (irc_gemm_mx) of the BERT shapes")
-    ap.add_argument("--duo", default="0", help="irc_gemm_set_duo: 0, 1, or 'ab' (both, interleaved)")
     args = ap.parse_args()
     only = set(filter(None, args.only.split(",")))
     if args.mx:
@@ -107,24 +106,19 @@ def main():
         if res is not None:
             res = res.to(od)
         out = torch.empty((M, N), device=dev, dtype=od)
-        modes = (0, 1, 0, 1) if args.duo == "ab" else (int(args.duo),)
-        for mode in modes:
-            ops.gemm_set_duo(mode)
-            for _ in range(3):
-                ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
-            st = torch.cuda.current_stream()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            for _ in range(args.iters):
-                ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
-            e1.record(st)
-            torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / args.iters
-            tf = 2.0 * M * N * K / us / 1e6
-            tag = f" duo={mode}" if args.duo != "0" else ""
-            print(f"{name:14s} M={M:6d} N={N:5d} K={K:5d} epi={epi}{tag}  {us:9.1f} us  {tf:7.1f} "
-                  f"TF/s  {tf / 2500:.1%}", flush=True)
-        ops.gemm_set_duo(0)
+        for _ in range(3):
+            ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(args.iters):
+            ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
+        e1.record(st)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / args.iters
+        tf = 2.0 * M * N * K / us / 1e6
+        print(f"{name:14s} M={M:6d} N={N:5d} K={K:5d} epi={epi}  {us:9.1f} us  {tf:7.1f} TF/s  "
+              f"{tf / 2500:.1%}", flush=True)
 
 
 def mx_shapes(args):
