@@ -78,8 +78,8 @@ int irc_scan_scores(const void* queries, const void* docs, int64_t Q, int64_t N,
  * query) kept in the filter's epilogue, then an exact select over those lists that
  * rescans any tile whose 4th key reaches the k-th; no threshold sample pass).  q > 256
  * selects the sampled-threshold pipeline for every Q.  Same top-k either way (exact);
- * env IRC_SCAN_PPL_MINQ sets the initial value (default 65), IRC_SCAN_PPL=0 turns it
- * off.  Returns the previous value.  Replaces nothing in the reference: it selects
+ * env IRC_SCAN_PPL_MINQ sets the initial value (default: off, 2^30), IRC_SCAN_PPL=0
+ * turns it off.  Returns the previous value.  Replaces nothing in the reference: it selects
  * between two exact implementations of evaluation.py:110-112 / tfidf_doc_ranker.py:60-75. */
 int irc_scan_set_ppl_min_q(int q);
 

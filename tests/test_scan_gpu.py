@@ -14,6 +14,24 @@ from oracle import irc_oracle as O
 pytestmark = pytest.mark.gpu
 
 
+class _single_pass:
+    """Enable the single-pass GEMM filter (off by default) for Q > 64 inside a test."""
+
+    def __init__(self, on=True):
+        self.on = on
+
+    def __enter__(self):
+        from irc_amd import retrieval
+
+        self.prev = retrieval.set_single_pass_min_q(65 if self.on else 1 << 30)
+
+    def __exit__(self, *exc):
+        from irc_amd import retrieval
+
+        torch.cuda.synchronize()
+        retrieval.set_single_pass_min_q(self.prev)
+
+
 def _grid(rng, shape, lim=127):
     return rng.integers(-lim, lim + 1, shape).astype(np.float32) / 128
 
@@ -85,6 +103,24 @@ def test_topk_exact_vs_oracle(gpu, Q, N, D, k, off):
     q = _grid(rng, (Q, D), 3)  # small range -> many exact ties
     d = _grid(rng, (N, D), 3)
     s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), k, off)
+    ri, rs = O.scan_topk(q, d, k, doc_offset=off)
+    np.testing.assert_array_equal(i.cpu().numpy(), ri)
+    np.testing.assert_array_equal(s.cpu().numpy(), rs)
+
+
+@pytest.mark.parametrize("Q,N,D,k,off", [(128, 60000, 768, 100, 0), (256, 50000, 128, 256, 5),
+                                         (100, 9000, 512, 50, 1), (256, 4099, 64, 100, 2)])
+def test_topk_exact_vs_oracle_single_pass(gpu, Q, N, D, k, off):
+    """The single-pass GEMM filter (4-key lists per 256-doc tile + select_dense with
+    rescans), enabled explicitly (off by default), bit-exact against the oracle on
+    integer grids with many exact ties."""
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(Q * 11 + N)
+    q = _grid(rng, (Q, D), 3)
+    d = _grid(rng, (N, D), 3)
+    with _single_pass():
+        s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), k, off)
     ri, rs = O.scan_topk(q, d, k, doc_offset=off)
     np.testing.assert_array_equal(i.cpu().numpy(), ri)
     np.testing.assert_array_equal(s.cpu().numpy(), rs)
@@ -223,15 +259,16 @@ def test_clustered_corpus_rescan_properties(gpu, Q, D, fp8):
     q = unit(base + 0.5 * unit(torch.randn(Q, D, generator=g)))
     d = unit(torch.randn(N, D, generator=g))
     d[17_000:17_600] = unit(base + 0.5 * unit(torch.randn(600, D, generator=g)))
-    if fp8:
-        qq = retrieval.quantize_fp8(q.to(gpu))
-        dd = retrieval.quantize_fp8(d.to(gpu))
-        s, i = retrieval.scan_topk_fp8(qq, dd, k, 0, 1.0 / 256)
-        full = retrieval.scan_scores_fp8(qq, dd) * (1.0 / 256)
-    else:
-        qq, dd = q.bfloat16().to(gpu), d.bfloat16().to(gpu)
-        s, i = retrieval.scan_topk(qq, dd, k)
-        full = retrieval.scan_scores(qq, dd)
+    with _single_pass(Q > 64):  # Q > 64: the single-pass GEMM filter and its rescans
+        if fp8:
+            qq = retrieval.quantize_fp8(q.to(gpu))
+            dd = retrieval.quantize_fp8(d.to(gpu))
+            s, i = retrieval.scan_topk_fp8(qq, dd, k, 0, 1.0 / 256)
+            full = retrieval.scan_scores_fp8(qq, dd) * (1.0 / 256)
+        else:
+            qq, dd = q.bfloat16().to(gpu), d.bfloat16().to(gpu)
+            s, i = retrieval.scan_topk(qq, dd, k)
+            full = retrieval.scan_scores(qq, dd)
     assert bool((i >= 0).all()) and bool((i < N).all())
     assert bool(((i >= 17_000) & (i < 17_600)).all())  # the block wins
     assert torch.equal(s, torch.gather(full, 1, i))
@@ -330,15 +367,16 @@ def test_rescan_bit_exact_vs_oracle_on_grid(gpu, Q, D, fp8):
     d = (docs / step).astype(np.float32)
     q = (qs / step).astype(np.float32)
     retrieval.rescan_stats(reset=True)
-    if fp8:
-        q8, d8 = O.quantize_e4m3(q), O.quantize_e4m3(d)
-        assert np.array_equal(O.dequantize_e4m3(d8), d)  # the grid is e4m3-exact
-        s, i = retrieval.scan_topk_fp8(_dev(q8, gpu), _dev(d8, gpu), k, 3, 1.0 / 256)
-        ri, rs = O.scan_topk_fp8(q8, d8, k, doc_offset=3, score_scale=1.0 / 256)
-    else:
-        s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), k, 3)
-        ri, rs = O.scan_topk(q, d, k, doc_offset=3)
-    nq, nw = retrieval.rescan_stats(reset=True)
+    with _single_pass(Q > 64):
+        if fp8:
+            q8, d8 = O.quantize_e4m3(q), O.quantize_e4m3(d)
+            assert np.array_equal(O.dequantize_e4m3(d8), d)  # the grid is e4m3-exact
+            s, i = retrieval.scan_topk_fp8(_dev(q8, gpu), _dev(d8, gpu), k, 3, 1.0 / 256)
+            ri, rs = O.scan_topk_fp8(q8, d8, k, doc_offset=3, score_scale=1.0 / 256)
+        else:
+            s, i = retrieval.scan_topk(_dev(q, gpu), _dev(d, gpu), k, 3)
+            ri, rs = O.scan_topk(q, d, k, doc_offset=3)
+        nq, nw = retrieval.rescan_stats(reset=True)
     print(f"Q={Q} D={D} fp8={fp8}: {nq} queries rescanned, {nw} workers")
     assert nq >= 1 and nw >= nq  # the block's truncated lists forced rescans
     np.testing.assert_array_equal(i.cpu().numpy(), ri)
