@@ -722,8 +722,33 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
       const int col = cbase + j * 32 + r32;
       bv[j] = epi_has_bias(EPI) && col < g.N ? bias[col] : 0.f;
     }
+#ifdef IRC_BIG_RPRE2  // A/B build: residual rows of pass i + 1 loaded during pass i
+    constexpr int CPRR2 = WCOLS / 8, NRR2 = 32 * CPRR2 / 64;
+    constexpr bool RES2 = sizeof(TO) == 2 && (EPI == EPI_BIAS_RESID || EPI == EPI_RESID);
+    u16x8 rnext[NRR2];
+    auto rload = [&](int i, u16x8 (&dst)[NRR2]) {
+#pragma unroll
+      for (int it = 0; it < NRR2; ++it) {
+        const int c = it * 64 + lane;
+        const int row = rbase0 + i * 32 + c / CPRR2, col = cbase + (c % CPRR2) * 8;
+        dst[it] = (row < g.M && col < g.N)
+                      ? *reinterpret_cast<const u16x8*>(
+                            reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col)
+                      : (u16x8)0;
+      }
+    };
+    if constexpr (RES2) rload(0, rnext);
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
+#ifdef IRC_BIG_RPRE2
+      u16x8 rpre[NRR2];
+      if constexpr (RES2) {
+#pragma unroll
+        for (int it = 0; it < NRR2; ++it) rpre[it] = rnext[it];
+        if (i + 1 < 4) rload(i + 1, rnext);
+      }
+#endif
 #ifdef IRC_BIG_RPRE  // A/B build: the pass's residual rows loaded before its LDS staging
       constexpr int CPRR = WCOLS / 8, NRR = 32 * CPRR / 64;
       u16x8 rpre[NRR];
@@ -763,7 +788,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
           const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c8 + 4]);
           float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
           if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
-#ifdef IRC_BIG_RPRE
+#if defined(IRC_BIG_RPRE) || defined(IRC_BIG_RPRE2)
             const u16x8 rr = EPI == EPI_DGELU ? *reinterpret_cast<const u16x8*>(
                 reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col) : rpre[it];
 #else

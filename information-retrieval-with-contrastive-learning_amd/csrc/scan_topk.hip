@@ -2439,10 +2439,10 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
     return check_launch("select_dense_kernel(gemm lists)");
   }
   if (p.two_phase && p.pp && pp_sample_enabled() && p.pp_sG * LT_M <= SEL_STAGE &&
-      p.pp_sG * LT_M >= 8 * k) {
+      p.pp_sG * LT_M >= 4 * k) {
     // threshold sample on the GEMM kernel: the sample docs (every stride-th row) as B
     // with row stride ldb = stride * D, the 4 largest keys per (256-doc sample tile,
-    // query) kept, thr[q] = their k-th.  Only where the lists hold >= 8 k keys (C2's
+    // query) kept, thr[q] = their k-th.  Only where the lists hold >= 4 k keys (C2's
     // 6,250-doc sample has 25 tiles = 100 keys: no threshold at k = 100, every doc
     // survives -- 640 us a call, profiles/r04_b_ppl_ab.txt; the tile kernel's GMAX
     // pass keeps 4 keys per 32 docs).  (The tile kernel's GMAX pass ran at ~0.05 of
