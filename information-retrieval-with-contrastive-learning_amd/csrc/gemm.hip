@@ -554,8 +554,26 @@ inline std::atomic<int>& big_ring_mode() {
 }
 inline bool big_ring() { return big_ring_mode().load(std::memory_order_relaxed) != 0; }
 
-template <typename TO, int EPI, int WNB, bool RING = false>
+// IRC_BIG_MF16=1 selects the 16x16x32 MFMA form of gemm_big_kernel (A/B; read on first
+// use; irc_gemm_set_big_mf16 switches it at run time).
+inline std::atomic<int>& big_mf16_mode() {
+  static std::atomic<int> on{[] {
+    const char* e = getenv("IRC_BIG_MF16");
+    return (e && e[0] == '1') ? 1 : 0;
+  }()};
+  return on;
+}
+inline bool big_mf16() { return big_mf16_mode().load(std::memory_order_relaxed) != 0; }
+
+// MF16: v_mfma_f32_16x16x32_bf16 instead of 32x32x16 (2-slot form only): the same
+// 256 x 128 WNB tile and LDS image, 8 x 2 WNB accumulators of 16 x 16 per wave, one
+// k32 step per half K-tile.  The chunk key (r >> 1) & 7 stays conflict free for the
+// 16x16x32 fragment reads too (lane l: row l & 15, chunk 4 s + (l >> 4): each 16-lane
+// group covers 16 distinct 16-byte bank slots).  On MI355X the 16x16x32 loop runs at
+// a higher clock for the same work (MI355X_MICROARCH.md, bf16 MFMA shapes).
+template <typename TO, int EPI, int WNB, bool RING = false, bool MF16 = false>
 __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
+  static_assert(!(RING && MF16), "the 16x16x32 form is 2-slot only");
   using big::BK;
   using big::NT;
   using big::NW;
@@ -584,10 +602,15 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
   const int h = lane >> 5, r32 = lane & 31;
 
   f32x16 acc[4][WNB];
+  f32x4 acc4[8][2 * WNB];  // MF16: element e -> row 16 i + 4 (lane >> 4) + e, col 16 j + (lane & 15)
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < WNB; ++j) acc[i][j] = (f32x16)0.0f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2 * WNB; ++j) acc4[i][j] = (f32x4)0.0f;
 
   if constexpr (RING) {
     using big::BK4;
@@ -652,12 +675,39 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 #ifndef IRC_BIG_SPREAD
     if (more) {
       char* nxt = lds + (cur ^ 1) * STAGE;
-      big::stage<BM>(A, g.lda, m0, g.M, (kt + 1) * BK, nxt, wave, lane);
-      big::stage<BN>(B, g.ldb, n0, g.N, (kt + 1) * BK, nxt + A_BYTES, wave, lane);
+      // MF16: the DMA addresses are re-derived per K-tile (kept live through the loop
+      // they would push the 16x16 fragments into spills)
+      int ln = lane;
+      if constexpr (MF16) asm volatile("" : "+v"(ln));
+      big::stage<BM>(A, g.lda, m0, g.M, (kt + 1) * BK, nxt, wave, ln);
+      big::stage<BN>(B, g.ldb, n0, g.N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
     }
 #endif
     const char* la = lds + cur * STAGE;
     const char* lb = la + A_BYTES;
+    if constexpr (MF16) {
+      const int l16 = lane & 15, q4 = lane >> 4;
+      const int key = big::chunk_key(l16);  // rows 16 i + l16: (row >> 1) & 7 = (l16 >> 1) & 7
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int coff = (((4 * s2 + q4) ^ key) * 16);
+        bf16x8 fa[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 16 + l16) * 128 + coff);
+#pragma unroll
+        for (int j = 0; j < 2 * WNB; ++j) {
+          const bf16x8 fb =
+              *reinterpret_cast<const bf16x8*>(lb + (wn * 32 * WNB + j * 16 + l16) * 128 + coff);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc4[i][j], 0, 0, 0);
+        }
+      }
+      wait_vmcnt<0>();
+      __syncthreads();
+      continue;
+    }
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
 #ifdef IRC_BIG_SPREAD  // A/B build: the next K-tile's DMA spread over the 4 k-steps
@@ -699,6 +749,12 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
       for (int j = 0; j < WNB; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) t += acc[i][j][e];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 2 * WNB; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t += acc4[i][j][e];
     if (t == 1234.5f) reinterpret_cast<float*>(g.C)[threadIdx.x] = t;
     return;
   }
@@ -716,39 +772,19 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
     float* st = reinterpret_cast<float*>(lds) + wave * (32 * PITCH);
     const int rbase0 = m0 + wm * 128;
     const int cbase = n0 + wn * WCOLS;
-    float bv[WNB];
+    float bv[WNB], bv16[2 * WNB];
 #pragma unroll
     for (int j = 0; j < WNB; ++j) {
       const int col = cbase + j * 32 + r32;
-      bv[j] = epi_has_bias(EPI) && col < g.N ? bias[col] : 0.f;
+      bv[j] = !MF16 && epi_has_bias(EPI) && col < g.N ? bias[col] : 0.f;
     }
-#ifdef IRC_BIG_RPRE2  // A/B build: residual rows of pass i + 1 loaded during pass i
-    constexpr int CPRR2 = WCOLS / 8, NRR2 = 32 * CPRR2 / 64;
-    constexpr bool RES2 = sizeof(TO) == 2 && (EPI == EPI_BIAS_RESID || EPI == EPI_RESID);
-    u16x8 rnext[NRR2];
-    auto rload = [&](int i, u16x8 (&dst)[NRR2]) {
 #pragma unroll
-      for (int it = 0; it < NRR2; ++it) {
-        const int c = it * 64 + lane;
-        const int row = rbase0 + i * 32 + c / CPRR2, col = cbase + (c % CPRR2) * 8;
-        dst[it] = (row < g.M && col < g.N)
-                      ? *reinterpret_cast<const u16x8*>(
-                            reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col)
-                      : (u16x8)0;
-      }
-    };
-    if constexpr (RES2) rload(0, rnext);
-#endif
+    for (int j = 0; j < 2 * WNB; ++j) {
+      const int col = cbase + j * 16 + (lane & 15);
+      bv16[j] = MF16 && epi_has_bias(EPI) && col < g.N ? bias[col] : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-#ifdef IRC_BIG_RPRE2
-      u16x8 rpre[NRR2];
-      if constexpr (RES2) {
-#pragma unroll
-        for (int it = 0; it < NRR2; ++it) rpre[it] = rnext[it];
-        if (i + 1 < 4) rload(i + 1, rnext);
-      }
-#endif
 #ifdef IRC_BIG_RPRE  // A/B build: the pass's residual rows loaded before its LDS staging
       constexpr int CPRR = WCOLS / 8, NRR = 32 * CPRR / 64;
       u16x8 rpre[NRR];
@@ -764,6 +800,19 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
         }
       }
 #endif
+      if constexpr (MF16) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < 2 * WNB; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int rl = 16 * ii + 4 * (lane >> 4) + e;
+              float v = acc4[2 * i + ii][j][e] * g.alpha + bv16[j];
+              if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
+              st[rl * PITCH + j * 16 + (lane & 15)] = v;
+            }
+      } else {
 #pragma unroll
       for (int j = 0; j < WNB; ++j)
 #pragma unroll
@@ -773,6 +822,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
           if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
           st[rl * PITCH + j * 32 + r32] = v;
         }
+      }
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const int rbase = rbase0 + i * 32;
@@ -788,7 +838,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
           const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c8 + 4]);
           float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
           if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
-#if defined(IRC_BIG_RPRE) || defined(IRC_BIG_RPRE2)
+#ifdef IRC_BIG_RPRE
             const u16x8 rr = EPI == EPI_DGELU ? *reinterpret_cast<const u16x8*>(
                 reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col) : rpre[it];
 #else
@@ -850,18 +900,21 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
     }
     return;
   }
+  constexpr int NJ = MF16 ? 2 * WNB : WNB, NI = MF16 ? 8 : 4, NE = MF16 ? 4 : 16;
 #pragma unroll
-  for (int j = 0; j < WNB; ++j) {
-    const int col = n0 + wn * WCOLS + j * 32 + r32;
+  for (int j = 0; j < NJ; ++j) {
+    const int col = MF16 ? n0 + wn * WCOLS + j * 16 + (lane & 15) : n0 + wn * WCOLS + j * 32 + r32;
     if (col >= g.N) continue;
     const float bv = epi_has_bias(EPI) ? bias[col] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      for (int e = 0; e < NE; ++e) {
+        const int row = MF16 ? m0 + wm * 128 + i * 16 + 4 * (lane >> 4) + e
+                             : m0 + wm * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (row >= g.M) continue;
-        float v = acc[i][j][e] * g.alpha + bv;
+        float v = (MF16 ? acc4[i % 8][j % (2 * WNB)][e % 4] : acc[i % 4][j % WNB][e % 16]) * g.alpha +
+                  bv;
         if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
         if (EPI == EPI_BIAS_GELU_SAVE) {
           TO* pre = const_cast<TO*>(R) + (int64_t)row * g.ldr + col;
@@ -909,7 +962,12 @@ static int launch_big(const Args& g, int batch, int wnb, hipStream_t st) {
   const int tiles = ((g.M + big::BM - 1) / big::BM) * ((g.N + bn - 1) / bn);
   prof_begin(st);
   const bool ring = big_ring() && g.K % big::BK4 == 0;
-  if (wnb == 3 && ring)
+  if (big_mf16() && !ring) {
+    if (wnb == 3)
+      hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 3, false, true>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
+    else
+      hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 2, false, true>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
+  } else if (wnb == 3 && ring)
     hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 3, true>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
   else if (wnb == 3)
     hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 3>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
@@ -1013,6 +1071,12 @@ extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue,
 // 4-slot ring (1) or 2-slot loop (0, the default: the ring measured no faster on
 // the BERT shapes, profiles/r03_ring_r_*) of the 256-row big-tile GEMM; returns the
 // previous setting.
+// 16x16x32 (1) or 32x32x16 (0) MFMAs in the big-tile kernel's 2-slot loop; returns the
+// previous setting.
+extern "C" int irc_gemm_set_big_mf16(int on) {
+  return irc::gemm::big_mf16_mode().exchange(on ? 1 : 0);
+}
+
 extern "C" int irc_gemm_set_big_ring(int on) {
   return irc::gemm::big_ring_mode().exchange(on ? 1 : 0);
 }

@@ -33,6 +33,12 @@ def gemm_set_big_ring(on) -> int:
     return int(_lib.load().irc_gemm_set_big_ring(1 if on else 0))
 
 
+def gemm_set_big_mf16(on) -> int:
+    """MFMA shape of the big-tile bf16 GEMM's 2-slot loop (irc_gemm_set_big_mf16):
+    True = 16x16x32, False = 32x32x16.  Returns the previous setting."""
+    return int(_lib.load().irc_gemm_set_big_mf16(1 if on else 0))
+
+
 def gemm_set_persistent(mode) -> int:
     """Persistent tile loop of the 256x256 bf16 GEMM (irc_gemm_set_persistent): 0 off
     (the default), 1 / True dynamic tiles with the next tile's first K-tile prestaged

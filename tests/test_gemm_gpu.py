@@ -213,6 +213,65 @@ def test_big_tile_chunk_key_exact(gpu, ring, M, N, K):
     assert torch.equal(out, ref)
 
 
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,K", [(32768, 2304, 768), (32768, 768, 3072), (32700, 2304, 192),
+                                   (4000, 2100, 640)])
+def test_big_tile_mf16_exact(gpu, epi, M, N, K):
+    """The big-tile kernel's 16x16x32 form (irc_gemm_set_big_mf16) on the BERT QKV /
+    FFN2 shapes, a ragged M and a 256 x 256 case (N % 384 != 0): small-integer
+    operands, bias and residual make every sum exact in fp32, so the output equals the
+    32x32x16 form's bit for bit (GELU: the same function of the same exact input)."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(M + N + K + epi)
+    a = torch.randint(-4, 5, (M, K), generator=g).to(torch.bfloat16).to(gpu)
+    b = torch.randint(-4, 5, (N, K), generator=g).to(torch.bfloat16).to(gpu)
+    bias = (torch.randint(-8, 9, (N,), generator=g).float() / 4).to(gpu) if epi in (1, 2, 3) else None
+    res = torch.randint(-8, 9, (M, N), generator=g).to(torch.bfloat16).to(gpu) if epi in (3, 4) else None
+    outs = []
+    prev = ops.gemm_set_big_mf16(False)
+    try:
+        for mf in (False, True):
+            ops.gemm_set_big_mf16(mf)
+            outs.append(ops.gemm(a, b, bias=bias, epilogue=epi, residual=res,
+                                 out_dtype=torch.bfloat16))
+            if epi == 0:  # fp32 output too (the LSTM input projection's form)
+                outs.append(ops.gemm(a, b, out_dtype=torch.float32))
+        torch.cuda.synchronize()
+    finally:
+        ops.gemm_set_big_mf16(prev)
+    half = len(outs) // 2
+    for x, y in zip(outs[:half], outs[half:]):
+        assert torch.equal(x, y)
+    if epi == 0:
+        ref = a.float() @ b.float().t()
+        assert torch.equal(outs[1], ref)
+
+
+def test_big_tile_mf16_random_close(gpu):
+    """Random bf16 operands: the 16x16x32 and 32x32x16 forms agree within fp32
+    reassociation (FFN2 shape, K = 3072, bias + residual)."""
+    from irc_amd import ops
+
+    M, N, K = 32768, 768, 3072
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn((M, K), generator=g).to(torch.bfloat16).to(gpu)
+    b = (torch.randn((N, K), generator=g) * 0.03).to(torch.bfloat16).to(gpu)
+    bias = torch.randn((N,), generator=g).to(gpu)
+    res = torch.randn((M, N), generator=g).to(torch.bfloat16).to(gpu)
+    outs = []
+    prev = ops.gemm_set_big_mf16(False)
+    try:
+        for mf in (False, True):
+            ops.gemm_set_big_mf16(mf)
+            outs.append(ops.gemm(a, b, bias=bias, epilogue=3, residual=res,
+                                 out_dtype=torch.float32))
+        torch.cuda.synchronize()
+    finally:
+        ops.gemm_set_big_mf16(prev)
+    assert (outs[0] - outs[1]).abs().max().item() <= 1e-4 * K ** 0.5
+
+
 @pytest.mark.parametrize("M,N", [(4096, 3072), (32768, 768), (300, 260)])
 def test_gelu_bf16_epilogue_matches_exact_erf_gelu(gpu, M, N):
     """The bf16-output GELU epilogue (gelu_lite2, irc_common.h) against torch's exact erf

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--layouts", action="store_true")
     ap.add_argument("--only", default="", help="comma-separated shape names")
     ap.add_argument("--mx", action="store_true", help="MX-fp8 GEMMs (irc_gemm_mx) of the BERT shapes")
+    ap.add_argument("--mf16", default="0", help="big-tile MFMA shape: 0, 1 or 'ab' (interleaved)")
     args = ap.parse_args()
     only = set(filter(None, args.only.split(",")))
     if args.mx:
@@ -106,19 +107,24 @@ def main():
         if res is not None:
             res = res.to(od)
         out = torch.empty((M, N), device=dev, dtype=od)
-        for _ in range(3):
-            ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
-        st = torch.cuda.current_stream()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        for _ in range(args.iters):
-            ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
-        e1.record(st)
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / args.iters
-        tf = 2.0 * M * N * K / us / 1e6
-        print(f"{name:14s} M={M:6d} N={N:5d} K={K:5d} epi={epi}  {us:9.1f} us  {tf:7.1f} TF/s  "
-              f"{tf / 2500:.1%}", flush=True)
+        modes = (0, 1, 0, 1) if args.mf16 == "ab" else (int(args.mf16),)
+        for mode in modes:
+            ops.gemm_set_big_mf16(mode)
+            for _ in range(3):
+                ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(args.iters):
+                ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
+            e1.record(st)
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.iters
+            tf = 2.0 * M * N * K / us / 1e6
+            tag = f" mf16={mode}" if args.mf16 != "0" else ""
+            print(f"{name:14s} M={M:6d} N={N:5d} K={K:5d} epi={epi}{tag}  {us:9.1f} us  "
+                  f"{tf:7.1f} TF/s  {tf / 2500:.1%}", flush=True)
+        ops.gemm_set_big_mf16(0)
 
 
 def mx_shapes(args):
