@@ -258,7 +258,7 @@ def test_big_tile_mf16_random_close(gpu):
     a = torch.randn((M, K), generator=g).to(torch.bfloat16).to(gpu)
     b = (torch.randn((N, K), generator=g) * 0.03).to(torch.bfloat16).to(gpu)
     bias = torch.randn((N,), generator=g).to(gpu)
-    res = torch.randn((M, N), generator=g).to(torch.bfloat16).to(gpu)
+    res = torch.randn((M, N), generator=g).to(gpu)
     outs = []
     prev = ops.gemm_set_big_mf16(False)
     try:
