@@ -17,3 +17,10 @@ print("train mf16=%s" % sys.argv[2], round(d["value"]), round(d["ms_per_step"], 
 PY
   done
 done
+cd /tmp
+for mode in bert overlap heads; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r4f/ov_$mode -o run -- \
+    python3 $GRAFT_REPO_ROOT/tools/overlap_prof.py --mode $mode --steps 20 > $GRAFT_REPO_ROOT/gpurun_out/r4f/ov_$mode.log 2>&1 || exit 1
+  (cd $GRAFT_REPO_ROOT && grep "mode" gpurun_out/r4f/ov_$mode.log | tail -1 && python3 tools/prof_summary.py gpurun_out/r4f/ov_$mode --by-grid > gpurun_out/r4f/ov_${mode}_kernels.txt && head -14 gpurun_out/r4f/ov_${mode}_kernels.txt)
+  find $GRAFT_REPO_ROOT/gpurun_out/r4f/ov_$mode -name "*.db" -delete
+done
