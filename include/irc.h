@@ -144,10 +144,10 @@ int irc_gemm_set_persistent(int mode);
  * results are bit-identical (env IRC_BIG_RING sets the initial value).  Returns the
  * previous setting. */
 int irc_gemm_set_big_ring(int on);
-/* MFMA shape of the big-tile kernel's 2-slot loop: 1 = v_mfma_f32_16x16x32_bf16,
- * 0 = v_mfma_f32_32x32x16_bf16.  Same products; the fp32 accumulation order within
- * a k32 step differs, so results agree within fp32 reassociation (env IRC_BIG_MF16
- * sets the initial value).  Returns the previous setting. */
+/* MFMA shape of the big-tile kernel's 2-slot loop: 1 = v_mfma_f32_16x16x32_bf16 (the
+ * default), 0 = v_mfma_f32_32x32x16_bf16.  Same products; the fp32 accumulation order
+ * within a k32 step differs, so results agree within fp32 reassociation (env
+ * IRC_BIG_MF16 sets the initial value).  Returns the previous setting. */
 int irc_gemm_set_big_mf16(int on);
 
 /* ------------------------------------------------------------- BERT encoder

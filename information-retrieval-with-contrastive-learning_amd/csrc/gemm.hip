@@ -554,12 +554,14 @@ inline std::atomic<int>& big_ring_mode() {
 }
 inline bool big_ring() { return big_ring_mode().load(std::memory_order_relaxed) != 0; }
 
-// IRC_BIG_MF16=1 selects the 16x16x32 MFMA form of gemm_big_kernel (A/B; read on first
-// use; irc_gemm_set_big_mf16 switches it at run time).
+// The 16x16x32 MFMA form of gemm_big_kernel is the default (IRC_BIG_MF16=0 selects the
+// 32x32x16 form; read on first use; irc_gemm_set_big_mf16 switches it at run time).
+// Measured on MI355X, interleaved (profiles/r04_f_*): out-proj 48.6 / 48.4 vs 53.1 /
+// 50.3 us, FFN2 156.7 / 152.9 vs 163.5 / 164.2 us, the C2 step 27.3k vs 26.7k pairs/s.
 inline std::atomic<int>& big_mf16_mode() {
   static std::atomic<int> on{[] {
     const char* e = getenv("IRC_BIG_MF16");
-    return (e && e[0] == '1') ? 1 : 0;
+    return (e && e[0] == '0') ? 0 : 1;
   }()};
   return on;
 }

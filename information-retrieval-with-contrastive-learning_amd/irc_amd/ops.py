@@ -35,7 +35,7 @@ def gemm_set_big_ring(on) -> int:
 
 def gemm_set_big_mf16(on) -> int:
     """MFMA shape of the big-tile bf16 GEMM's 2-slot loop (irc_gemm_set_big_mf16):
-    True = 16x16x32, False = 32x32x16.  Returns the previous setting."""
+    True = 16x16x32 (the default), False = 32x32x16.  Returns the previous setting."""
     return int(_lib.load().irc_gemm_set_big_mf16(1 if on else 0))
 
 
