@@ -144,6 +144,25 @@ int irc_gemm_set_persistent(int mode);
  * results are bit-identical (env IRC_BIG_RING sets the initial value).  Returns the
  * previous setting. */
 int irc_gemm_set_big_ring(int on);
+/* LayerNorm-fold GEMM of the BERT encoder forward (bf16; HF BertLayer's
+ * attention.output / intermediate / output sublayers, contrastive_module.py:39 ->
+ * modeling_bert): the encoder keeps each pre-LayerNorm activation h with per-row
+ * statistics -- partial (sum, sum of squares) pairs over column tiles,
+ * stats[row][nt][2] -- instead of materialising LN(h).
+ *   epilogue 1 / 2 (fold): C = r (A . B^T) + (-r mu) colsum + bias (-> GELU), where A = h,
+ *     B = W diag(gamma) (bf16), colsum[n] = sum_k B[n][k], bias = b + W beta, and mu, r =
+ *     1 / sqrt(var + eps) come from ln_stats (ln_nt pairs per row, row length ln_h):
+ *     = LN(h) . W^T + b (HF: LayerNorm then Linear).
+ *   epilogue 3: C = A . B^T + bias + residual, the residual taken as LN(R) recomputed from
+ *     R = h, ln_stats, ln_gamma, ln_beta (bf16-rounded, as irc_layernorm writes it) when
+ *     ln_gamma != NULL, else R itself.
+ * stats_out (optional): the partials of C's bf16 values, *stats_nt_out pairs per row.
+ * A [M][K], B [N][K], C / R [M][N]-strided bf16; K % 64 == 0, N % 8 == 0, 16-byte rows. */
+int irc_gemm_ln(int epilogue, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
+                const void* B, int64_t ldb, const float* bias, const void* R, int64_t ldr,
+                void* C, int64_t ldc, const float* ln_stats, int ln_nt, const float* ln_gamma,
+                const float* ln_beta, float ln_eps, int64_t ln_h, const float* fold_colsum,
+                float* stats_out, int* stats_nt_out, irc_stream_t stream);
 /* MFMA shape of the big-tile kernel's 2-slot loop: 1 = v_mfma_f32_16x16x32_bf16 (the
  * default), 0 = v_mfma_f32_32x32x16_bf16.  Same products; the fp32 accumulation order
  * within a k32 step differs, so results agree within fp32 reassociation (env

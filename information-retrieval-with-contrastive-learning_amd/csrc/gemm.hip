@@ -114,6 +114,7 @@ struct Args {
   int kchunk;        // split-K: K range of one blockIdx.z slice (multiple of BK)
   float* P;          // split-K partials [batch][split][M][N] (raw sums), or null
   int group_m;       // big-tile kernel: grouped tile order (irc_common.h); 0 = row-major
+  LnArgs ln;         // LayerNorm fold (big-tile kernel, bf16 C, vectorised epilogue)
 };
 
 // bf16 K-outer (COL / KN) slabs are kept k-major in LDS: [BK=32 k][128 rows]
@@ -573,9 +574,13 @@ inline bool big_mf16() { return big_mf16_mode().load(std::memory_order_relaxed) 
 // 16x16x32 fragment reads too (lane l: row l & 15, chunk 4 s + (l >> 4): each 16-lane
 // group covers 16 distinct 16-byte bank slots).  On MI355X the 16x16x32 loop runs at
 // a higher clock for the same work (MI355X_MICROARCH.md, bf16 MFMA shapes).
-template <typename TO, int EPI, int WNB, bool RING = false, bool MF16 = false>
+//
+// LN: the LayerNorm-fold instantiation (irc_gemm_ln, 16x16x32 form only; see LnArgs) --
+// a template flag so the other instantiations keep their register allocation.
+template <typename TO, int EPI, int WNB, bool RING = false, bool MF16 = false, bool LN = false>
 __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
   static_assert(!(RING && MF16), "the 16x16x32 form is 2-slot only");
+  static_assert(!LN || (MF16 && sizeof(TO) == 2), "the LayerNorm fold: 16x16x32 form, bf16 C");
   using big::BK;
   using big::NT;
   using big::NW;
@@ -774,6 +779,17 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
     float* st = reinterpret_cast<float*>(lds) + wave * (32 * PITCH);
     const int rbase0 = m0 + wm * 128;
     const int cbase = n0 + wn * WCOLS;
+    // LayerNorm fold (bf16 C; uniform flags): see LnArgs (gemm_pp.h)
+    constexpr bool LNOK = LN;
+    const bool lnfold = LNOK && g.ln.fold_s != nullptr;
+    const bool lnres = LNOK && g.ln.gamma != nullptr;
+    const bool lnout = LNOK && g.ln.st_out != nullptr;
+    float* lst = reinterpret_cast<float*>(lds) + 8 * 32 * PITCH;  // [256 rows][2] partials
+    static_assert((8 * 32 * PITCH + 512) * 4 <= 2 * STAGE, "LN partials fit the LDS");
+    if (lnout) {
+      lst[threadIdx.x] = 0.f;  // 512 threads, 512 floats
+      __syncthreads();
+    }
     float bv[WNB], bv16[2 * WNB];
 #pragma unroll
     for (int j = 0; j < WNB; ++j) {
@@ -810,8 +826,8 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               const int rl = 16 * ii + 4 * (lane >> 4) + e;
-              float v = acc4[2 * i + ii][j][e] * g.alpha + bv16[j];
-              if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
+              float v = acc4[2 * i + ii][j][e] * g.alpha + (lnfold ? 0.f : bv16[j]);
+              if (EPI == EPI_BIAS_GELU && !lnfold) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
               st[rl * PITCH + j * 16 + (lane & 15)] = v;
             }
       } else {
@@ -820,8 +836,8 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int rl = (e & 3) + 8 * (e >> 2) + 4 * h;
-          float v = acc[i][j][e] * g.alpha + bv[j];
-          if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
+          float v = acc[i][j][e] * g.alpha + (lnfold ? 0.f : bv[j]);
+          if (EPI == EPI_BIAS_GELU && !lnfold) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
           st[rl * PITCH + j * 32 + r32] = v;
         }
       }
@@ -839,7 +855,40 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
           const f32x4 v0 = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c8]);
           const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * PITCH + c8 + 4]);
           float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
+          if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU) {
+            if (lnfold) {  // y = r acc + (-r mu) s + t, then GELU
+              float mu, rs;
+              ln_row_stats(g.ln, row, mu, rs);
+              const float nrm = -rs * mu;
+              const float* sc = g.ln.fold_s + col;
+              const float* tc = bias + col;
+              const f32x4 s0 = *reinterpret_cast<const f32x4*>(sc), s1 = *reinterpret_cast<const f32x4*>(sc + 4);
+              const f32x4 t0 = *reinterpret_cast<const f32x4*>(tc), t1 = *reinterpret_cast<const f32x4*>(tc + 4);
+              const float ss[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+              const float tt[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+#pragma unroll
+              for (int t = 0; t < 8; ++t) v[t] = __builtin_fmaf(rs, v[t], __builtin_fmaf(nrm, ss[t], tt[t]));
+              if (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+                for (int t = 0; t < 8; ++t) v[t] = gelu_lite(v[t]);
+              }
+            }
+          }
+          if (EPI == EPI_BIAS_RESID && lnres) {  // residual = LN(R) as the LN kernel writes it
+            const u16x8 rr = *reinterpret_cast<const u16x8*>(
+                reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col);
+            float mu, rs;
+            ln_row_stats(g.ln, row, mu, rs);
+            const f32x4 g0 = *reinterpret_cast<const f32x4*>(g.ln.gamma + col);
+            const f32x4 g1 = *reinterpret_cast<const f32x4*>(g.ln.gamma + col + 4);
+            const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.ln.beta + col);
+            const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.ln.beta + col + 4);
+            const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+            const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+              v[t] += bf16_to_f32(f32_to_bf16(__builtin_fmaf((bf16_to_f32(rr[t]) - mu) * rs, gg[t], bb[t])));
+          } else if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
 #ifdef IRC_BIG_RPRE
             const u16x8 rr = EPI == EPI_DGELU ? *reinterpret_cast<const u16x8*>(
                 reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col) : rpre[it];
@@ -865,6 +914,18 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
           u16x8 o;
 #pragma unroll
           for (int t = 0; t < 8; ++t) o[t] = f32_to_bf16(v[t]);
+          if (lnout) {  // row partials of the bf16 output (this tile's columns)
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const float x = bf16_to_f32(o[t]);
+              s1 += x;
+              s2 = __builtin_fmaf(x, x, s2);
+            }
+            const int lr = row - m0;
+            atomicAdd(&lst[2 * lr], s1);
+            atomicAdd(&lst[2 * lr + 1], s2);
+          }
 #ifdef IRC_PP_DIAG_NOSTORE  // diagnostic build: the epilogue without its C stores
           if (o[0] == 0x7fc1 && o[7] == 0x7fc3)
 #endif
@@ -899,6 +960,12 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (lnout) {  // this tile's (sum, sum of squares) of every row, one pair per tile column
+      lds_barrier();
+      const int lr = threadIdx.x >> 1, row = m0 + lr;
+      if (row < g.M)
+        g.ln.st_out[((int64_t)row * g.ln.nt_out + tn) * 2 + (threadIdx.x & 1)] = lst[threadIdx.x];
     }
     return;
   }
@@ -958,13 +1025,18 @@ inline int big_wnb(const Args& g, int batch, int la, int lb) {
   return tiles >= 128 ? wnb : 0;
 }
 
-template <typename TO, int EPI>
+template <typename TO, int EPI, bool LN = false>
 static int launch_big(const Args& g, int batch, int wnb, hipStream_t st) {
   const int bn = 128 * wnb;
   const int tiles = ((g.M + big::BM - 1) / big::BM) * ((g.N + bn - 1) / bn);
   prof_begin(st);
   const bool ring = big_ring() && g.K % big::BK4 == 0;
-  if (big_mf16() && !ring) {
+  if constexpr (LN) {
+    if (wnb == 3)
+      hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 3, false, true, true>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
+    else
+      hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 2, false, true, true>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
+  } else if (big_mf16() && !ring) {
     if (wnb == 3)
       hipLaunchKernelGGL((gemm_big_kernel<TO, EPI, 3, false, true>), dim3(tiles, batch), dim3(big::NT), 0, st, g);
     else
@@ -1070,15 +1142,81 @@ extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue,
   return s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
 }
 
-// 4-slot ring (1) or 2-slot loop (0, the default: the ring measured no faster on
-// the BERT shapes, profiles/r03_ring_r_*) of the 256-row big-tile GEMM; returns the
-// previous setting.
+// LayerNorm-fold GEMM of the BERT encoder (include/irc.h irc_gemm_ln): bf16 A [M][K],
+// B [N][K], bf16 C; routed like irc_gemm (ping-pong 256 x 256 where it qualifies, else the
+// big-tile kernel in its 16x16x32 form), never split or persistent.
+extern "C" int irc_gemm_ln(int epilogue, int64_t M, int64_t N, int64_t K, const void* A,
+                           int64_t lda, const void* B, int64_t ldb, const float* bias,
+                           const void* R, int64_t ldr, void* C, int64_t ldc,
+                           const float* ln_stats, int ln_nt, const float* ln_gamma,
+                           const float* ln_beta, float ln_eps, int64_t ln_h,
+                           const float* fold_colsum, float* stats_out, int* stats_nt_out,
+                           irc_stream_t stream) {
+  using namespace irc::gemm;
+  IRC_REQUIRE(epilogue == EPI_BIAS || epilogue == EPI_BIAS_GELU || epilogue == EPI_BIAS_RESID,
+              "gemm_ln: epilogue must be 1 (fold), 2 (fold + GELU) or 3 (residual)");
+  IRC_REQUIRE(M > 0 && N > 0 && K > 0 && M < (1ll << 31) && N < (1ll << 31), "gemm_ln: bad sizes");
+  IRC_REQUIRE(bias != nullptr, "gemm_ln: bias required");
+  const bool fold = epilogue != EPI_BIAS_RESID;
+  IRC_REQUIRE(!fold || (ln_stats && fold_colsum && ln_nt > 0 && ln_h > 0),
+              "gemm_ln: the fold needs the input statistics and the column sums");
+  IRC_REQUIRE(fold || R != nullptr, "gemm_ln: epilogue 3 needs the residual");
+  IRC_REQUIRE(fold || ln_gamma == nullptr || (ln_stats && ln_beta && ln_nt > 0 && ln_h > 0),
+              "gemm_ln: the residual LayerNorm needs statistics, gamma and beta");
+  IRC_REQUIRE(stats_out == nullptr || stats_nt_out != nullptr, "gemm_ln: stats_nt_out required");
+  IRC_REQUIRE(K % 64 == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 &&
+                  (R == nullptr || ldr % 8 == 0) &&
+                  (((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)R) % 16) == 0,
+              "gemm_ln: needs K %% 64 == 0, N %% 8 == 0 and 16-byte aligned rows");
+  LnArgs ln{};
+  ln.st = ln_stats;
+  ln.nt = ln_nt;
+  ln.inv_h = ln_h > 0 ? 1.0f / (float)ln_h : 0.f;
+  ln.eps = ln_eps;
+  ln.gamma = fold ? nullptr : ln_gamma;
+  ln.beta = fold ? nullptr : ln_beta;
+  ln.fold_s = fold ? fold_colsum : nullptr;
+  ln.st_out = stats_out;
+  hipStream_t st = as_stream(stream);
+  const double flops = 2.0 * M * N * K;
+  Args g{A, B, C, bias, R, (int)M, (int)N, (int)K, lda, ldb, ldc, ldr, 0, 0, 0, 0, 0, 1.0f, 0, 1, 1,
+         1, 0, nullptr, gemm_group_m()};
+  const int wnb = big_wnb(g, 1, ROW, ROW);
+  // the 256 x 256 kernel unless the big-tile one is preferred and applies (small shapes
+  // that neither kernel's heuristics take also run 256 x 256)
+  if ((pp_enabled() && gpp::qualifies(0, 0, M, N, K, A, lda, 0, B, ldb, 0, 1, 1)) || wnb == 0) {
+    gpp::PArgs pa{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), C,
+                  bias, R, nullptr, (int)M, (int)N, (int)K, (int)K, lda, ldb, ldc, ldr, 0, 0, 0, 0,
+                  0, 1.0f, 0, 1};
+    pa.group_m = gemm_group_m();
+    ln.nt_out = (int)((N + 255) / 256);
+    pa.ln = ln;
+    if (stats_nt_out) *stats_nt_out = ln.nt_out;
+    prof_begin(st);
+    gpp::run_ln(epilogue, pa, st);
+    prof_end("gemm_bf16", st, flops);
+    prof_work("gemm_bf16_bytes", gemm_alg_bytes(0, epilogue, 0, M, N, K, 1));
+    return check_launch("gemm_pp_kernel(ln)");
+  }
+  ln.nt_out = (int)((N + 128 * wnb - 1) / (128 * wnb));
+  g.ln = ln;
+  if (stats_nt_out) *stats_nt_out = ln.nt_out;
+  switch (epilogue) {
+    case EPI_BIAS: return launch_big<unsigned short, EPI_BIAS, true>(g, 1, wnb, st);
+    case EPI_BIAS_GELU: return launch_big<unsigned short, EPI_BIAS_GELU, true>(g, 1, wnb, st);
+    default: return launch_big<unsigned short, EPI_BIAS_RESID, true>(g, 1, wnb, st);
+  }
+}
+
 // 16x16x32 (1) or 32x32x16 (0) MFMAs in the big-tile kernel's 2-slot loop; returns the
 // previous setting.
 extern "C" int irc_gemm_set_big_mf16(int on) {
   return irc::gemm::big_mf16_mode().exchange(on ? 1 : 0);
 }
 
+// 4-slot ring (1) or 2-slot loop (0, the default: the ring measured no faster on
+// the BERT shapes, profiles/r03_ring_r_*) of the 256-row big-tile GEMM; returns the
+// previous setting.
 extern "C" int irc_gemm_set_big_ring(int on) {
   return irc::gemm::big_ring_mode().exchange(on ? 1 : 0);
 }

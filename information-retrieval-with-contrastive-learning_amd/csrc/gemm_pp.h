@@ -3,6 +3,38 @@
 #include "irc_common.h"
 
 namespace irc {
+
+// LayerNorm fold of the BERT encoder: a pre-LN activation h is kept
+// with per-row statistics as partial (sum, sum of squares) pairs over disjoint column
+// tiles, stats[row][tile][2], written by the epilogue that produces h.  A GEMM whose
+// input is LN(h) = (h - mu) r gamma + beta runs on h itself with the folded weight
+// W' = W diag(gamma) and the epilogue  y = r acc + (-r mu) s_n + t_n  (s_n = sum_k W'_nk,
+// t_n = b_n + sum_k beta_k W_nk); a residual LN(h) is recomputed in the epilogue as the
+// LayerNorm kernel would write it (bf16 of fma((h - mu) r, gamma, beta)).
+struct LnArgs {
+  const float* st;  // input statistics [M][nt][2] (fold: of A's rows; else of R's rows)
+  int nt;
+  float inv_h, eps;
+  const float* gamma;  // residual recompute (EPI_BIAS_RESID): LN weight / bias of R
+  const float* beta;
+  const float* fold_s;  // fold (EPI_BIAS / EPI_BIAS_GELU): column sums of the folded weight
+  float* st_out;        // output statistics [M][nt_out][2] of C's bf16 values, or null
+  int nt_out;
+};
+
+__device__ __forceinline__ void ln_row_stats(const LnArgs& l, int row, float& mu, float& r) {
+  const float2* p = reinterpret_cast<const float2*>(l.st) + (int64_t)row * l.nt;
+  float s = 0.f, q = 0.f;
+  for (int t = 0; t < l.nt; ++t) {
+    const float2 v = p[t];
+    s += v.x;
+    q += v.y;
+  }
+  mu = s * l.inv_h;
+  const float var = fmaxf(q * l.inv_h - mu * mu, 0.f);
+  r = rsqrtf(var + l.eps);
+}
+
 namespace gpp {
 
 struct PArgs {
@@ -48,6 +80,8 @@ struct PArgs {
   const unsigned char* sbx;
   int mpad, npad;
   unsigned char* cx;
+  // LayerNorm fold (bf16 C, vectorised epilogue, non-persistent): ln.st == null = off
+  LnArgs ln;
 };
 
 constexpr int EPI_SCAN = 7;
@@ -68,6 +102,9 @@ void run_fp8(int epi, const PArgs& a, hipStream_t st);
 // MX-fp8 linear layer: C = (A8 . B8^T with per-32-k E8M0 block scales) (+ bias /
 // GELU / residual); bf16 C, or MX-fp8 C when a.cx != null (epilogues 1, 2 only)
 void run_mx(int epi, const PArgs& a, hipStream_t st);
+// LayerNorm-fold linear layer (irc_gemm_ln): bf16 K-major operands, bf16 vec_c C,
+// epilogues 1-3 with a.ln set (see LnArgs)
+void run_ln(int epi, const PArgs& a, hipStream_t st);
 
 }  // namespace gpp
 }  // namespace irc

@@ -458,7 +458,9 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
 // split-K slabs): per wave, four 32-row passes through its LDS staging rows (the
 // first 8 * 32 * EP_PITCH floats of LDS), fused bias / GELU / GELU' / residual /
 // pre-activation save / fp32 accumulate, then coalesced 16-byte stores.
-template <typename TO, int EPI, int F8>
+// LN: the LayerNorm-fold instantiation (irc_gemm_ln; see LnArgs) -- a template flag so the
+// other instantiations keep their register allocation.
+template <typename TO, int EPI, int F8, bool LN = false>
 __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[8][4], char* lds,
                                              int m0, int n0, int batch, int grp, int wn, int wave,
                                              int lane) {
@@ -475,6 +477,17 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
       bv[j] = (!slab && has_bias(EPI) && col < g.N) ? bias[col] : 0.f;
     }
     const float alpha = slab ? 1.f : g.alpha;
+    // LayerNorm fold (bf16 C only; uniform): the staged values are raw acc, the fold,
+    // bias and GELU are applied per 8-column chunk below
+    constexpr bool LNOK = LN && sizeof(TO) == 2 && F8 == 0;
+    const bool lnfold = LNOK && !slab && g.ln.fold_s != nullptr;
+    const bool lnres = LNOK && !slab && g.ln.gamma != nullptr;
+    const bool lnout = LNOK && !slab && g.ln.st_out != nullptr;
+    float* lst = reinterpret_cast<float*>(lds) + 8 * 32 * EP_PITCH;  // [256 rows][2] partials
+    if (lnout) {
+      lst[threadIdx.x] = 0.f;  // 512 threads, 512 floats
+      __syncthreads();
+    }
     // fp8 linear layers: per-row (A) and per-column (B) dequantisation scales
     float sbv[4] = {1.f, 1.f, 1.f, 1.f};
     float sav[8][4];
@@ -505,9 +518,9 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
               v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * (alpha * sav[2 * p + ii][e] * sbv[j]) +
                                  bv[j];
             else
-              v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * alpha + bv[j];
+              v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * alpha + (lnfold ? 0.f : bv[j]);
           }
-          if (!slab && EPI == EPI_BIAS_GELU) {
+          if (!slab && EPI == EPI_BIAS_GELU && !lnfold) {
             if constexpr (sizeof(TO) == 2 || F8 == 2) {  // bf16 / MX output
               v[0] = gelu_lite2(v[0]);
               v[1] = gelu_lite2(v[1]);
@@ -552,9 +565,44 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
           const f32x4 v0 = *reinterpret_cast<const f32x4*>(&st[rl * EP_PITCH + c8]);
           const f32x4 v1 = *reinterpret_cast<const f32x4*>(&st[rl * EP_PITCH + c8 + 4]);
           float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          if constexpr (LNOK && (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU)) {
+            if (lnfold) {  // y = r acc + (-r mu) s + t, then GELU
+              float mu, rs;
+              ln_row_stats(g.ln, row, mu, rs);
+              const float nrm = -rs * mu;
+              const float* sc = g.ln.fold_s + col;
+              const float* tc = g.bias + batch * g.sBias + col;
+              const f32x4 s0 = *reinterpret_cast<const f32x4*>(sc), s1 = *reinterpret_cast<const f32x4*>(sc + 4);
+              const f32x4 t0 = *reinterpret_cast<const f32x4*>(tc), t1 = *reinterpret_cast<const f32x4*>(tc + 4);
+              const float ss[8] = {s0[0], s0[1], s0[2], s0[3], s1[0], s1[1], s1[2], s1[3]};
+              const float tt[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
+#pragma unroll
+              for (int t = 0; t < 8; ++t) v[t] = __builtin_fmaf(rs, v[t], __builtin_fmaf(nrm, ss[t], tt[t]));
+              if (EPI == EPI_BIAS_GELU) {
+#pragma unroll
+                for (int t = 0; t < 8; t += 2) {
+                  const f32x2 gg = gelu_lite2(f32x2{v[t], v[t + 1]});
+                  v[t] = gg.x;
+                  v[t + 1] = gg.y;
+                }
+              }
+            }
+          }
           if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
             const u16x8 rr = *reinterpret_cast<const u16x8*>(R + (int64_t)row * g.ldr + col);
-            if constexpr (EPI == EPI_DGELU) {
+            if (EPI == EPI_BIAS_RESID && lnres) {  // residual = LN(R) as the LN kernel writes it
+              float mu, rs;
+              ln_row_stats(g.ln, row, mu, rs);
+              const f32x4 g0 = *reinterpret_cast<const f32x4*>(g.ln.gamma + col);
+              const f32x4 g1 = *reinterpret_cast<const f32x4*>(g.ln.gamma + col + 4);
+              const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.ln.beta + col);
+              const f32x4 b1 = *reinterpret_cast<const f32x4*>(g.ln.beta + col + 4);
+              const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+              const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+              for (int t = 0; t < 8; ++t)
+                v[t] += bf16_to_f32(f32_to_bf16(__builtin_fmaf((bf16_to_f32(rr[t]) - mu) * rs, gg[t], bb[t])));
+            } else if constexpr (EPI == EPI_DGELU) {
 #pragma unroll
               for (int t = 0; t < 8; t += 2) {
                 const f32x2 g2 = gelu_grad_f2(f32x2{bf16_to_f32(rr[t]), bf16_to_f32(rr[t + 1])});
@@ -595,6 +643,18 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
           u16x8 o;
 #pragma unroll
           for (int t = 0; t < 8; ++t) o[t] = f32_to_bf16(v[t]);
+          if (lnout) {  // row partials of the bf16 output (this tile's columns)
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const float x = bf16_to_f32(o[t]);
+              s1 += x;
+              s2 = __builtin_fmaf(x, x, s2);
+            }
+            const int lr = row - m0;
+            atomicAdd(&lst[2 * lr], s1);
+            atomicAdd(&lst[2 * lr + 1], s2);
+          }
 #ifdef IRC_PP_DIAG_NOSTORE  // diagnostic build: the epilogue without its C stores
           if (o[0] == 0x7fc1 && o[7] == 0x7fc3)
 #endif
@@ -627,6 +687,12 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
       }
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (lnout) {  // this tile's (sum, sum of squares) of every row, one pair per tile column
+      lds_barrier();
+      const int lr = threadIdx.x >> 1, row = m0 + lr;
+      if (row < g.M)
+        g.ln.st_out[((int64_t)row * g.ln.nt_out + n0 / BN) * 2 + (threadIdx.x & 1)] = lst[threadIdx.x];
     }
     return;
   }
@@ -839,7 +905,7 @@ __device__ __forceinline__ void epilogue_scan_lists(const PArgs& g, const f32x4 
   }
 }
 
-template <bool AK, bool BK_, typename TO, int EPI, int F8 = 0>
+template <bool AK, bool BK_, typename TO, int EPI, int F8 = 0, bool LN = false>
 __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
   const int tiles_m = (g.M + BM - 1) / BM;
@@ -899,7 +965,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   }
 #endif
   if (g.P != nullptr || g.vec_c) {
-    epilogue_vec<TO, EPI, F8>(g, acc, lds, m0, n0, batch, grp, wn, wave, lane);
+    epilogue_vec<TO, EPI, F8, LN>(g, acc, lds, m0, n0, batch, grp, wn, wave, lane);
     return;
   }
   // scalar epilogue (unaligned C / R)
@@ -1184,6 +1250,21 @@ void run_fp8(int epi, const PArgs& a, hipStream_t st) {
     break;
     IRC_PP8(0) IRC_PP8(1) IRC_PP8(2) IRC_PP8(3)
 #undef IRC_PP8
+  }
+}
+
+// LayerNorm-fold GEMM (irc_gemm_ln): bf16 A / B K-major, bf16 C, epilogues 1-3
+void run_ln(int epi, const PArgs& a, hipStream_t st) {
+  const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
+  const dim3 grid((unsigned)tiles);
+  switch (epi) {
+#define IRC_PPL(E)                                                                             \
+  case E:                                                                                      \
+    hipLaunchKernelGGL((gemm_pp_kernel<true, true, unsigned short, E, 0, true>), grid, dim3(NT), \
+                       0, st, a);                                                              \
+    break;
+    IRC_PPL(1) IRC_PPL(2) IRC_PPL(3)
+#undef IRC_PPL
   }
 }
 

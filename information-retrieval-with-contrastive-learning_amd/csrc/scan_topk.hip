@@ -2051,8 +2051,8 @@ static int ltop_max_q() {
   return v;
 }
 
-// IRC_SCAN_PPL=0 disables the single-pass GEMM filter; IRC_SCAN_PPL_MINQ (default 65)
-// is its smallest Q (its largest is 256, one query tile).
+// IRC_SCAN_PPL_MINQ sets the smallest Q of the single-pass GEMM filter (its largest is
+// 256, one query tile); unset or IRC_SCAN_PPL=0: off.
 // irc_scan_set_ppl_min_q changes it at run time (the tests compare both pipelines).
 static std::atomic<int>& ppl_min_q_ref() {
   static std::atomic<int> v{[] {

@@ -148,6 +148,8 @@ class BertModel(nn.Module):
         # "bf16" (default) or "fp8": MX-fp8 weights and inputs (e4m3 with one E8M0 scale
         # per 32 consecutive values) for every nn.Linear of the frozen encoder (config C5)
         self.weight_format = os.environ.get("IRC_ENCODER_WEIGHTS", "bf16")
+        # LayerNorm fold of the bf16 encoder (_encode_folded); IRC_LN_FOLD=0 / 1 overrides
+        self.ln_fold = os.environ.get("IRC_LN_FOLD", "0") != "0"
         self.eval()
 
     # HF _init_weights: normal(0, 0.02) for Linear/Embedding, padding row 0, LN (1, 0)
@@ -234,6 +236,78 @@ class BertModel(nn.Module):
         self._cache = {key: w}
         return w
 
+    def _fold_weights(self, w):
+        """The LayerNorm fold's operands (bf16 mode): each GEMM that reads a LayerNorm
+        output instead reads the pre-LN activation h, with W' = bf16(W diag(gamma)),
+        s = sum_k W'[n, k] (fp32 over the bf16 values the MFMA sees) and
+        t = bias + W beta (fp32), so that LN(h) . W^T + b = r (h . W'^T) - r mu s + t
+        per row (mu, r = 1 / sqrt(var + eps) of h; irc_gemm_ln).  FFN1 folds its
+        layer's LN1, QKV of layer l >= 1 folds layer l-1's LN2."""
+        f = w.get("fold")  # cached with the cast weights (same invalidation)
+        if f is not None:
+            return f
+
+        def fold(W, bias, ln):
+            W = W.detach().float()
+            wf = (W * ln.weight.detach().float()[None, :]).to(torch.bfloat16).contiguous()
+            s = wf.float().sum(1).contiguous()
+            t = (bias.detach().float() + W @ ln.bias.detach().float()).contiguous()
+            return wf, s, t
+
+        f = []
+        layers = self.encoder.layer
+        for li, lyr in enumerate(layers):
+            e = {}
+            dense = lyr.intermediate.dense
+            e["w1"], e["s1"], e["t1"] = fold(dense.weight, dense.bias, lyr.attention.output.LayerNorm)
+            if li > 0:
+                sa = lyr.attention.self
+                e["wqkv"], e["sqkv"], e["tqkv"] = fold(
+                    torch.cat([sa.query.weight, sa.key.weight, sa.value.weight], 0),
+                    torch.cat([sa.query.bias, sa.key.bias, sa.value.bias], 0),
+                    layers[li - 1].output.LayerNorm)
+            f.append(e)
+        w["fold"] = f
+        return f
+
+    def _encode_folded(self, ids, mask, w):
+        """encode() with every LayerNorm but the last folded into the GEMMs around it
+        (irc_gemm_ln): the out-projection and FFN2 write the pre-LN activation plus its
+        per-row (sum, sum of squares) partials from their epilogue, the next GEMM that
+        reads LN(h) takes h with W' and applies r, -r mu s and t in its epilogue, and the
+        residual adds LN(h) recomputed from the same statistics, rounded to bf16 as the
+        LayerNorm kernel writes it.  Removes 2 x layers - 1 LayerNorm passes
+        (read + write of [B*L, H] each)."""
+        c = self.config
+        B, L = ids.shape
+        H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
+        fw = self._fold_weights(w)
+        x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
+        h2 = st2 = None
+        prev = None
+        for li, lw in enumerate(w["layers"]):
+            f = fw[li]
+            if li == 0:
+                qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
+            else:
+                qkv = ops.gemm_ln(h2, f["wqkv"], f["tqkv"], epilogue=ops.EPI_BIAS, stats=st2,
+                                  eps=eps, colsum=f["sqkv"])
+            ctx = ops.attention(qkv, mask, B, L, H, heads)
+            if li == 0:
+                h1, st1 = ops.gemm_ln(ctx, lw["wo"], lw["bo"], epilogue=ops.EPI_BIAS_RESID,
+                                      residual=x, want_stats=True)
+            else:
+                h1, st1 = ops.gemm_ln(ctx, lw["wo"], lw["bo"], epilogue=ops.EPI_BIAS_RESID,
+                                      residual=h2, stats=st2, gamma=prev["ln2_g"],
+                                      beta=prev["ln2_b"], eps=eps, want_stats=True)
+            u = ops.gemm_ln(h1, f["w1"], f["t1"], epilogue=ops.EPI_BIAS_GELU, stats=st1, eps=eps,
+                            colsum=f["s1"])
+            h2, st2 = ops.gemm_ln(u, lw["w2"], lw["b2"], epilogue=ops.EPI_BIAS_RESID, residual=h1,
+                                  stats=st1, gamma=lw["ln1_g"], beta=lw["ln1_b"], eps=eps,
+                                  want_stats=True)
+            prev = lw
+        return ops.layernorm(h2, prev["ln2_g"], prev["ln2_b"], eps, out=h2)
+
     @torch.no_grad()
     def encode(self, input_ids: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
         """last_hidden_state [B, L, H] in the compute dtype (bf16 or fp32)."""
@@ -247,6 +321,8 @@ class BertModel(nn.Module):
         w = self._weights()
         if self._fp8_mode():
             return self._encode_fp8(ids, mask, w).view(B, L, H)
+        if self.ln_fold and compute_dtype() == torch.bfloat16:
+            return self._encode_folded(ids, mask, w).view(B, L, H)
         x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
         for lw in w["layers"]:
             qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)

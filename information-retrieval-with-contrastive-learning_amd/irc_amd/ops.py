@@ -6,6 +6,8 @@ fallback: a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
@@ -31,6 +33,51 @@ def gemm_set_big_ring(on) -> int:
     faster on MI355X).  Bit-identical results.
     Returns the previous setting."""
     return int(_lib.load().irc_gemm_set_big_ring(1 if on else 0))
+
+
+class LnStats:
+    """Per-row statistics of a pre-LayerNorm activation: partial (sum, sum of squares)
+    pairs over column tiles, [rows, nt, 2] fp32, written by irc_gemm_ln."""
+
+    def __init__(self, t: torch.Tensor, nt: int, h: int):
+        self.t, self.nt, self.h = t, nt, h
+
+
+def gemm_ln(a, b, bias, *, epilogue, stats=None, gamma=None, beta=None, eps=1e-12,
+            colsum=None, residual=None, want_stats=False, out=None):
+    """irc_gemm_ln (include/irc.h): the BERT encoder's LayerNorm-fold GEMMs, bf16.
+    epilogue EPI_BIAS / EPI_BIAS_GELU: out = LN(a) . W^T + bias' with b = W diag(gamma)
+    (the fold: stats of a, colsum of b); EPI_BIAS_RESID: out = a . b^T + bias + LN(residual)
+    (stats, gamma, beta of the residual) or + residual.  Returns out, or (out, LnStats)."""
+    require_hip(a, b, bias, residual, out)
+    for t in (a, b, residual, out):
+        if t is not None and (t.dtype != BF16 or t.dim() != 2 or t.stride(-1) != 1):
+            raise TypeError("gemm_ln: a, b, residual and out must be 2-D bf16, unit column stride")
+    for t in (bias, gamma, beta, colsum):
+        if t is not None and (t.dtype != F32 or not t.is_contiguous()):
+            raise TypeError("gemm_ln: bias, gamma, beta and colsum must be contiguous fp32")
+    M, K = a.shape
+    N = b.shape[0]
+    if b.shape[1] != K:
+        raise ValueError(f"gemm_ln inner dims differ: {K} vs {b.shape[1]}")
+    if stats is not None and (stats.t.shape[0] != M or stats.h != K):
+        raise ValueError("gemm_ln: the statistics describe another activation")
+    if out is None:
+        out = torch.empty((M, N), dtype=BF16, device=a.device)
+    st_out = None
+    if want_stats:
+        st_out = torch.empty((M, (N + 127) // 128, 2), dtype=F32, device=a.device)
+    nt = ctypes.c_int(0)
+    _lib.call("irc_gemm_ln", int(epilogue), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
+              ptr(bias), ptr(residual), residual.stride(0) if residual is not None else 0,
+              ptr(out), out.stride(0), ptr(stats.t) if stats is not None else None,
+              stats.nt if stats is not None else 0, ptr(gamma), ptr(beta), float(eps),
+              stats.h if stats is not None else 0, ptr(colsum), ptr(st_out),
+              ctypes.addressof(nt) if want_stats else None, stream_ptr(a.device))
+    if want_stats:
+        n = int(nt.value)
+        return out, LnStats(st_out.view(-1)[:M * n * 2].view(M, n, 2), n, N)
+    return out
 
 
 def gemm_set_big_mf16(on) -> int:
