@@ -60,7 +60,8 @@ def gemm_ln(a, b, bias, *, epilogue, stats=None, gamma=None, beta=None, eps=1e-1
     N = b.shape[0]
     if b.shape[1] != K:
         raise ValueError(f"gemm_ln inner dims differ: {K} vs {b.shape[1]}")
-    if stats is not None and (stats.t.shape[0] != M or stats.h != K):
+    # the statistics describe a (the fold, epilogues 1 / 2) or the residual (epilogue 3)
+    if stats is not None and (stats.t.shape[0] != M or stats.h != (N if residual is not None else K)):
         raise ValueError("gemm_ln: the statistics describe another activation")
     if out is None:
         out = torch.empty((M, N), dtype=BF16, device=a.device)

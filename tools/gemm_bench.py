@@ -26,6 +26,12 @@ SHAPES = [  # (name, M, N, K, epilogue)
     ("square4k", 4096, 4096, 4096, 0),
     ("dW_ih^T", 1024, 768, 16384, -1),   # dg^T x: both operands K-outer, split-K
     ("dW_hh^T", 1024, 256, 16384, -1),
+    # trainable BERT-base forward at 256 anchors x L=64 = 16384 rows (epi 6: bias + GELU,
+    # pre-activation saved for the backward)
+    ("bert_fwd_qkv", 16384, 2304, 768, 1),
+    ("bert_fwd_o", 16384, 768, 768, 3),
+    ("bert_fwd_ffn1", 16384, 3072, 768, 6),
+    ("bert_fwd_ffn2", 16384, 768, 3072, 3),
     # trainable BERT-base backward (256 anchors x L=64 -> 16384 rows)
     ("bert_dx_ffn2", 16384, 3072, 768, 5),   # dU = (dS2 W2) * gelu'(u)
     ("bert_dx_ffn1", 16384, 768, 3072, 4),   # dA = dU W1 + dS2
@@ -46,7 +52,8 @@ def main():
     ap.add_argument("--layouts", action="store_true")
     ap.add_argument("--only", default="", help="comma-separated shape names")
     ap.add_argument("--mx", action="store_true", help="MX-fp8 GEMMs (irc_gemm_mx) of the BERT shapes")
-    ap.add_argument("--mf16", default="0", help="big-tile MFMA shape: 0, 1 or 'ab' (interleaved)")
+    ap.add_argument("--mf16", default="", help="big-tile MFMA shape: 0, 1 or 'ab' (interleaved); "
+                    "default: the library's setting")
     args = ap.parse_args()
     only = set(filter(None, args.only.split(",")))
     if args.mx:
@@ -99,17 +106,20 @@ def main():
             continue
         a = torch.randn((M, K), device=dev).to(torch.bfloat16)
         b = torch.randn((N, K), device=dev).to(torch.bfloat16)
-        bias = torch.randn((N,), device=dev) if epi in (1, 2, 3) else None
-        res = torch.randn((M, N), device=dev).to(torch.bfloat16) if epi in (3, 4, 5) else None
+        bias = torch.randn((N,), device=dev) if epi in (1, 2, 3, 6) else None
+        res = torch.randn((M, N), device=dev).to(torch.bfloat16) if epi in (3, 4, 5, 6) else None
         od = torch.float32 if name in ("lstm_dx",) or name.startswith("lstm_xp") else torch.bfloat16
         if name.startswith("scan"):
             od = torch.bfloat16
         if res is not None:
             res = res.to(od)
         out = torch.empty((M, N), device=dev, dtype=od)
-        modes = (0, 1, 0, 1) if args.mf16 == "ab" else (int(args.mf16),)
+        modes = (0, 1, 0, 1) if args.mf16 == "ab" else ((int(args.mf16),) if args.mf16 else (None,))
+        prev = None
         for mode in modes:
-            ops.gemm_set_big_mf16(mode)
+            if mode is not None:
+                p0 = ops.gemm_set_big_mf16(mode)
+                prev = p0 if prev is None else prev
             for _ in range(3):
                 ops.gemm(a, b, bias=bias, epilogue=epi, residual=res, out=out)
             st = torch.cuda.current_stream()
@@ -121,10 +131,11 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / args.iters
             tf = 2.0 * M * N * K / us / 1e6
-            tag = f" mf16={mode}" if args.mf16 != "0" else ""
+            tag = f" mf16={mode}" if mode is not None else ""
             print(f"{name:14s} M={M:6d} N={N:5d} K={K:5d} epi={epi}{tag}  {us:9.1f} us  "
                   f"{tf:7.1f} TF/s  {tf / 2500:.1%}", flush=True)
-        ops.gemm_set_big_mf16(0)
+        if prev is not None:
+            ops.gemm_set_big_mf16(prev)
 
 
 def mx_shapes(args):
