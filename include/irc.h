@@ -181,6 +181,16 @@ int irc_layernorm(int dtype, const void* x, void* y, const float* gamma, const f
                   int64_t rows, int64_t H, float eps, irc_stream_t stream);
 int irc_attention(int dtype, const void* qkv, const int64_t* mask, void* ctx, int64_t B,
                   int64_t L, int64_t H, int64_t heads, irc_stream_t stream);
+/* QKV projection + self-attention in one launch (replaces irc_gemm(QKV) + irc_attention
+ * for the bf16 frozen encoder at L = 64, head dim 64, H % 128 == 0): ctx [M = B*64][H]
+ * (row stride ldc) = attention(x . Wqkv^T + b) with the same arithmetic as the unfused
+ * pair.  wqkv_perm / bias_perm: Wqkv [3H][H] and its bias with the rows permuted so that
+ * each 384-row block n holds the Q, K, V rows of heads 2n and 2n + 1 (64 each, in that
+ * order) -- the QKV activation never leaves the CU.  x [M][H] (row stride ldx), mask
+ * [M / 64][64] int64 (nonzero = visible) or NULL. */
+int irc_qkv_attention(int64_t M, int64_t H, int64_t heads, int64_t L, const void* x, int64_t ldx,
+                      const void* wqkv_perm, const float* bias_perm, const int64_t* mask,
+                      void* ctx, int64_t ldc, irc_stream_t stream);
 
 /* ----------------------------------------------------- BERT encoder backward
  * Gradients of the forward above for the trainable bi-encoder (`--model BERT`,

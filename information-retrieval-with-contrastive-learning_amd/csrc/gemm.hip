@@ -540,6 +540,66 @@ __device__ __forceinline__ void stage4(const unsigned short* __restrict__ X, int
     glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
   }
 }
+
+// The 2-slot K loop in its 16x16x32 form (gemm_big_kernel MF16, qkv_attn_kernel) over
+// the 256 x (128 WNB) tile at (m0, n0): wave (wm, wn) = (wave >> 2, wave & 3) accumulates
+// acc4[i][j] element e = C[m0 + 128 wm + 16 i + 4 (lane >> 4) + e][n0 + 32 WNB wn + 16 j +
+// (lane & 15)].  The chunk key (r >> 1) & 7 stays conflict free for the 16x16x32 fragment
+// reads (lane l: row l & 15, chunk 4 s + (l >> 4): each 16-lane group covers 16 distinct
+// 16-byte bank slots).  Ends with every wave past its last LDS read (LDS free).
+template <int WNB>
+__device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t lda,
+                                              const unsigned short* B, int64_t ldb, int m0,
+                                              int n0, int M, int N, int K, char* lds, int wave,
+                                              int lane, f32x4 (&acc4)[8][2 * WNB]) {
+  constexpr int BN = 128 * WNB;
+  constexpr int A_BYTES = BM * ROW_BYTES, STAGE = A_BYTES + BN * ROW_BYTES;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nk = K / BK;
+  stage<BM>(A, lda, m0, M, 0, lds, wave, lane);
+  stage<BN>(B, ldb, n0, N, 0, lds + A_BYTES, wave, lane);
+  wait_vmcnt<0>();
+  __syncthreads();
+  const int l16 = lane & 15, q4 = lane >> 4;
+  const int key = chunk_key(l16);  // rows 16 i + l16: (row >> 1) & 7 = (l16 >> 1) & 7
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+#ifdef IRC_PP_DIAG_NODMA  // diagnostic build: only K-tile 0 is loaded
+    const bool more = kt + 1 < nk && kt < 0;
+#else
+    const bool more = kt + 1 < nk;
+#endif
+    if (more) {
+      char* nxt = lds + (cur ^ 1) * STAGE;
+      // the DMA addresses are re-derived per K-tile (kept live through the loop they
+      // would push the 16x16 fragments into spills)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln);
+      stage<BN>(B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
+    }
+    const char* la = lds + cur * STAGE;
+    const char* lb = la + A_BYTES;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int coff = (((4 * s2 + q4) ^ key) * 16);
+      bf16x8 fa[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 16 + l16) * 128 + coff);
+#pragma unroll
+      for (int j = 0; j < 2 * WNB; ++j) {
+        const bf16x8 fb =
+            *reinterpret_cast<const bf16x8*>(lb + (wn * 32 * WNB + j * 16 + l16) * 128 + coff);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc4[i][j], 0, 0, 0);
+      }
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+}
 }  // namespace big
 
 // IRC_BIG_RING=1 selects the 4-slot ring of gemm_big_kernel (A/B; read on first use;
@@ -665,6 +725,8 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
       }
     }
     __syncthreads();  // the epilogue's staging rows overlap the ring
+  } else if constexpr (MF16) {
+    big::mainloop_mf16<WNB>(A, g.lda, B, g.ldb, m0, n0, g.M, g.N, g.K, lds, wave, lane, acc4);
   } else {
   const int nk = g.K / BK;
   big::stage<BM>(A, g.lda, m0, g.M, 0, lds, wave, lane);
@@ -682,39 +744,12 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 #ifndef IRC_BIG_SPREAD
     if (more) {
       char* nxt = lds + (cur ^ 1) * STAGE;
-      // MF16: the DMA addresses are re-derived per K-tile (kept live through the loop
-      // they would push the 16x16 fragments into spills)
-      int ln = lane;
-      if constexpr (MF16) asm volatile("" : "+v"(ln));
-      big::stage<BM>(A, g.lda, m0, g.M, (kt + 1) * BK, nxt, wave, ln);
-      big::stage<BN>(B, g.ldb, n0, g.N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
+      big::stage<BM>(A, g.lda, m0, g.M, (kt + 1) * BK, nxt, wave, lane);
+      big::stage<BN>(B, g.ldb, n0, g.N, (kt + 1) * BK, nxt + A_BYTES, wave, lane);
     }
 #endif
     const char* la = lds + cur * STAGE;
     const char* lb = la + A_BYTES;
-    if constexpr (MF16) {
-      const int l16 = lane & 15, q4 = lane >> 4;
-      const int key = big::chunk_key(l16);  // rows 16 i + l16: (row >> 1) & 7 = (l16 >> 1) & 7
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const int coff = (((4 * s2 + q4) ^ key) * 16);
-        bf16x8 fa[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 16 + l16) * 128 + coff);
-#pragma unroll
-        for (int j = 0; j < 2 * WNB; ++j) {
-          const bf16x8 fb =
-              *reinterpret_cast<const bf16x8*>(lb + (wn * 32 * WNB + j * 16 + l16) * 128 + coff);
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-            acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc4[i][j], 0, 0, 0);
-        }
-      }
-      wait_vmcnt<0>();
-      __syncthreads();
-      continue;
-    }
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
 #ifdef IRC_BIG_SPREAD  // A/B build: the next K-tile's DMA spread over the 4 k-steps
@@ -1015,6 +1050,188 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// QKV projection + self-attention in one launch: the frozen encoder's BertSelfAttention
+// (modeling_bert, reached from contrastive_module.py:36-41) at L = 64, head dim 64.
+// The Wqkv rows are permuted so that output tile column block n (384 wide) holds
+// [Q | K | V] of heads 2n and 2n + 1 (64 columns each), and a 256-row tile holds four
+// whole sequences; the QKV activation then never leaves the CU.  Main loop: the big-tile
+// kernel's 16x16x32 2-slot loop (WNB = 3).  Epilogue, per 128-row half (the waves with
+// wm == half own its accumulators): those 4 waves write bf16(acc + bias) into LDS
+// [128][392] (the same bf16 values the unfused GEMM stores), then each of them runs attention for
+// one (sequence, head) pair with attention_mfma_kernel's arithmetic (encoder.hip: S^T by
+// 32x32x16 MFMAs, scale, mask bias, max / exp / sum, P rounded to bf16, P.V), so the
+// context equals the unfused QKV GEMM + irc_attention output bit for bit wherever the
+// unfused QKV runs on this main loop (the big-tile shapes).  The halves run one after
+// the other; every wave first packs its accumulators to bf16 pairs (96 VGPRs), so the
+// waiting half's values and the attention's registers fit side by side.
+typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+struct QaArgs {
+  const unsigned short* x;  // [M][K] layer input
+  const unsigned short* w;  // [3H][K] head-pair-permuted Wqkv
+  const float* bias;        // [3H] permuted bias
+  const int64_t* mask;      // [M / 64][64], nonzero = key visible; null = all visible
+  unsigned short* ctx;      // [M][H] (row stride ldc)
+  int M, K, H;
+  int64_t ldx, ldc;
+  float scale;
+};
+
+__global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
+  constexpr int WNB = 3, BM = big::BM, BN = 128 * WNB, TP = BN + 8;  // L = 64
+  __shared__ __attribute__((aligned(1024))) char lds[2 * (BM + BN) * big::ROW_BYTES];
+  static_assert(128 * TP * 2 + 4 * 64 * 4 <= 2 * (BM + BN) * big::ROW_BYTES,
+                "staged half and mask biases fit the LDS");
+  const int tiles_m = (g.M + BM - 1) / BM;
+  const int tiles_n = 3 * g.H / BN;
+  const int ntiles = tiles_m * tiles_n;
+  int bid = blockIdx.x;
+  {  // XCD-aware bijective remap, as gemm_big_kernel
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
+  int tm, tn;
+  grouped_tile(bid, tiles_m, tiles_n, 0, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  f32x4 acc4[8][2 * WNB];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 2 * WNB; ++j) acc4[i][j] = (f32x4)0.0f;
+  big::mainloop_mf16<WNB>(g.x, g.ldx, g.w, g.K, m0, n0, g.M, 3 * g.H, g.K, lds, wave, lane, acc4);
+
+  unsigned short* T = reinterpret_cast<unsigned short*>(lds);    // [128][TP] staged half
+  float* mbw = reinterpret_cast<float*>(lds + 128 * TP * 2) + 64 * wn;  // this wave's mask bias
+  // acc + bias -> bf16 pairs (rows e, e + 1 of one column) in registers:
+  // 96 VGPRs instead of 192 live while the halves take turns through the LDS
+  uint32_t pk[8][2 * WNB][2];
+#pragma unroll
+  for (int j = 0; j < 2 * WNB; ++j) {
+    const int col = n0 + wn * 32 * WNB + 16 * j + (lane & 15);
+    const float bvj = g.bias[col];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e2 = 0; e2 < 2; ++e2) {
+        f32x2_t v;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) v[u] = acc4[i][j][2 * e2 + u] * 1.0f + bvj;
+        // one v_cvt_pk_bf16_f32 per pair (RNE, as f32_to_bf16); opaque, so the compiler
+        // cannot forward the unpacked values to the staging stores and keep 192 live
+        uint32_t w = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_v));
+        asm volatile("" : "+v"(w));
+        pk[i][j][e2] = w;
+      }
+  }
+  const int h = lane >> 5, r32 = lane & 31;
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    if (wm == hf) {  // this half's accumulators -> T [128][TP]
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2 * WNB; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rl = 16 * i + 4 * (lane >> 4) + e;
+            T[rl * TP + wn * 32 * WNB + 16 * j + (lane & 15)] =
+                (unsigned short)(pk[i][j][e >> 1] >> (16 * (e & 1)));
+          }
+    }
+    __syncthreads();  // the half is staged
+    // attention of (sequence wn >> 1, head 2 tn + (wn & 1)) of this half: 64 queries
+    const int sl = wn >> 1, hh = wn & 1;
+    const int r0 = m0 + 128 * hf + 64 * sl;  // first token of the sequence
+    if (wm == hf && r0 < g.M) {
+      mbw[lane] = (g.mask == nullptr || g.mask[r0 + lane] != 0) ? 0.f : -1e30f;
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const unsigned short* Ts = T + 64 * sl * TP;
+      const unsigned short* Q = Ts + hh * 64;
+      const unsigned short* Kp = Ts + 128 + hh * 64;
+      const unsigned short* V = Ts + 256 + hh * 64;
+      unsigned short* out = g.ctx + (int64_t)r0 * g.ldc + (2 * tn + hh) * 64;
+#pragma unroll 1
+      for (int ib = 0; ib < 2; ++ib) {
+        bf16x8 qf[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          qf[kk] = *reinterpret_cast<const bf16x8*>(Q + (32 * ib + r32) * TP + 16 * kk + 8 * h);
+        f32x16 sc[2];
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          sc[jb] = (f32x16)0.f;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const bf16x8 kf =
+                *reinterpret_cast<const bf16x8*>(Kp + (32 * jb + r32) * TP + 16 * kk + 8 * h);
+            sc[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[jb], 0, 0, 0);
+          }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 bias = *reinterpret_cast<const f32x4*>(&mbw[32 * jb + 8 * q + 4 * h]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = sc[jb][4 * q + r] * g.scale + bias[r];
+              sc[jb][4 * q + r] = v;
+              mx = fmaxf(mx, v);
+            }
+          }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        float sum = 0.f;
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float p = __expf(sc[jb][e] - mx);
+            sc[jb][e] = p;
+            sum += p;
+          }
+        sum += __shfl_xor(sum, 32, 64);
+        const float inv = 1.f / sum;
+        f32x16 o[2] = {(f32x16)0.f, (f32x16)0.f};
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+          for (int k2 = 0; k2 < 2; ++k2) {
+            bf16x8 pa;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) pa[t] = (__bf16)(sc[jb][8 * k2 + t] * inv);
+            const int j0 = 32 * jb + 16 * k2 + 4 * h;  // keys: t < 4: j0 + t; else j0 + 8 + t - 4
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+              const unsigned short* vc = V + 32 * db + r32;
+              u16x8 vv;
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                vv[t] = vc[(j0 + t) * TP];
+                vv[4 + t] = vc[(j0 + 8 + t) * TP];
+              }
+              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(bf16x8, vv),
+                                                              o[db], 0, 0, 0);
+            }
+          }
+        // O: col = d (32 db + r32), row = query 32 ib + (e & 3) + 8 (e >> 2) + 4 h
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int i = 32 * ib + (e & 3) + 8 * (e >> 2) + 4 * h;
+            out[(int64_t)i * g.ldc + 32 * db + r32] = f32_to_bf16(o[db][e]);
+          }
+      }
+    }
+    if (hf == 0) __syncthreads();  // the half's readers are done with T
+  }
+}
+
 // The large-tile path applies: bf16 in, A [M][K] and B [N][K], aligned, K % 64,
 // and enough tiles to occupy the chip.  Returns the per-wave N blocks (0: no).
 inline int big_wnb(const Args& g, int batch, int la, int lb) {
@@ -1206,6 +1423,33 @@ extern "C" int irc_gemm_ln(int epilogue, int64_t M, int64_t N, int64_t K, const 
     case EPI_BIAS_GELU: return launch_big<unsigned short, EPI_BIAS_GELU, true>(g, 1, wnb, st);
     default: return launch_big<unsigned short, EPI_BIAS_RESID, true>(g, 1, wnb, st);
   }
+}
+
+// QKV projection + attention in one launch (include/irc.h irc_qkv_attention; see
+// qkv_attn_kernel): L = 64, head dim 64, H % 128 == 0.
+extern "C" int irc_qkv_attention(int64_t M, int64_t H, int64_t heads, int64_t L, const void* x,
+                                 int64_t ldx, const void* wqkv_perm, const float* bias_perm,
+                                 const int64_t* mask, void* ctx, int64_t ldc,
+                                 irc_stream_t stream) {
+  using namespace irc::gemm;
+  IRC_REQUIRE(L == 64 && heads * 64 == H && H % 128 == 0,
+              "qkv_attention: needs L = 64, head dim 64 and H %% 128 == 0");
+  IRC_REQUIRE(M > 0 && M % 64 == 0 && M < (1ll << 31), "qkv_attention: M must be a multiple of L");
+  IRC_REQUIRE(H % 64 == 0 && ldx % 8 == 0 && ldx >= H && ldc >= H, "qkv_attention: bad strides");
+  IRC_REQUIRE((((uintptr_t)x | (uintptr_t)wqkv_perm) % 16) == 0 && ((uintptr_t)ctx % 2) == 0,
+              "qkv_attention: operands must be 16-byte aligned");
+  IRC_REQUIRE(bias_perm != nullptr, "qkv_attention: bias required");
+  QaArgs a{static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(wqkv_perm),
+           bias_perm, mask, static_cast<unsigned short*>(ctx), (int)M, (int)H, (int)H, ldx, ldc,
+           0.125f};
+  hipStream_t st = as_stream(stream);
+  const int tiles = (int)((M + big::BM - 1) / big::BM) * (int)(3 * H / 384);
+  prof_begin(st);
+  hipLaunchKernelGGL(qkv_attn_kernel, dim3(tiles), dim3(big::NT), 0, st, a);
+  // a GEMM with an attention epilogue: its flops and bytes (x, Wqkv, ctx) count as one
+  prof_end("gemm_bf16", st, 2.0 * M * 3 * H * H + 4.0 * M * L * H);
+  prof_work("gemm_bf16_bytes", 2.0 * (double)M * H + 2.0 * 3 * H * H + 2.0 * (double)M * H);
+  return check_launch("qkv_attn_kernel");
 }
 
 // 16x16x32 (1) or 32x32x16 (0) MFMAs in the big-tile kernel's 2-slot loop; returns the

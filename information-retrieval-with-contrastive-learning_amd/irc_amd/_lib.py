@@ -61,6 +61,7 @@ SIGNATURES = {
     "irc_embed_ln": (I32, [I32, P, P, P, P, P, P, P, I64, I64, I64, F32, P]),
     "irc_layernorm": (I32, [I32, P, P, P, P, I64, I64, F32, P]),
     "irc_attention": (I32, [I32, P, P, P, I64, I64, I64, I64, P]),
+    "irc_qkv_attention": (I32, [I64, I64, I64, I64, P, I64, P, P, P, P, I64, P]),
     "irc_layernorm_bwd_workspace": (I64, [I64, I64]),
     "irc_layernorm_bwd": (I32, [I32, I32, P, P, P, P, P, P, P, I64, I64, I64, F32, I64, F32, I32,
                                 P]),

@@ -150,6 +150,9 @@ class BertModel(nn.Module):
         self.weight_format = os.environ.get("IRC_ENCODER_WEIGHTS", "bf16")
         # LayerNorm fold of the bf16 encoder (_encode_folded); IRC_LN_FOLD=0 / 1 overrides
         self.ln_fold = os.environ.get("IRC_LN_FOLD", "0") != "0"
+        # QKV projection + attention in one launch where it applies (bf16, L = 64, head
+        # dim 64; irc_qkv_attention); IRC_QKV_ATTN=0 keeps the two-launch form
+        self.fused_attention = os.environ.get("IRC_QKV_ATTN", "0") != "0"
         self.eval()
 
     # HF _init_weights: normal(0, 0.02) for Linear/Embedding, padding row 0, LN (1, 0)
@@ -308,6 +311,17 @@ class BertModel(nn.Module):
             prev = lw
         return ops.layernorm(h2, prev["ln2_g"], prev["ln2_b"], eps, out=h2)
 
+    def _qkv_attention(self, x, lw, mask, B, L, H, heads):
+        """ctx of one layer: one fused launch where it applies, else QKV GEMM + attention."""
+        if self.fused_attention and ops.qkv_attention_supported(L, H, heads):
+            if "wqkv_p" not in lw:  # permuted once per cast weight set
+                perm = ops.qkv_perm_index(H, lw["wqkv"].device)
+                lw["wqkv_p"] = lw["wqkv"].index_select(0, perm).contiguous()
+                lw["bqkv_p"] = lw["bqkv"].index_select(0, perm).contiguous()
+            return ops.qkv_attention(x, lw["wqkv_p"], lw["bqkv_p"], mask, B, L, H, heads)
+        qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
+        return ops.attention(qkv, mask, B, L, H, heads)
+
     @torch.no_grad()
     def encode(self, input_ids: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
         """last_hidden_state [B, L, H] in the compute dtype (bf16 or fp32)."""
@@ -324,9 +338,13 @@ class BertModel(nn.Module):
         if self.ln_fold and compute_dtype() == torch.bfloat16:
             return self._encode_folded(ids, mask, w).view(B, L, H)
         x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
+        bf16 = compute_dtype() == torch.bfloat16
         for lw in w["layers"]:
-            qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
-            ctx = ops.attention(qkv, mask, B, L, H, heads)
+            if bf16:
+                ctx = self._qkv_attention(x, lw, mask, B, L, H, heads)
+            else:
+                qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
+                ctx = ops.attention(qkv, mask, B, L, H, heads)
             a = ops.gemm(ctx, lw["wo"], bias=lw["bo"], residual=x, epilogue=ops.EPI_BIAS_RESID)
             a = ops.layernorm(a, lw["ln1_g"], lw["ln1_b"], eps, out=a)
             i = ops.gemm(a, lw["w1"], bias=lw["b1"], epilogue=ops.EPI_BIAS_GELU)

@@ -180,6 +180,35 @@ def attention(qkv, mask, B, L, H, heads, out=None):
     return ctx
 
 
+def qkv_perm_index(H: int, device=None) -> torch.Tensor:
+    """Row order of Wqkv [3H][H] (query | key | value) for qkv_attention: block n of 384
+    rows = Q, K, V rows of heads 2n and 2n + 1 (head dim 64)."""
+    n = torch.arange(H // 128).view(-1, 1, 1) * 128
+    part = torch.arange(3).view(1, -1, 1) * H
+    return (n + part + torch.arange(128).view(1, 1, -1)).reshape(-1).to(device)
+
+
+def qkv_attention_supported(L: int, H: int, heads: int) -> bool:
+    return L == 64 and heads * 64 == H and H % 128 == 0
+
+
+def qkv_attention(x, wqkv_perm, bias_perm, mask, B, L, H, heads, out=None):
+    """irc_qkv_attention: ctx [B*L, H] bf16 = attention(x . Wqkv^T + b) in one launch
+    (the QKV activation stays on chip).  wqkv_perm / bias_perm: rows in qkv_perm_index
+    order.  Same result as gemm(EPI_BIAS) + attention on the big-tile shapes."""
+    require_hip(x, wqkv_perm, bias_perm, mask, out)
+    if x.dtype != BF16 or wqkv_perm.dtype != BF16 or bias_perm.dtype != F32:
+        raise TypeError("qkv_attention: bf16 x / weights, fp32 bias")
+    if not qkv_attention_supported(L, H, heads):
+        raise ValueError("qkv_attention: needs L = 64, head dim 64, H % 128 == 0")
+    if x.shape != (B * L, H) or x.stride(-1) != 1 or tuple(wqkv_perm.shape) != (3 * H, H):
+        raise ValueError("qkv_attention: x [B*L, H], Wqkv [3H, H]")
+    ctx = torch.empty((B * L, H), dtype=BF16, device=x.device) if out is None else out
+    _lib.call("irc_qkv_attention", B * L, H, heads, L, ptr(x), x.stride(0), ptr(wqkv_perm),
+              ptr(bias_perm), ptr(mask), ptr(ctx), ctx.stride(0), stream_ptr(x.device))
+    return ctx
+
+
 def lstm_fwd(xp, whh, B, L, H, ndir, h_dtype, save=True):
     """xp [B*L, ndir*4H] fp32 -> hout [B*L, ndir*H] (+ saved state for BPTT)."""
     require_hip(xp, whh)

@@ -1,0 +1,62 @@
+"""QKV projection + attention: one fused launch (irc_qkv_attention) against the two-launch
+form (irc_gemm EPI_BIAS + irc_attention) at the frozen encoder's shapes, interleaved.
+
+    python tools/qkv_attn_bench.py [--iters 20] [--h 768]
+
+Prints us per layer (HIP events on the launch stream) for each form, twice.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "information-retrieval-with-contrastive-learning_amd"))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--h", type=int, default=768)
+    ap.add_argument("--b", type=int, default=512)
+    a = ap.parse_args()
+    from irc_amd import ops
+
+    dev = torch.device("cuda:0")
+    B, L, H = a.b, 64, a.h
+    heads = H // 64
+    x = (torch.randn(B * L, H, device=dev) * 0.5).bfloat16()
+    w = (torch.randn(3 * H, H, device=dev) * 0.05).bfloat16()
+    b = torch.randn(3 * H, device=dev) * 0.1
+    mask = torch.ones(B, L, dtype=torch.int64, device=dev)
+    perm = ops.qkv_perm_index(H, dev)
+    wp, bp = w.index_select(0, perm).contiguous(), b.index_select(0, perm).contiguous()
+    qkv = torch.empty(B * L, 3 * H, dtype=torch.bfloat16, device=dev)
+    ctx = torch.empty(B * L, H, dtype=torch.bfloat16, device=dev)
+
+    def unfused():
+        ops.gemm(x, w, bias=b, epilogue=ops.EPI_BIAS, out=qkv)
+        ops.attention(qkv, mask, B, L, H, heads, out=ctx)
+
+    def fused():
+        ops.qkv_attention(x, wp, bp, mask, B, L, H, heads, out=ctx)
+
+    flops = 2.0 * B * L * 3 * H * H + 4.0 * B * L * L * H
+    for r in range(2):
+        for name, fn in (("unfused", unfused), ("fused", fused)):
+            for _ in range(3):
+                fn()
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.iters):
+                fn()
+            e1.record(st)
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.iters
+            print(f"H={H} M={B * L} {name:8s} {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
