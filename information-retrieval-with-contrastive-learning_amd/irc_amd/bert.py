@@ -152,7 +152,7 @@ class BertModel(nn.Module):
         self.ln_fold = os.environ.get("IRC_LN_FOLD", "0") != "0"
         # QKV projection + attention in one launch where it applies (bf16, L = 64, head
         # dim 64; irc_qkv_attention); IRC_QKV_ATTN=0 keeps the two-launch form
-        self.fused_attention = os.environ.get("IRC_QKV_ATTN", "0") != "0"
+        self.fused_attention = os.environ.get("IRC_QKV_ATTN", "1") != "0"
         self.eval()
 
     # HF _init_weights: normal(0, 0.02) for Linear/Embedding, padding row 0, LN (1, 0)
