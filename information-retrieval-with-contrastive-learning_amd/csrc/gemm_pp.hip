@@ -463,7 +463,7 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
 template <typename TO, int EPI, int F8, bool LN = false>
 __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[8][4], char* lds,
                                              int m0, int n0, int batch, int grp, int wn, int wave,
-                                             int lane) {
+                                             int lane, int split = 0) {
   const int rbase0 = m0 + 128 * grp;
   const int cbase = n0 + 64 * wn;
   float* st = reinterpret_cast<float*>(lds) + wave * (32 * EP_PITCH);
@@ -539,7 +539,7 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const int rbase = rbase0 + 32 * p;
       if (slab) {
-        float* P = g.P + ((int64_t)batch * gridDim.z + blockIdx.z) * g.M * g.N;
+        float* P = g.P + ((int64_t)batch * gridDim.z + split) * g.M * g.N;
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
           const int c = it * 64 + lane;
@@ -911,11 +911,34 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   const int tiles_m = (g.M + BM - 1) / BM;
   const int tiles_n = (g.N + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
-  int bid = blockIdx.x;
-  {  // XCD-aware bijective remap: blocks sharing an XCD walk consecutive tiles
+  // XCD-aware bijective remap over the whole grid: workgroups go to the 8 XCDs round
+  // robin in dispatch order (x fastest), so XCD x gets the contiguous run x of the work
+  // list (batch, split, tile), tile fastest -- the tiles of one K-slice / batch entry
+  // share their A and B K-tiles through one XCD's L2 (the K-outer dW GEMMs of the
+  // trainable encoder read 3.4-5x their operand bytes from HBM when the slices of a run
+  // spread over every XCD, profiles/r04_h_pmc_shapes_bert.txt)
+  int bid, batch, split;
+#ifdef IRC_PP_OLD_REMAP  // A/B build: the remap over blockIdx.x alone (rounds 2-3)
+  bid = blockIdx.x;
+  {
     const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
+  batch = blockIdx.y;
+  split = blockIdx.z;
+#else
+  {
+    const int nz = gridDim.y * gridDim.z;
+    const int total = ntiles * nz;
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int q = total / 8, r = total % 8, x = lin % 8;
+    const int w = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lin / 8;
+    bid = w % ntiles;
+    const int rest = w / ntiles;
+    split = rest % gridDim.z;
+    batch = rest / gridDim.z;
+  }
+#endif
   // EPI_SCAN: query tiles fastest, so the blocks of one doc tile run back to back
   // on one XCD and read it from that XCD's L2 (C4: 2048 queries = 8 query tiles)
   int tm, tn;
@@ -925,8 +948,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   } else {
     grouped_tile(bid, tiles_m, tiles_n, g.group_m, tm, tn);
   }
-  const int batch = blockIdx.y;
-  const int kbeg = blockIdx.z * g.kchunk;
+  const int kbeg = split * g.kchunk;
   const int kend = min(g.K, kbeg + g.kchunk);
   const int nk = (kend - kbeg) / BK;
   const unsigned short* A = g.A + batch * g.sA;
@@ -965,7 +987,7 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   }
 #endif
   if (g.P != nullptr || g.vec_c) {
-    epilogue_vec<TO, EPI, F8, LN>(g, acc, lds, m0, n0, batch, grp, wn, wave, lane);
+    epilogue_vec<TO, EPI, F8, LN>(g, acc, lds, m0, n0, batch, grp, wn, wave, lane, split);
     return;
   }
   // scalar epilogue (unaligned C / R)
