@@ -1058,9 +1058,10 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 // whole sequences; the QKV activation then never leaves the CU.  Main loop: the big-tile
 // kernel's 16x16x32 2-slot loop (WNB = 3).  Epilogue, per 128-row half (the waves with
 // wm == half own its accumulators): those 4 waves write bf16(acc + bias) into LDS
-// [128][392] (the same bf16 values the unfused GEMM stores), then each of them runs attention for
-// one (sequence, head) pair with attention_mfma_kernel's arithmetic (encoder.hip: S^T by
-// 32x32x16 MFMAs, scale, mask bias, max / exp / sum, P rounded to bf16, P.V), so the
+// [128][392] (the same bf16 values the unfused GEMM stores), then all 8 waves run its
+// attention, one (sequence, head, 32 queries) each, with attention_mfma_kernel's
+// arithmetic (encoder.hip: S^T by 32x32x16 MFMAs, scale, mask bias, max / exp / sum,
+// P rounded to bf16, P.V), so the
 // context equals the unfused QKV GEMM + irc_attention output bit for bit wherever the
 // unfused QKV runs on this main loop (the big-tile shapes).  The halves run one after
 // the other; every wave first packs its accumulators to bf16 pairs (96 VGPRs), so the
@@ -1080,7 +1081,7 @@ struct QaArgs {
 __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
   constexpr int WNB = 3, BM = big::BM, BN = 128 * WNB, TP = BN + 8;  // L = 64
   __shared__ __attribute__((aligned(1024))) char lds[2 * (BM + BN) * big::ROW_BYTES];
-  static_assert(128 * TP * 2 + 4 * 64 * 4 <= 2 * (BM + BN) * big::ROW_BYTES,
+  static_assert(128 * TP * 2 + 8 * 64 * 4 <= 2 * (BM + BN) * big::ROW_BYTES,
                 "staged half and mask biases fit the LDS");
   const int tiles_m = (g.M + BM - 1) / BM;
   const int tiles_n = 3 * g.H / BN;
@@ -1104,7 +1105,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
   big::mainloop_mf16<WNB>(g.x, g.ldx, g.w, g.K, m0, n0, g.M, 3 * g.H, g.K, lds, wave, lane, acc4);
 
   unsigned short* T = reinterpret_cast<unsigned short*>(lds);    // [128][TP] staged half
-  float* mbw = reinterpret_cast<float*>(lds + 128 * TP * 2) + 64 * wn;  // this wave's mask bias
+  float* mbw = reinterpret_cast<float*>(lds + 128 * TP * 2) + 64 * wave;  // this wave's mask bias
   // acc + bias -> bf16 pairs (rows e, e + 1 of one column) in registers:
   // 96 VGPRs instead of 192 live while the halves take turns through the LDS
   uint32_t pk[8][2 * WNB][2];
@@ -1142,10 +1143,11 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
           }
     }
     __syncthreads();  // the half is staged
-    // attention of (sequence wn >> 1, head 2 tn + (wn & 1)) of this half: 64 queries
+    // every wave: queries [32 wm, +32) of (sequence wn >> 1, head 2 tn + (wn & 1)) of
+    // this half (the other half's waves hold their packed values meanwhile)
     const int sl = wn >> 1, hh = wn & 1;
     const int r0 = m0 + 128 * hf + 64 * sl;  // first token of the sequence
-    if (wm == hf && r0 < g.M) {
+    if (r0 < g.M) {
       mbw[lane] = (g.mask == nullptr || g.mask[r0 + lane] != 0) ? 0.f : -1e30f;
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1154,8 +1156,8 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
       const unsigned short* Kp = Ts + 128 + hh * 64;
       const unsigned short* V = Ts + 256 + hh * 64;
       unsigned short* out = g.ctx + (int64_t)r0 * g.ldc + (2 * tn + hh) * 64;
-#pragma unroll 1
-      for (int ib = 0; ib < 2; ++ib) {
+      {
+        const int ib = wm;
         bf16x8 qf[4];
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk)

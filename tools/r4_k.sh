@@ -4,6 +4,10 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/r4k
 mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_qkv_attn_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
+timeout -k 10 120 python tools/qkv_attn_bench.py > $OUT/qkv_attn.txt 2>&1 || exit 1
+grep -v amdgpu $OUT/qkv_attn.txt
 for r in 1 2; do
   timeout -k 10 200 python tools/gemm_bench.py --only ffn1+gelu,ffn1+bias,ffn2+res > $OUT/ffn_pp_$r.txt 2>&1 || exit 1
   IRC_GEMM_PP=0 timeout -k 10 200 python tools/gemm_bench.py --only ffn1+gelu,ffn1+bias,ffn2+res > $OUT/ffn_big_$r.txt 2>&1 || exit 1
