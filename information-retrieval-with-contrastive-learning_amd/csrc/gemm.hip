@@ -541,6 +541,29 @@ __device__ __forceinline__ void stage4(const unsigned short* __restrict__ X, int
   }
 }
 
+#ifdef IRC_BIG_STAMPS  // diagnostic build: per-K-tile phase stamps of block 0, wave 0
+// [kt][phase]: s_memtime (shader clock) and s_memrealtime (100 MHz) after each phase of
+// mainloop_mf16 -- 0 loop top, 1 DMA issued, 2 fragment reads + MFMAs issued, 3 vmcnt(0)
+// returned, 4 barrier passed.  Read by irc_big_dbg_stamps (this build only).
+__device__ uint64_t big_stamps[64][5][2];
+#define BSTAMP(kt, i)                                                                      \
+  do {                                                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (kt) < 64) {                               \
+      uint64_t c_, r_;                                                                     \
+      asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)"            \
+                   : "=s"(c_), "=s"(r_)::"memory");                                        \
+      *(volatile uint64_t*)&big_stamps[(kt)][(i)][0] = c_;                                 \
+      *(volatile uint64_t*)&big_stamps[(kt)][(i)][1] = r_;                                 \
+    }                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+  } while (0)
+#else
+#define BSTAMP(kt, i) \
+  do {                \
+  } while (0)
+#endif
+
 // The 2-slot K loop in its 16x16x32 form (gemm_big_kernel MF16, qkv_attn_kernel) over
 // the 256 x (128 WNB) tile at (m0, n0): wave (wm, wn) = (wave >> 2, wave & 3) accumulates
 // acc4[i][j] element e = C[m0 + 128 wm + 16 i + 4 (lane >> 4) + e][n0 + 32 WNB wn + 16 j +
@@ -569,6 +592,7 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
 #else
     const bool more = kt + 1 < nk;
 #endif
+    BSTAMP(kt, 0);
     if (more) {
       char* nxt = lds + (cur ^ 1) * STAGE;
       // the DMA addresses are re-derived per K-tile (kept live through the loop they
@@ -578,6 +602,7 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
       stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln);
       stage<BN>(B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
     }
+    BSTAMP(kt, 1);
     const char* la = lds + cur * STAGE;
     const char* lb = la + A_BYTES;
 #pragma unroll
@@ -596,8 +621,11 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
           acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb, acc4[i][j], 0, 0, 0);
       }
     }
+    BSTAMP(kt, 2);
     wait_vmcnt<0>();
+    BSTAMP(kt, 3);
     __syncthreads();
+    BSTAMP(kt, 4);
   }
 }
 }  // namespace big
@@ -1453,6 +1481,14 @@ extern "C" int irc_qkv_attention(int64_t M, int64_t H, int64_t heads, int64_t L,
   prof_work("gemm_bf16_bytes", 2.0 * (double)M * H + 2.0 * 3 * H * H + 2.0 * (double)M * H);
   return check_launch("qkv_attn_kernel");
 }
+
+#ifdef IRC_BIG_STAMPS
+extern "C" int irc_big_dbg_stamps(uint64_t* out /* [64][5][2] */) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(irc::gemm::big::big_stamps),
+                             sizeof(irc::gemm::big::big_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // 16x16x32 (1) or 32x32x16 (0) MFMAs in the big-tile kernel's 2-slot loop; returns the
 // previous setting.
