@@ -500,6 +500,18 @@ __device__ __forceinline__ void stage(const unsigned short* __restrict__ X, int6
     glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
   }
 }
+// pass i of stage<ROWS> (i uniform; constant after unrolling)
+template <int ROWS>
+__device__ __forceinline__ void stage_one(int i, const unsigned short* __restrict__ X, int64_t ld,
+                                          int r0, int nrows, int k0, char* lds_tile, int wave,
+                                          int lane) {
+  const int p = (i * NW + wave) * 64 + lane;
+  const int row = p >> 3;
+  const int c = (p & 7) ^ chunk_key(row);
+  int gr = r0 + row;
+  gr = gr < nrows ? gr : nrows - 1;
+  glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
+}
 // passes [P0, P1) of stage<ROWS> (spreading one K-tile's DMA over the k-steps)
 template <int ROWS, int P0, int P1>
 __device__ __forceinline__ void stage_part(const unsigned short* __restrict__ X, int64_t ld,
@@ -593,8 +605,9 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
     const bool more = kt + 1 < nk;
 #endif
     BSTAMP(kt, 0);
+    char* nxt = lds + (cur ^ 1) * STAGE;
+#ifndef IRC_BIG_IL
     if (more) {
-      char* nxt = lds + (cur ^ 1) * STAGE;
       // the DMA addresses are re-derived per K-tile (kept live through the loop they
       // would push the 16x16 fragments into spills)
       int ln = lane;
@@ -602,6 +615,7 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
       stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln);
       stage<BN>(B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
     }
+#endif
     BSTAMP(kt, 1);
     const char* la = lds + cur * STAGE;
     const char* lb = la + A_BYTES;
@@ -614,6 +628,19 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
         fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 16 + l16) * 128 + coff);
 #pragma unroll
       for (int j = 0; j < 2 * WNB; ++j) {
+#ifdef IRC_BIG_IL
+        // the next K-tile's DMA, one pass per MFMA group (A: 4 passes, B: 2 WNB), so the
+        // LDS-DMA requests queue behind MFMAs instead of stalling the wave in one burst
+        const int gp = s2 * 2 * WNB + j;
+        if (more && gp < 4 + 2 * WNB) {
+          int ln = lane;
+          asm volatile("" : "+v"(ln));
+          if (gp < 4)
+            stage_one<BM>(gp, A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln);
+          else
+            stage_one<BN>(gp - 4, B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
+        }
+#endif
         const bf16x8 fb =
             *reinterpret_cast<const bf16x8*>(lb + (wn * 32 * WNB + j * 16 + l16) * 128 + coff);
 #pragma unroll

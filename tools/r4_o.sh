@@ -1,0 +1,33 @@
+# Round 4 job o: the big-tile main loop with the next K-tile's DMA interleaved one pass per
+# MFMA group (-DIRC_BIG_IL) against the burst-issue loop: stamps, GEMM shapes, the fused
+# QKV + attention layer, and the C2 step (interleaved A/B).
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+OUT=$GRAFT_REPO_ROOT/gpurun_out/r4o
+mkdir -p $OUT
+V=$GRAFT_REPO_ROOT/information-retrieval-with-contrastive-learning_amd/irc_amd/lib/variants
+for s in ffn2 qkv; do
+  IRC_LIB_PATH=$V/il_stamps.so timeout -k 10 120 python tools/big_stamps.py --shape $s > $OUT/stamps_il_$s.txt 2>&1 || { tail -5 $OUT/stamps_il_$s.txt; exit 1; }
+  grep -v amdgpu $OUT/stamps_il_$s.txt
+done
+IRC_LIB_PATH=$V/il.so timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py tests/test_qkv_attn_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/tests_il.log 2>&1 || { tail -30 $OUT/tests_il.log; exit 1; }
+tail -1 $OUT/tests_il.log
+SH=qkv,attn_out+res,ffn2+res
+for r in 1 2; do
+  timeout -k 10 200 python tools/gemm_bench.py --only $SH > $OUT/g_base_$r.txt 2>&1 || exit 1
+  IRC_LIB_PATH=$V/il.so timeout -k 10 200 python tools/gemm_bench.py --only $SH > $OUT/g_il_$r.txt 2>&1 || exit 1
+  timeout -k 10 100 python tools/qkv_attn_bench.py --iters 30 > $OUT/qa_base_$r.txt 2>&1 || exit 1
+  IRC_LIB_PATH=$V/il.so timeout -k 10 100 python tools/qkv_attn_bench.py --iters 30 > $OUT/qa_il_$r.txt 2>&1 || exit 1
+done
+for f in g_base_1 g_il_1 g_base_2 g_il_2 qa_base_1 qa_il_1 qa_base_2 qa_il_2; do echo "== $f"; grep -v amdgpu $OUT/$f.txt; done
+for r in 1 2; do
+  for m in base il; do
+    if [ $m = il ]; then export IRC_LIB_PATH=$V/il.so; else unset IRC_LIB_PATH; fi
+    timeout -k 10 200 python bench.py --part train --steps 30 --warmup 5 --no-cpu-baseline > $OUT/train_${m}_$r.log 2>&1 || exit 1
+    python3 - $OUT/train_${m}_$r.log $m <<'PY'
+import json, sys
+d = json.loads([x for x in open(sys.argv[1]) if x.startswith('{')][-1])
+print("train %s" % sys.argv[2], round(d["value"]), round(d["ms_per_step"], 3), round(d["roofline"]["frac"], 4))
+PY
+  done
+done
