@@ -633,9 +633,13 @@ def mx_pad(rows: int) -> int:
 
 
 def mx_empty(rows, K, device):
+    """Codes + scales of an MX operand.  Scale slots of the padding rows (rows..mpad) are
+    zeroed (finite); with no padding every slot is written by the producer, so the zero
+    fill (a separate launch per activation) is skipped."""
     mp = mx_pad(rows)
-    return MX(torch.empty((rows, K), dtype=torch.uint8, device=device),
-              torch.zeros((K // 128) * mp * 4, dtype=torch.uint8, device=device), mp)
+    n = (K // 128) * mp * 4
+    scales = (torch.empty if mp == rows else torch.zeros)(n, dtype=torch.uint8, device=device)
+    return MX(torch.empty((rows, K), dtype=torch.uint8, device=device), scales, mp)
 
 
 def quantize_mx(x):
