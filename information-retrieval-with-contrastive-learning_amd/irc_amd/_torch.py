@@ -3,6 +3,8 @@ HIP stream, and the workspace allocator.  PyTorch is plumbing only here: memory,
 streams, autograd bookkeeping and torch.distributed -- never the compute."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ._lib import IRCError
@@ -31,7 +33,9 @@ _side: dict = {}
 
 # Streams created with the high priority (none by default: on MI355X, giving the
 # heads' streams priority over the BERT-feature prefetch measured 3% slower).
-HIGH_PRIORITY_TAGS: tuple = ()
+# IRC_HIGH_PRIORITY_STREAMS: comma-separated tags (A/B runs, e.g. "bert_prefetch").
+HIGH_PRIORITY_TAGS: tuple = tuple(
+    t for t in os.environ.get("IRC_HIGH_PRIORITY_STREAMS", "").split(",") if t)
 
 
 _serial = [0]
