@@ -582,6 +582,74 @@ __device__ uint64_t big_stamps[64][5][2];
 // (lane & 15)].  The chunk key (r >> 1) & 7 stays conflict free for the 16x16x32 fragment
 // reads (lane l: row l & 15, chunk 4 s + (l >> 4): each 16-lane group covers 16 distinct
 // 16-byte bank slots).  Ends with every wave past its last LDS read (LDS free).
+#ifdef IRC_BIG_PP
+// Ping-pong form (A/B build): the two row groups (wm = 0 / 1, 4 waves each) run one
+// section apart -- while one group issues its LDS fragment reads (and its share of the
+// next K-tile's DMA), the other runs MFMAs from registers.  Unit u = half K-tile (kt, s2):
+// L(u) = [s2 == 0: this group's passes of K-tile kt + 1's DMA] + the unit's 14 fragment
+// reads; M(u) = its 8 x 2 WNB MFMAs.  Same MFMAs in the same k order per accumulator as
+// the 2-slot loop: bit-identical results.  Buffer rule: the DMA of kt + 1 (into kt - 1's
+// buffer) is issued in L(kt, 0), after the barrier that ends group 1's L(kt - 1, 1), its
+// last reads of kt - 1.  Landing rule: group 0 reads kt + 1 first, in L(kt + 1, 0); group
+// 1 waits vmcnt(0) before the barrier that ends its L(kt, 1) (which is the barrier before
+// that section), group 0 before the one that ends its M(kt, 1).  Group 1 starts one barrier
+// late and skips its last one, so both groups pass the same barrier count.
+template <int WNB>
+__device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t lda,
+                                              const unsigned short* B, int64_t ldb, int m0,
+                                              int n0, int M, int N, int K, char* lds, int wave,
+                                              int lane, f32x4 (&acc4)[8][2 * WNB]) {
+  constexpr int BN = 128 * WNB;
+  constexpr int A_BYTES = BM * ROW_BYTES, STAGE = A_BYTES + BN * ROW_BYTES;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nk = K / BK;
+  stage<BM>(A, lda, m0, M, 0, lds, wave, lane);
+  stage<BN>(B, ldb, n0, N, 0, lds + A_BYTES, wave, lane);
+  wait_vmcnt<0>();
+  __syncthreads();
+  if (wm == 1) wg_barrier();  // group 1 runs one section behind
+  const int l16 = lane & 15, q4 = lane >> 4;
+  const int key = chunk_key(l16);
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* la = lds + (kt & 1) * STAGE;
+    const char* lb = la + A_BYTES;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      // ---- L section
+      if (s2 == 0 && kt + 1 < nk) {
+        char* nxt = lds + ((kt + 1) & 1) * STAGE;
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln);
+        stage<BN>(B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
+      }
+      const int coff = (((4 * s2 + q4) ^ key) * 16);
+      bf16x8 fa[8], fb[2 * WNB];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 16 + l16) * 128 + coff);
+#pragma unroll
+      for (int j = 0; j < 2 * WNB; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(lb + (wn * 32 * WNB + j * 16 + l16) * 128 + coff);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (wm == 1 && s2 == 1) wait_vmcnt<0>();  // group 0 reads kt + 1 after this barrier
+      wg_barrier();
+      // ---- M section
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 2 * WNB; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc4[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (wm == 0 && s2 == 1) wait_vmcnt<0>();  // its own kt + 1 DMA, read next section
+      if (!(wm == 1 && kt == nk - 1 && s2 == 1)) wg_barrier();
+    }
+  }
+  // group 0 returns under group 1's last MFMAs: every fragment read of both groups is
+  // done (group 1's last L section ended at group 0's last barrier), LDS is free
+}
+#else
 template <int WNB>
 __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t lda,
                                               const unsigned short* B, int64_t ldb, int m0,
@@ -655,6 +723,7 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
     BSTAMP(kt, 4);
   }
 }
+#endif  // IRC_BIG_PP
 }  // namespace big
 
 // IRC_BIG_RING=1 selects the 4-slot ring of gemm_big_kernel (A/B; read on first use;

@@ -31,11 +31,13 @@ def stream_ptr(device: torch.device | None = None):
 _side: dict = {}
 
 
-# Streams created with the high priority (none by default: on MI355X, giving the
-# heads' streams priority over the BERT-feature prefetch measured 3% slower).
-# IRC_HIGH_PRIORITY_STREAMS: comma-separated tags (A/B runs, e.g. "bert_prefetch").
+# Streams created with the high priority: the frozen encoder's feature prefetch (the C2
+# step's critical path; on MI355X +0.6-1.1% against no priorities, three interleaved pairs,
+# profiles/r04_q_priority_ab.txt; the heads' streams at high priority instead measured 3%
+# slower).  IRC_HIGH_PRIORITY_STREAMS overrides: comma-separated tags, "none" for none.
 HIGH_PRIORITY_TAGS: tuple = tuple(
-    t for t in os.environ.get("IRC_HIGH_PRIORITY_STREAMS", "").split(",") if t)
+    t for t in os.environ.get("IRC_HIGH_PRIORITY_STREAMS", "bert_prefetch").split(",")
+    if t and t != "none")
 
 
 _serial = [0]
