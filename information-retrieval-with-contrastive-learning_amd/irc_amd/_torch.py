@@ -31,13 +31,14 @@ def stream_ptr(device: torch.device | None = None):
 _side: dict = {}
 
 
-# Streams created with the high priority: the frozen encoder's feature prefetch (the C2
-# step's critical path; on MI355X +0.6-1.1% against no priorities, three interleaved pairs,
-# profiles/r04_q_priority_ab.txt; the heads' streams at high priority instead measured 3%
-# slower).  IRC_HIGH_PRIORITY_STREAMS overrides: comma-separated tags, "none" for none.
+# Streams created with the high priority: none by default.  The frozen encoder's feature
+# prefetch at high priority gains the C2 step 0.6-1.1% (profiles/r04_q_priority_ab.txt), but
+# once such a stream exists in the process the pipelined retrieval (search_many: HIP-graph
+# replays on DEPTH streams) runs 2.5x slower -- C2 3.04M -> 1.25M queries/s, serial calls
+# unchanged (profiles/r04_t_priority_retrieval.txt); the heads' streams at high priority
+# measured 3% slower.  IRC_HIGH_PRIORITY_STREAMS: comma-separated tags (A/B runs).
 HIGH_PRIORITY_TAGS: tuple = tuple(
-    t for t in os.environ.get("IRC_HIGH_PRIORITY_STREAMS", "bert_prefetch").split(",")
-    if t and t != "none")
+    t for t in os.environ.get("IRC_HIGH_PRIORITY_STREAMS", "").split(",") if t and t != "none")
 
 
 _serial = [0]
