@@ -203,6 +203,9 @@ def qkv_attention(x, wqkv_perm, bias_perm, mask, B, L, H, heads, out=None):
         raise ValueError("qkv_attention: needs L = 64, head dim 64, H % 128 == 0")
     if x.shape != (B * L, H) or x.stride(-1) != 1 or tuple(wqkv_perm.shape) != (3 * H, H):
         raise ValueError("qkv_attention: x [B*L, H], Wqkv [3H, H]")
+    if mask is not None and (mask.dtype != torch.int64 or not mask.is_contiguous()
+                             or mask.numel() != B * L):
+        raise ValueError("qkv_attention: mask must be a contiguous int64 [B, L] tensor")
     ctx = torch.empty((B * L, H), dtype=BF16, device=x.device) if out is None else out
     _lib.call("irc_qkv_attention", B * L, H, heads, L, ptr(x), x.stride(0), ptr(wqkv_perm),
               ptr(bias_perm), ptr(mask), ptr(ctx), ctx.stride(0), stream_ptr(x.device))
