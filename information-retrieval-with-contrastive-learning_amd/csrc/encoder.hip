@@ -183,6 +183,90 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const unsigned short
   }
 }
 
+// The bf16 LayerNorm of layernorm_vec_kernel (same per-row arithmetic, bit-identical)
+// with R consecutive rows per half-wave: gamma / beta stay in registers across the rows
+// and the next row's loads are issued before this row's statistics.
+template <int CPL, int R>
+__global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned short* __restrict__ x,
+                                                            unsigned short* __restrict__ y,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta,
+                                                            int64_t rows, float eps) {
+  constexpr int H = CPL * 256;
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int64_t row0 = (((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * R;
+  float gg[CPL][8], bb[CPL][8];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c0 = (i * 32 + hl) * 8;
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c0);
+    const f32x4 g1 = *reinterpret_cast<const f32x4*>(gamma + c0 + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + c0);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(beta + c0 + 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      gg[i][t] = g0[t];
+      gg[i][4 + t] = g1[t];
+      bb[i][t] = b0[t];
+      bb[i][4 + t] = b1[t];
+    }
+  }
+  u16x8 cur[CPL];
+  {
+    const unsigned short* xr = x + (row0 < rows ? row0 : 0) * H;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) cur[i] = *reinterpret_cast<const u16x8*>(xr + (i * 32 + hl) * 8);
+  }
+#pragma unroll 1
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = row0 + r;
+    u16x8 nxt[CPL];
+    if (r + 1 < R) {
+      const int64_t rn = row + 1 < rows ? row + 1 : 0;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i)
+        nxt[i] = *reinterpret_cast<const u16x8*>(x + rn * H + (i * 32 + hl) * 8);
+    }
+    float v[CPL][8];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        v[i][t] = bf16_to_f32(cur[i][t]);
+        s += v[i][t];
+      }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / H;
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const float d = v[i][t] - mean;
+        s2 += d * d;
+      }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+    const float rstd = rsqrtf(s2 / H + eps);
+    if (row < rows) {
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        u16x8 o;
+#pragma unroll
+        for (int t = 0; t < 8; ++t)  // explicit fma: the rounding of layernorm_vec_kernel
+          o[t] = f32_to_bf16(__builtin_fmaf((v[i][t] - mean) * rstd, gg[i][t], bb[i][t]));
+        *reinterpret_cast<u16x8*>(y + row * H + (i * 32 + hl) * 8) = o;
+      }
+    }
+    if (r + 1 < R) {
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) cur[i] = nxt[i];
+    }
+  }
+}
+
 // Attention: one workgroup per (sequence b, head a).  qkv is the fused
 // projection output [B*L, 3H] (cols [0,H)=Q, [H,2H)=K, [2H,3H)=V, head a at
 // a*dh); ctx [B*L, H].  K and V of the (b, a) pair are staged in LDS as fp32;
@@ -448,7 +532,15 @@ extern "C" int irc_layernorm(int dtype, const void* x, void* y, const float* gam
     const dim3 g8((unsigned)((rows + 7) / 8));
     hipStream_t st = as_stream(stream);
     prof_begin(st);
-    if (H == 768)
+    static const int nr = [] {  // IRC_LN_ROWS: rows per half-wave (1 or 4; A/B, read once)
+      const char* e = getenv("IRC_LN_ROWS");
+      return e ? atoi(e) : 1;
+    }();
+    if (nr == 4 && H == 768)
+      hipLaunchKernelGGL((enc::layernorm_rows_kernel<3, 4>), dim3((unsigned)((rows + 31) / 32)),
+                         dim3(256), 0, st, (const unsigned short*)x, (unsigned short*)y, gamma,
+                         beta, rows, eps);
+    else if (H == 768)
       hipLaunchKernelGGL((enc::layernorm_vec_kernel<3>), g8, dim3(256), 0, st,
                          (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
     else if (H == 1024)

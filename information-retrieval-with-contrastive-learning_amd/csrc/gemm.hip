@@ -1255,15 +1255,21 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     if (wm == hf) {  // this half's accumulators -> T [128][TP]
+      // a lane holds rows (r, r + 1) of its column; swapping with the neighbour lane
+      // (DPP quad_perm [1,0,3,2]) gives the even lane columns (c, c + 1) of row r and the
+      // odd lane those of row r + 1: one 4-byte store per pair instead of two 2-byte ones
+      const int odd = lane & 1;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 2 * WNB; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int rl = 16 * i + 4 * (lane >> 4) + e;
-            T[rl * TP + wn * 32 * WNB + 16 * j + (lane & 15)] =
-                (unsigned short)(pk[i][j][e >> 1] >> (16 * (e & 1)));
+          for (int e2 = 0; e2 < 2; ++e2) {
+            const uint32_t w = pk[i][j][e2];
+            const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false);
+            const uint32_t v = odd ? ((x >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (x << 16));
+            const int rl = 16 * i + 4 * (lane >> 4) + 2 * e2 + odd;
+            *reinterpret_cast<uint32_t*>(&T[rl * TP + wn * 32 * WNB + 16 * j + (lane & 14)]) = v;
           }
     }
     __syncthreads();  // the half is staged
@@ -1333,14 +1339,16 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
             const int j0 = 32 * jb + 16 * k2 + 4 * h;  // keys: t < 4: j0 + t; else j0 + 8 + t - 4
 #pragma unroll
             for (int db = 0; db < 2; ++db) {
-              const unsigned short* vc = V + 32 * db + r32;
-              u16x8 vv;
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                vv[t] = vc[(j0 + t) * TP];
-                vv[4 + t] = vc[(j0 + 8 + t) * TP];
-              }
-              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(bf16x8, vv),
+              // V^T fragment by two transposed LDS reads: 16-lane group g (d half g & 1)
+              // addresses keys j0 + (l >> 2) and 4 columns 4 (l & 3) of its 16; lane l of
+              // the group receives column l of those 4 keys (then keys + 8)
+              const int i16 = lane & 15;
+              const unsigned short* vp =
+                  V + (j0 + (i16 >> 2)) * TP + 32 * db + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+              const v4s lo = ds_tr16(reinterpret_cast<const char*>(vp));
+              const v4s hi = ds_tr16(reinterpret_cast<const char*>(vp + 8 * TP));
+              const v4s both[2] = {lo, hi};
+              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(bf16x8, both),
                                                               o[db], 0, 0, 0);
             }
           }

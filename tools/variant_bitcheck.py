@@ -3,6 +3,7 @@ per build (IRC_LIB_PATH selects the variant) with --save / --check.
 
     python tools/variant_bitcheck.py --save gpurun_out/base.pt
     IRC_LIB_PATH=.../variants/x.so python tools/variant_bitcheck.py --check gpurun_out/base.pt
+    (or an A/B environment switch such as IRC_LN_ROWS=4 instead of IRC_LIB_PATH)
 """
 import argparse
 import os
@@ -29,6 +30,12 @@ def run():
         bias = torch.randn(N, device=dev, generator=g)
         r = torch.randn(M, N, device=dev, generator=g).bfloat16() if epi == 3 else None
         out[name] = ops.gemm(a, b, bias=bias, epilogue=epi, residual=r).cpu()
+    for name, rows in (("ln", 32768), ("ln_ragged", 1003)):
+        g = torch.Generator(device=dev).manual_seed(rows)
+        x = (torch.randn(rows, 768, device=dev, generator=g) * 3 + 1).bfloat16()
+        gm = torch.rand(768, device=dev, generator=g) + 0.5
+        bt = torch.randn(768, device=dev, generator=g)
+        out[name] = ops.layernorm(x, gm, bt, 1e-12).cpu()
     B, L, H = 512, 64, 768
     g = torch.Generator(device=dev).manual_seed(9)
     x = torch.randn(B * L, H, device=dev, generator=g).bfloat16()
