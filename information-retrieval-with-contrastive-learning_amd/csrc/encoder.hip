@@ -105,6 +105,70 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(
   }
 }
 
+// bf16 embedding gather + LayerNorm for H % 256 == 0: embed_ln_kernel's arithmetic with
+// layernorm_vec_kernel's layout (one half-wave per row, 16-byte gathers of the word row,
+// position row and token-type row, CPL chunks of 8 per lane).  The 32-lane statistics
+// sum in another order than the 64-lane one, so the output can differ from
+// embed_ln_kernel's in the last bf16 bit.
+template <int CPL>
+__global__ __launch_bounds__(256) void embed_ln_vec_kernel(
+    const int64_t* __restrict__ ids, const unsigned short* __restrict__ word,
+    const unsigned short* __restrict__ pos, const unsigned short* __restrict__ type0,
+    const float* __restrict__ gamma, const float* __restrict__ beta,
+    unsigned short* __restrict__ y, int64_t rows, int L, float eps) {
+  constexpr int H = CPL * 256;
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool ok = row < rows;
+  const int64_t rr = ok ? row : 0;
+  const int64_t id = ids[rr];
+  const int l = (int)(rr % L);
+  float v[CPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c0 = (i * 32 + hl) * 8;
+    const u16x8 w = *reinterpret_cast<const u16x8*>(word + id * H + c0);
+    const u16x8 t = *reinterpret_cast<const u16x8*>(type0 + c0);
+    const u16x8 p = *reinterpret_cast<const u16x8*>(pos + (int64_t)l * H + c0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      // HF order: (word + token_type) + position
+      v[i][e] = (bf16_to_f32(w[e]) + bf16_to_f32(t[e])) + bf16_to_f32(p[e]);
+      s += v[i][e];
+    }
+  }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / H;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[i][e] - mean;
+      s2 = __builtin_fmaf(d, d, s2);
+    }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+  const float rstd = rsqrtf(s2 / H + eps);
+  if (!ok) return;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c0 = (i * 32 + hl) * 8;
+    const f32x4 g0 = *reinterpret_cast<const f32x4*>(gamma + c0);
+    const f32x4 g1 = *reinterpret_cast<const f32x4*>(gamma + c0 + 4);
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(beta + c0);
+    const f32x4 b1 = *reinterpret_cast<const f32x4*>(beta + c0 + 4);
+    const float gg[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+    const float bb[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f32_to_bf16((v[i][e] - mean) * rstd * gg[e] + bb[e]);
+    *reinterpret_cast<u16x8*>(y + row * H + c0) = o;
+  }
+}
+
 // bf16 LayerNorm for H % 256 == 0 (BERT-base 768, -large 1024): one half-wave
 // (32 lanes) per row, 16-byte loads/stores (H/256 chunks of 8 per lane), the
 // two half-waves of a wave on consecutive rows; statistics fp32 in the same
@@ -147,7 +211,7 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const unsigned short
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const float d = v[i][t] - mean;
-      s2 += d * d;
+      s2 = __builtin_fmaf(d, d, s2);  // explicit: the same rounding in every LN kernel
     }
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
@@ -245,7 +309,7 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned shor
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
         const float d = v[i][t] - mean;
-        s2 += d * d;
+        s2 = __builtin_fmaf(d, d, s2);  // explicit: the same rounding in every LN kernel
       }
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
@@ -633,6 +697,23 @@ extern "C" int irc_embed_ln(int dtype, const int64_t* ids, const void* word, con
   IRC_REQUIRE(H >= 1 && H <= 64 * enc::MAXH_PER_LANE, "embed_ln: H=%lld unsupported",
               (long long)H);
   if (rows == 0) return IRC_OK;
+  const bool al = ((((uintptr_t)word | (uintptr_t)pos | (uintptr_t)type0 | (uintptr_t)y |
+                     (uintptr_t)gamma | (uintptr_t)beta) % 16) == 0);
+  if (dtype == 0 && al && (H == 768 || H == 1024)) {
+    const dim3 g8((unsigned)((rows + 7) / 8));
+    hipStream_t st = as_stream(stream);
+    if (H == 768)
+      hipLaunchKernelGGL((enc::embed_ln_vec_kernel<3>), g8, dim3(256), 0, st, ids,
+                         (const unsigned short*)word, (const unsigned short*)pos,
+                         (const unsigned short*)type0, gamma, beta, (unsigned short*)y, rows,
+                         (int)L, eps);
+    else
+      hipLaunchKernelGGL((enc::embed_ln_vec_kernel<4>), g8, dim3(256), 0, st, ids,
+                         (const unsigned short*)word, (const unsigned short*)pos,
+                         (const unsigned short*)type0, gamma, beta, (unsigned short*)y, rows,
+                         (int)L, eps);
+    return check_launch("embed_ln_vec_kernel");
+  }
   dim3 grid((unsigned)((rows + 3) / 4));
   if (dtype == 0)
     hipLaunchKernelGGL((enc::embed_ln_kernel<unsigned short>), grid, dim3(256), 0,

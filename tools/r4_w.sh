@@ -1,5 +1,6 @@
 # Round 4 job w: LayerNorm with 4 rows per half-wave (IRC_LN_ROWS=4): bit-for-bit against
-# the one-row kernel, the kernel time, and the C2 step (interleaved).
+# the one-row kernel, the kernel time, and the C2 step (interleaved); the vectorised
+# embedding gather + LN and the encoder / model / config tests.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/r4w
@@ -13,6 +14,8 @@ for r in 1 2 3; do
   IRC_LN_ROWS=4 timeout -k 10 60 python tools/ln_bench.py >> $OUT/ln.txt 2>&1 || exit 1
 done
 grep -v amdgpu $OUT/ln.txt
+timeout -k 10 300 python -u -m pytest tests/test_encoder_gpu.py tests/test_model_gpu.py tests/test_configs_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
 for r in 1 2; do
   for m in 1 4; do
     IRC_LN_ROWS=$m timeout -k 10 200 python bench.py --part train --steps 30 --warmup 5 --no-cpu-baseline > $OUT/train_${m}_$r.log 2>&1 || exit 1
