@@ -596,14 +596,23 @@ extern "C" int irc_layernorm(int dtype, const void* x, void* y, const float* gam
     const dim3 g8((unsigned)((rows + 7) / 8));
     hipStream_t st = as_stream(stream);
     prof_begin(st);
-    static const int nr = [] {  // IRC_LN_ROWS: rows per half-wave (1 or 4; A/B, read once)
+    // IRC_LN_ROWS=1 selects the one-row-per-half-wave kernel (A/B, read once; bit-identical):
+    // 4 rows per half-wave measured 15.9 vs 17.7 us over [32768, 768] (6.35 vs 5.70 TB/s,
+    // profiles/r04_w_ln_rows.txt)
+    static const int nr = [] {
       const char* e = getenv("IRC_LN_ROWS");
-      return e ? atoi(e) : 1;
+      return (e && e[0] == '1') ? 1 : 4;
     }();
+    const dim3 g32((unsigned)((rows + 31) / 32));
     if (nr == 4 && H == 768)
-      hipLaunchKernelGGL((enc::layernorm_rows_kernel<3, 4>), dim3((unsigned)((rows + 31) / 32)),
-                         dim3(256), 0, st, (const unsigned short*)x, (unsigned short*)y, gamma,
-                         beta, rows, eps);
+      hipLaunchKernelGGL((enc::layernorm_rows_kernel<3, 4>), g32, dim3(256), 0, st,
+                         (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
+    else if (nr == 4 && H == 1024)
+      hipLaunchKernelGGL((enc::layernorm_rows_kernel<4, 4>), g32, dim3(256), 0, st,
+                         (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
+    else if (nr == 4)
+      hipLaunchKernelGGL((enc::layernorm_rows_kernel<2, 4>), g32, dim3(256), 0, st,
+                         (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
     else if (H == 768)
       hipLaunchKernelGGL((enc::layernorm_vec_kernel<3>), g8, dim3(256), 0, st,
                          (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
