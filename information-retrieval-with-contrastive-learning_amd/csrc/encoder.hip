@@ -250,12 +250,16 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const unsigned short
 // The bf16 LayerNorm of layernorm_vec_kernel (same per-row arithmetic, bit-identical)
 // with R consecutive rows per half-wave: gamma / beta stay in registers across the rows
 // and the next row's loads are issued before this row's statistics.
+// y8 != null: also the MX-fp8 copy, as layernorm_vec_kernel writes it (config C5).
 template <int CPL, int R>
 __global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned short* __restrict__ x,
                                                             unsigned short* __restrict__ y,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta,
-                                                            int64_t rows, float eps) {
+                                                            int64_t rows, float eps,
+                                                            unsigned char* __restrict__ y8 = nullptr,
+                                                            unsigned char* __restrict__ ys = nullptr,
+                                                            int64_t mpad = 0) {
   constexpr int H = CPL * 256;
   const int lane = threadIdx.x & 63, hl = lane & 31;
   const int64_t row0 = (((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5)) * R;
@@ -321,7 +325,17 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned shor
 #pragma unroll
         for (int t = 0; t < 8; ++t)  // explicit fma: the rounding of layernorm_vec_kernel
           o[t] = f32_to_bf16(__builtin_fmaf((v[i][t] - mean) * rstd, gg[i][t], bb[i][t]));
-        *reinterpret_cast<u16x8*>(y + row * H + (i * 32 + hl) * 8) = o;
+        const int c0 = (i * 32 + hl) * 8;
+        *reinterpret_cast<u16x8*>(y + row * H + c0) = o;
+        if (y8 != nullptr) {  // uniform; the bf16-rounded values quantised, as layernorm_vec_kernel
+          float rq[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) rq[t] = bf16_to_f32(o[t]);
+          uint2 q8;
+          const unsigned e8 = gpp::mx_quant8(rq, q8);
+          *reinterpret_cast<uint2*>(y8 + row * H + c0) = q8;
+          if ((hl & 3) == 0) ys[gpp::mx_scale_index(row, c0, mpad)] = (unsigned char)e8;
+        }
       }
     }
     if (r + 1 < R) {
@@ -652,7 +666,24 @@ extern "C" int irc_layernorm_mx(const void* x, void* y, const float* gamma, cons
   prof_begin(st);
   auto* yy8 = static_cast<unsigned char*>(y8);
   auto* yys = static_cast<unsigned char*>(ys);
-  if (H == 768)
+  static const bool rows4 = [] {  // IRC_LN_ROWS=1: the one-row kernel (as irc_layernorm)
+    const char* e = getenv("IRC_LN_ROWS");
+    return !(e && e[0] == '1');
+  }();
+  const dim3 g32((unsigned)((rows + 31) / 32));
+  if (rows4 && H == 768)
+    hipLaunchKernelGGL((enc::layernorm_rows_kernel<3, 4>), g32, dim3(256), 0, st,
+                       (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
+                       yys, mpad);
+  else if (rows4 && H == 1024)
+    hipLaunchKernelGGL((enc::layernorm_rows_kernel<4, 4>), g32, dim3(256), 0, st,
+                       (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
+                       yys, mpad);
+  else if (rows4)
+    hipLaunchKernelGGL((enc::layernorm_rows_kernel<2, 4>), g32, dim3(256), 0, st,
+                       (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
+                       yys, mpad);
+  else if (H == 768)
     hipLaunchKernelGGL((enc::layernorm_vec_kernel<3>), g8, dim3(256), 0, st,
                        (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
                        yys, mpad);
