@@ -666,9 +666,11 @@ extern "C" int irc_layernorm_mx(const void* x, void* y, const float* gamma, cons
   prof_begin(st);
   auto* yy8 = static_cast<unsigned char*>(y8);
   auto* yys = static_cast<unsigned char*>(ys);
-  static const bool rows4 = [] {  // IRC_LN_ROWS=1: the one-row kernel (as irc_layernorm)
-    const char* e = getenv("IRC_LN_ROWS");
-    return !(e && e[0] == '1');
+  // the 4-rows kernel only on request (IRC_LN_MX_ROWS=4): with the MX outputs it measured
+  // no faster (C5 step 29.2k / 29.2k vs 29.3k / 29.3k pairs/s, profiles/r04_y_ln_mx_rows.txt)
+  static const bool rows4 = [] {
+    const char* e = getenv("IRC_LN_MX_ROWS");
+    return e && e[0] == '4';
   }();
   const dim3 g32((unsigned)((rows + 31) / 32));
   if (rows4 && H == 768)
