@@ -505,6 +505,58 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
           sav[i][e] = (g.sa != nullptr && row < g.M) ? g.sa[row] : 1.f;
         }
     }
+#ifdef IRC_PP_B16_STAGE
+    // bf16 outputs without a residual: stage the rounded values as bf16 (half the LDS bytes;
+    // the neighbour-lane swap pairs two columns of a row into one 4-byte store), then read
+    // whole 16-byte row pieces: the same RNE rounding, bit-identical C
+    constexpr bool B16 = sizeof(TO) == 2 && F8 == 0 && !LN &&
+                         (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_GELU);
+    if constexpr (B16) {
+      constexpr int BP = 72;  // u16 row pitch: rows 4 apart 16 banks apart
+      unsigned short* stb = reinterpret_cast<unsigned short*>(lds) + wave * (32 * BP);
+      unsigned short* C = reinterpret_cast<unsigned short*>(g.C) + batch * g.sC;
+      const int odd = lane & 1;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            f32x2 v[2];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * alpha + bv[j];
+            if (EPI == EPI_BIAS_GELU) {
+              v[0] = gelu_lite2(v[0]);
+              v[1] = gelu_lite2(v[1]);
+            }
+#pragma unroll
+            for (int e2 = 0; e2 < 2; ++e2) {
+              typedef __bf16 bf16x2_s __attribute__((ext_vector_type(2)));
+              const uint32_t w = __builtin_bit_cast(uint32_t, __builtin_convertvector(v[e2], bf16x2_s));
+              const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false);
+              const uint32_t o2 = odd ? ((x >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (x << 16));
+              const int rl = 16 * ii + 4 * (lane >> 4) + 2 * e2 + odd;
+              *reinterpret_cast<uint32_t*>(&stb[rl * BP + 16 * j + (lane & 14)]) = o2;
+            }
+          }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int rbase = rbase0 + 32 * p;
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int c = it * 64 + lane;
+          const int rl = c >> 3, c8 = (c & 7) * 8;
+          const int row = rbase + rl, col = cbase + c8;
+          if (row >= g.M || col >= g.N) continue;
+          *reinterpret_cast<u16x8*>(C + (int64_t)row * g.ldc + col) =
+              *reinterpret_cast<const u16x8*>(&stb[rl * BP + c8]);
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      return;
+    }
+#endif
 #pragma unroll
     for (int p = 0; p < 4; ++p) {  // 32-row passes
 #pragma unroll

@@ -15,7 +15,9 @@ sys.path.insert(0, os.path.join(ROOT, "information-retrieval-with-contrastive-le
 import torch  # noqa: E402
 
 CASES = [("qkv", 32768, 2304, 768, 1), ("out", 32768, 768, 768, 3), ("ffn2", 32768, 768, 3072, 3),
-         ("ragged", 32700, 768, 768, 3), ("k64", 4096, 768, 64, 1), ("c4_out", 32768, 1024, 1024, 3)]
+         ("ragged", 32700, 768, 768, 3), ("k64", 4096, 768, 64, 1), ("c4_out", 32768, 1024, 1024, 3),
+         ("ffn1", 32768, 3072, 768, 2), ("ffn1_bias", 32768, 3072, 768, 1),
+         ("pp_ragged", 4000, 3072, 768, 2)]
 
 
 def run():
@@ -29,6 +31,8 @@ def run():
         b = (torch.randn(N, K, device=dev, generator=g) * 0.05).bfloat16()
         bias = torch.randn(N, device=dev, generator=g)
         r = torch.randn(M, N, device=dev, generator=g).bfloat16() if epi == 3 else None
+        if name.startswith("ffn1") or name == "pp_ragged":  # typical pre-activation scale
+            b = b * 0.3
         out[name] = ops.gemm(a, b, bias=bias, epilogue=epi, residual=r).cpu()
     for name, rows in (("ln", 32768), ("ln_ragged", 1003)):
         g = torch.Generator(device=dev).manual_seed(rows)
