@@ -274,7 +274,8 @@ int irc_lstm_hprev(const void* hout, void* hprev, int64_t B, int64_t L, int64_t 
  *   bytes, 3 backward exchange bytes, 4 sync bytes (flags + timeout word).
  * irc_lstm_coop_pack: W_hh fp32 [ndir][4H][H] -> wf, wb bf16 (4H*H per dir each).
  * irc_lstm_fwd_coop: xp_packed as irc_lstm_fwd_mfma; gsave/csave (NULL for the
- *   no-grad encoder) in a layout private to the coop pair.  sync is zeroed by the
+ *   no-grad encoder) in a layout private to the coop pair; hprev (may be NULL)
+ *   as irc_lstm_hprev's output, written by the recurrence itself.  sync is zeroed by the
  *   call; its last word is nonzero after a cluster timed out (never expected: the
  *   launch is sized from the device's CU count so both encoders' clusters are
  *   co-resident).  On a timeout the call itself overwrites its output (hout /
@@ -290,8 +291,8 @@ int64_t irc_lstm_coop_sizes(int64_t B, int64_t L, int64_t H, int64_t ndir, int w
 int irc_lstm_coop_pack(const float* whh, int64_t H, int64_t ndir, void* wf, void* wb,
                        irc_stream_t stream);
 int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* hout, float* gsave,
-                      float* csave, void* xch, void* sync, int64_t B, int64_t L, int64_t H,
-                      int64_t ndir, irc_stream_t stream);
+                      float* csave, void* hprev, void* xch, void* sync, int64_t B, int64_t L,
+                      int64_t H, int64_t ndir, irc_stream_t stream);
 int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* gsave, const float* csave,
                       void* dgates, void* xch, void* sync, int64_t B, int64_t L, int64_t H,
                       int64_t ndir, irc_stream_t stream);

@@ -197,8 +197,8 @@ __device__ __forceinline__ Member decode() {
 __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     const float* __restrict__ xp, const unsigned short* __restrict__ wpk,
     unsigned short* __restrict__ hout, float* __restrict__ gsave, float* __restrict__ csave,
-    unsigned short* xch, unsigned* flags, unsigned* tmo, int B, int L, int ndir, int grp0,
-    int ngrp_launch, int ngrp_total, unsigned spin_max) {
+    unsigned short* __restrict__ hprev, unsigned short* xch, unsigned* flags, unsigned* tmo, int B,
+    int L, int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max) {
   __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
   __shared__ __attribute__((aligned(16))) unsigned short hb[BG][HP];
   __shared__ int abort_lds;
@@ -218,6 +218,15 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     for (int i = threadIdx.x; i < WSLICE / 8; i += NTH) dst[i] = src[i];
     for (int i = threadIdx.x; i < BG * HP; i += NTH) (&hb[0][0])[i] = 0;
     if (threadIdx.x == 0) abort_lds = 0;
+  }
+  if (hprev) {  // h_{-1} = 0: the first step's row of hprev (own slice)
+    const int t0 = dir == 0 ? 0 : L - 1;
+    for (int p = threadIdx.x; p < BG * UPW / 8; p += NTH) {
+      const int row = p / (UPW / 8), col = m * UPW + (p % (UPW / 8)) * 8;
+      if (b0 + row < B)
+        *reinterpret_cast<u16x8*>(hprev + (((int64_t)dir * B + b0 + row) * L + t0) * H + col) =
+            u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
   }
   const int u = m * UPW + w * UPV + r16;  // this lane's hidden unit
   float c[2][4];
@@ -337,9 +346,15 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     }
     for (int p = threadIdx.x; p < BG * UPW / 8; p += NTH) {  // h_t -> hout (own slice)
       const int row = p / (UPW / 8), col = m * UPW + (p % (UPW / 8)) * 8;
-      if (b0 + row < B)
-        *reinterpret_cast<u16x8*>(hout + ((int64_t)(b0 + row) * L + t) * hld + dir * H + col) =
-            *reinterpret_cast<const u16x8*>(&hb[row][col]);
+      if (b0 + row < B) {
+        const u16x8 hv = *reinterpret_cast<const u16x8*>(&hb[row][col]);
+        *reinterpret_cast<u16x8*>(hout + ((int64_t)(b0 + row) * L + t) * hld + dir * H + col) = hv;
+        // ... and into hprev at the next step's row (the dW_hh operand: no separate pass)
+        const int tn = dir == 0 ? t + 1 : t - 1;
+        if (hprev && tn >= 0 && tn < L)
+          *reinterpret_cast<u16x8*>(hprev + (((int64_t)dir * B + b0 + row) * L + tn) * H + col) =
+              hv;
+      }
     }
     __syncthreads();  // h_t complete for the next step (and the abort word)
     if (abort_lds) return;
@@ -540,12 +555,17 @@ __global__ void pack_coop_kernel(const float* __restrict__ whh, unsigned short* 
 // NaN reaches the embeddings / gradients and the loss, whoever the caller is.
 // Every block reads the one word and leaves at once in the normal case.
 __global__ void poison_on_timeout_kernel(const unsigned* __restrict__ tmo,
-                                         unsigned short* __restrict__ out, int64_t n) {
+                                         unsigned short* __restrict__ out, int64_t n,
+                                         unsigned short* __restrict__ out2, int64_t n2) {
   if (__hip_atomic_load((const gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
     return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = 0x7FC0;  // bf16 quiet NaN
+  if (out2)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2;
+         i += (int64_t)gridDim.x * blockDim.x)
+      out2[i] = 0x7FC0;
 }
 
 // Sticky fault word: *fault |= timeout word (device side, no host sync).
@@ -607,15 +627,16 @@ static int coop_groups_per_launch(int64_t ndir) {
   return g < 1 ? 1 : g;
 }
 
-static void coop_poison(const unsigned* tmo, void* out, int64_t n, hipStream_t st) {
+static void coop_poison(const unsigned* tmo, void* out, int64_t n, hipStream_t st,
+                        void* out2 = nullptr, int64_t n2 = 0) {
   hipLaunchKernelGGL(lstmc::poison_on_timeout_kernel, dim3(256), dim3(256), 0, st, tmo,
-                     (unsigned short*)out, n);
+                     (unsigned short*)out, n, (unsigned short*)out2, n2);
 }
 
 // sync: flags (ndir*ngrp*P words) followed by the timeout word; zeroed here.
 extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* hout, float* gsave,
-                                 float* csave, void* xch, void* sync, int64_t B, int64_t L,
-                                 int64_t H, int64_t ndir, irc_stream_t stream) {
+                                 float* csave, void* hprev, void* xch, void* sync, int64_t B,
+                                 int64_t L, int64_t H, int64_t ndir, irc_stream_t stream) {
   IRC_REQUIRE(H == lstmc::H, "lstm_fwd_coop: H=%lld", (long long)H);
   IRC_REQUIRE((gsave == nullptr) == (csave == nullptr), "lstm_fwd_coop: gsave/csave together");
   if (B == 0 || L == 0) return IRC_OK;
@@ -633,11 +654,11 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
     const dim3 grid((unsigned)((n + 7) / 8 * 32), (unsigned)ndir);
     hipLaunchKernelGGL(lstmc::lstm_fwd_coop, grid, dim3(lstmc::NTH), 0, st, xp_packed,
                        (const unsigned short*)wf, (unsigned short*)hout, gsave, csave,
-                       (unsigned short*)xch, flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp,
-                       spin_max);
+                       (unsigned short*)hprev, (unsigned short*)xch, flags, tmo, (int)B, (int)L,
+                       (int)ndir, g0, n, ngrp, spin_max);
   }
   prof_end("lstm_fwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
-  coop_poison(tmo, hout, B * L * ndir * H, st);
+  coop_poison(tmo, hout, B * L * ndir * H, st, hprev, hprev ? B * L * ndir * H : 0);
   return check_launch("lstm_fwd_coop");
 }
 

@@ -79,7 +79,7 @@ SIGNATURES = {
     "irc_lstm_coop_supported": (I32, [I64]),
     "irc_lstm_coop_sizes": (I64, [I64, I64, I64, I64, I32]),
     "irc_lstm_coop_pack": (I32, [P, I64, I64, P, P, P]),
-    "irc_lstm_fwd_coop": (I32, [P, P, P, P, P, P, P, I64, I64, I64, I64, P]),
+    "irc_lstm_fwd_coop": (I32, [P, P, P, P, P, P, P, P, I64, I64, I64, I64, P]),
     "irc_lstm_bwd_coop": (I32, [P, P, P, P, P, P, P, I64, I64, I64, I64, P]),
     "irc_lstm_coop_fault": (I32, [P, I64, I64, P, P]),
     "irc_mean_rows": (I32, [I32, P, P, I64, I64, I64, I64, P]),

@@ -304,13 +304,12 @@ def lstm_fwd_coop(xp_packed, wf, B, L, H, ndir, save=True):
     if save:
         gsave = torch.empty((_coop_bytes(B, L, H, ndir, 0),), dtype=F32, device=dev)
         csave = torch.empty((_coop_bytes(B, L, H, ndir, 1),), dtype=F32, device=dev)
+        # h_{t-1} for dW_hh, written by the recurrence itself alongside hout
+        hprev = torch.empty((ndir, B * L, H), dtype=BF16, device=dev)
     xch = torch.empty((_coop_bytes(B, L, H, ndir, 2),), dtype=torch.uint8, device=dev)
     sync = torch.empty((_coop_bytes(B, L, H, ndir, 4) // 4,), dtype=torch.int32, device=dev)
     _lib.call("irc_lstm_fwd_coop", ptr(xp_packed), ptr(wf), ptr(hout), ptr(gsave), ptr(csave),
-              ptr(xch), ptr(sync), B, L, H, ndir, stream_ptr(dev))
-    if save:
-        hprev = torch.empty((ndir, B * L, H), dtype=BF16, device=dev)
-        _lib.call("irc_lstm_hprev", ptr(hout), ptr(hprev), B, L, H, ndir, stream_ptr(dev))
+              ptr(hprev), ptr(xch), ptr(sync), B, L, H, ndir, stream_ptr(dev))
     return hout, gsave, csave, hprev, sync
 
 

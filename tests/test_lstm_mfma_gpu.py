@@ -139,6 +139,13 @@ def test_coop_matches_single_cu_and_no_timeout(gpu, B, L):
     assert not ops.lstm_coop_timed_out(sync, B, nd)
     assert (h_c.float() - h_m.float()).abs().max().item() <= 2e-2
     assert (hp_c.float() - hp_m.float()).abs().max().item() <= 2e-2
+    # hprev written by the recurrence == the separate shift pass over its own hout
+    from irc_amd import _lib
+    from irc_amd._torch import ptr, stream_ptr
+
+    hp_ref = torch.full_like(hp_c, 7.0)
+    _lib.call("irc_lstm_hprev", ptr(h_c), ptr(hp_ref), B, L, H, nd, stream_ptr(gpu))
+    assert torch.equal(hp_c, hp_ref)
     dy = torch.randn(B * L, nd * H, device=gpu) * 0.1
     dg_c, sync_b = ops.lstm_bwd_coop(dy, wb, g_c, c_c, B, L, H, nd)
     dg_m = ops.lstm_bwd_mfma(dy, wT, g_m, c_m, B, L, H, nd)
@@ -173,11 +180,12 @@ def test_coop_forced_timeout_poisons_outputs(gpu, forced_coop_timeout, bf16_mode
     xp = torch.randn(B * L, nd * 4 * H, device=gpu)
     wf, wb = ops.lstm_coop_pack(whh, H, nd)
     fault = torch.zeros(1, dtype=torch.int32, device=gpu)
-    h, g, c, _, sync = ops.lstm_fwd_coop(xp, wf, B, L, H, nd, save=True)
+    h, g, c, hp, sync = ops.lstm_fwd_coop(xp, wf, B, L, H, nd, save=True)
     ops.lstm_coop_fault(sync, B, nd, fault)
     assert ops.lstm_coop_timed_out(sync, B, nd)
     assert int(fault.item()) != 0
     assert bool(torch.isnan(h.float()).all())
+    assert bool(torch.isnan(hp.float()).all())
     dg, sync_b = ops.lstm_bwd_coop(torch.randn(B * L, nd * H, device=gpu), wb, g, c, B, L, H, nd)
     assert ops.lstm_coop_timed_out(sync_b, B, nd)
     assert bool(torch.isnan(dg.float()).all())

@@ -118,7 +118,7 @@ def main():
     # host-time breakdown of the loop (seconds spent inside each call)
     from src.contrastor import contrastive_module as CM
 
-    spent = {"tokenize": [], "bert_issue": [], "step_issue": []}
+    spent = {"tokenize": [], "bert_issue": [], "step_issue": [], "loader_next": []}
 
     def wrap(obj, name, key):
         f = getattr(obj, name)
@@ -141,6 +141,11 @@ def main():
     CM.RetrievalModelWrapper.bert_extract_async = issue
     wrap(CM.RetrievalModelWrapper, "bert_extract_async", "bert_issue")
     wrap(T.TrainState, "micro_batch", "step_issue")
+    # host time the loop spends waiting in next(it) on the DataLoader
+    from torch.utils.data import dataloader as DL
+
+    for cls in (DL._SingleProcessDataLoaderIter, DL._MultiProcessingDataLoaderIter):
+        wrap(cls, "__next__", "loader_next")
     t_start = time.perf_counter()
     import main as entry
 
