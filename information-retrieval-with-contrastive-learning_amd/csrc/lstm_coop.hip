@@ -198,7 +198,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     const float* __restrict__ xp, const unsigned short* __restrict__ wpk,
     unsigned short* __restrict__ hout, float* __restrict__ gsave, float* __restrict__ csave,
     unsigned short* __restrict__ hprev, unsigned short* xch, unsigned* flags, unsigned* tmo, int B,
-    int L, int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max) {
+    int L, int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max, int sentinels) {
   __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
   __shared__ __attribute__((aligned(16))) unsigned short hb[BG][HP];
   __shared__ int abort_lds;
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         st_sc1_pair(Xp + row * (H / 2) + c2, granule(ep, hv.x), granule(ep, hv.y));
       }
       // ... and gather the other three (12 granules per thread)
-      {  // sentinel: each producer's first granule (own slot: already ours)
+      if (sentinels) {  // sentinel: each producer's first granule (own slot: already ours)
         const unsigned long long* sent[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) sent[q] = Xp + q * (UPW / 2);
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     const float* __restrict__ dy, const unsigned short* __restrict__ wtpk,
     const float* __restrict__ gsave, const float* __restrict__ csave,
     unsigned short* __restrict__ dg, float* xch, unsigned* flags, unsigned* tmo, int B, int L,
-    int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max) {
+    int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max, int tagged) {
   __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
   __shared__ __attribute__((aligned(16))) unsigned short dgl[BG][HP];  // own dgates, k = g*64+lu
   __shared__ int abort_lds;
@@ -457,9 +457,70 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
             acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw, acc[rb][cb], 0, 0, 0);
         }
       }
+      const unsigned ep = (unsigned)s;
+      if (tagged) {
+        // R2 (the data is the flag): each partial float travels as a granule
+        // {value, epoch}, two per 16-byte write-through store; block (wave w = unit
+        // block 64w = destination member w, cb, rb), lane, 4 rows -> 4 granules
+        unsigned long long* G = reinterpret_cast<unsigned long long*>(xch) +
+                                (int64_t)(dir * ngrp_total + grp) * 2 * P * PART;
+        unsigned long long* Gs = G + (int64_t)(s & 1) * P * PART;
+        unsigned long long* Gp = Gs + (int64_t)m * PART;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            unsigned long long* q = Gp + ((((w * 4 + cb) * 2 + rb) * 64 + lane) * 4);
+            st_sc1_pair(q, granule(ep, __float_as_uint(acc[rb][cb][0])),
+                        granule(ep, __float_as_uint(acc[rb][cb][1])));
+            st_sc1_pair(q + 2, granule(ep, __float_as_uint(acc[rb][cb][2])),
+                        granule(ep, __float_as_uint(acc[rb][cb][3])));
+          }
+        // own units (block m, cb = w) from every member; sweep until every tag is ep
+        u32x4 v[P][2][2];
+        for (unsigned spins = 0;;) {
+#pragma unroll
+          for (int mm = 0; mm < P; ++mm)
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+                v[mm][rb][j] =
+                    ld_sc1_x4(Gs + (int64_t)mm * PART + ((((m * 4 + w) * 2 + rb) * 64 + lane) * 4) + 2 * j);
+          asm volatile("s_waitcnt vmcnt(0)"
+                       : "+v"(v[0][0][0]), "+v"(v[0][0][1]), "+v"(v[0][1][0]), "+v"(v[0][1][1]),
+                         "+v"(v[1][0][0]), "+v"(v[1][0][1]), "+v"(v[1][1][0]), "+v"(v[1][1][1]),
+                         "+v"(v[2][0][0]), "+v"(v[2][0][1]), "+v"(v[2][1][0]), "+v"(v[2][1][1]),
+                         "+v"(v[3][0][0]), "+v"(v[3][0][1]), "+v"(v[3][1][0]), "+v"(v[3][1][1])
+                       :
+                       : "memory");
+          bool ok = true;
+#pragma unroll
+          for (int mm = 0; mm < P; ++mm)
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+              for (int j = 0; j < 2; ++j) ok &= v[mm][rb][j][1] == ep && v[mm][rb][j][3] == ep;
+          if (__all(ok) && spin_max) break;
+          if (++spins > spin_max) {
+            if (lane == 0) {
+              __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              abort_lds = 1;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        // sum in member order 0..3, as the flag form does
+#pragma unroll
+        for (int mm = 0; mm < P; ++mm)
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dh[rb][i] += __uint_as_float(v[mm][rb][i >> 1][(i & 1) * 2]);
+      } else {
       // publish the partial (R1): block (wave w = unit block 64w, cb, rb), each
       // lane's 4 rows as one 16-byte write-through store
-      const unsigned ep = (unsigned)s;
       float* Xs = X + (int64_t)(s & 1) * P * PART;
       float* Xp = Xs + (int64_t)m * PART;
 #pragma unroll
@@ -489,6 +550,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
           for (int i = 0; i < 4; ++i) dh[rb][i] += __uint_as_float(v[mm][rb][i]);
+      }
     }
     __syncthreads();  // all reads of dgl (MFMA) done before it is overwritten
     if (abort_lds) return;
@@ -589,7 +651,7 @@ extern "C" int64_t irc_lstm_coop_sizes(int64_t B, int64_t L, int64_t H, int64_t 
     case 0: return ndir * ngrp * L * lstmc::GSTEP;
     case 1: return ndir * ngrp * L * lstmc::CSTEP;
     case 2: return ndir * ngrp * 2 * lstmc::BG * (H / 2) * 8;   // granules
-    case 3: return ndir * ngrp * 2 * lstmc::P * lstmc::PART * 4;  // fp32 partials
+    case 3: return ndir * ngrp * 2 * lstmc::P * lstmc::PART * 8;  // fp32 partials as granules
     case 4: return ((ndir * ngrp * lstmc::P + 1) * 4 + 15) / 16 * 16;
   }
   return -1;
@@ -644,6 +706,9 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
   const int ngrp = (int)((B + lstmc::BG - 1) / lstmc::BG);
   const int gpl = coop_groups_per_launch(ndir);
   const unsigned spin_max = coop_spin_max();
+  // IRC_LSTM_COOP_SENTINELS=0: the granule sweep polls by itself (no sentinel pass)
+  const char* se = getenv("IRC_LSTM_COOP_SENTINELS");
+  const int sentinels = se ? atoi(se) : 1;
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::P;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
@@ -655,7 +720,7 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
     hipLaunchKernelGGL(lstmc::lstm_fwd_coop, grid, dim3(lstmc::NTH), 0, st, xp_packed,
                        (const unsigned short*)wf, (unsigned short*)hout, gsave, csave,
                        (unsigned short*)hprev, (unsigned short*)xch, flags, tmo, (int)B, (int)L,
-                       (int)ndir, g0, n, ngrp, spin_max);
+                       (int)ndir, g0, n, ngrp, spin_max, sentinels);
   }
   prof_end("lstm_fwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
   coop_poison(tmo, hout, B * L * ndir * H, st, hprev, hprev ? B * L * ndir * H : 0);
@@ -673,14 +738,18 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
   const unsigned spin_max = coop_spin_max();
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::P;
+  // IRC_LSTM_COOP_BWD_TAGGED=0: the flag hand-off (R1) instead of tagged granules
+  const char* te = getenv("IRC_LSTM_COOP_BWD_TAGGED");
+  const int tagged = te ? atoi(te) : 1;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
+  if (tagged) hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 3), st);
   prof_begin(st);
   for (int g0 = 0; g0 < ngrp; g0 += gpl) {
     const int n = ngrp - g0 < gpl ? ngrp - g0 : gpl;
     const dim3 grid((unsigned)((n + 7) / 8 * 32), (unsigned)ndir);
     hipLaunchKernelGGL(lstmc::lstm_bwd_coop, grid, dim3(lstmc::NTH), 0, st, dy,
                        (const unsigned short*)wb, gsave, csave, (unsigned short*)dg, (float*)xch,
-                       flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp, spin_max);
+                       flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp, spin_max, tagged);
   }
   prof_end("lstm_bwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
   coop_poison(tmo, dg, B * L * ndir * 4 * H, st);
