@@ -73,11 +73,15 @@ __device__ __forceinline__ unsigned long long granule(unsigned epoch, unsigned v
 // sc1: ~2.7x cheaper per byte than two dwordx2 sc1 stores; each 8-byte half is
 // observed untorn on gfx950).  Inline asm: the compiler does not count it in
 // vmcnt, which only makes its in-order waits for later loads stricter (safe);
-// nothing waits on this store's completion (form R2).
+// nothing waits on this store's completion (form R2).  The trailing s_nop: a
+// store of more than 8 bytes reads its data VGPRs late, so the next VALU op must
+// not overwrite them for 2 wait states -- a hazard the compiler pads for its own
+// stores but cannot see inside inline asm (without it the next v_accvgpr_read /
+// v_mov into the data registers corrupts the stored value).
 __device__ __forceinline__ void st_sc1_pair(void* p, unsigned long long a, unsigned long long b) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // One wave sweeps its N granules (addresses from addr(k)) until every tag ==
@@ -108,11 +112,11 @@ __device__ __forceinline__ void sweep(F addr, unsigned epoch, unsigned (&v)[N], 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // 16-byte write-through store / load (global_*_dwordx4 sc1) for the flag-based
-// hand-off (form R1).  The asm store is drained by the explicit vmcnt(0) before
+// hand-off (form R1); the store pads the data-VGPR hazard as st_sc1_pair does.  The asm store is drained by the explicit vmcnt(0) before
 // the flag; the asm loads are completed by wait_loaded(), which takes the
 // loaded registers as in/out operands so no use can be scheduled before it.
 __device__ __forceinline__ void st_sc1_x4(void* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 __device__ __forceinline__ u32x4 ld_sc1_x4(const void* p) {
   u32x4 v;
@@ -738,9 +742,9 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
   const unsigned spin_max = coop_spin_max();
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::P;
-  // IRC_LSTM_COOP_BWD_TAGGED=0: the flag hand-off (R1) instead of tagged granules
+  // IRC_LSTM_COOP_BWD_TAGGED=1: tagged granules (R2) instead of the flag hand-off (R1)
   const char* te = getenv("IRC_LSTM_COOP_BWD_TAGGED");
-  const int tagged = te ? atoi(te) : 1;
+  const int tagged = te ? atoi(te) : 0;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
   if (tagged) hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 3), st);
   prof_begin(st);
