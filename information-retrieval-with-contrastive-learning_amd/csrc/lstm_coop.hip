@@ -51,6 +51,7 @@ constexpr int GSTEP = BG * 4 * H;            // floats of gates per (dir, group,
 constexpr int CSTEP = BG * H;                // floats of c per (dir, group, t)
 constexpr int MAX_GROUPS = 16;               // per launch (co-residency bound)
 constexpr unsigned SPIN_MAX = 1u << 24;      // default spin bound (IRC_LSTM_COOP_SPIN_MAX)
+constexpr int NFLAG = P * NW;                // backward flag words per (dir, group)
 
 typedef __attribute__((address_space(1))) unsigned int gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -132,7 +133,8 @@ __device__ __forceinline__ void publish_flag(unsigned* flag, unsigned epoch) {
     __hip_atomic_store((gu32*)flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// R1 consume: wave 0 polls the P flags (relaxed, >= epoch), then a barrier.
+// R1 consume: wave 0 polls the P member flags (word NW*member; relaxed, >= epoch),
+// then a barrier.
 __device__ __forceinline__ void poll_flags(unsigned* flags, unsigned epoch, unsigned* tmo,
                                            int* abort_lds, unsigned spin_max) {
   if (threadIdx.x < 64) {
@@ -140,7 +142,7 @@ __device__ __forceinline__ void poll_flags(unsigned* flags, unsigned epoch, unsi
     for (unsigned spins = 0;;) {
       bool ok = true;
       if (lane < P)
-        ok = __hip_atomic_load((gu32*)(flags + lane), __ATOMIC_RELAXED,
+        ok = __hip_atomic_load((gu32*)(flags + lane * NW), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT) >= epoch;
       if (__all(ok) && spin_max) break;
       if (++spins > spin_max) {
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     for (int i = 0; i < 4; ++i) dc[rb][i] = 0.f;
   // partials [2 parity][P member][block = (w*4 + cb)*2 + rb][64 lanes][4] fp32
   float* X = reinterpret_cast<float*>(xch) + (int64_t)(dir * ngrp_total + grp) * 2 * P * PART;
-  unsigned* fl = flags + (dir * ngrp_total + grp) * P;
+  unsigned* fl = flags + (dir * ngrp_total + grp) * NFLAG;
   __syncthreads();
 
   for (int s = 0; s < L; ++s) {
@@ -462,7 +464,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
         }
       }
       const unsigned ep = (unsigned)s;
-      if (tagged) {
+      if (tagged == 1) {
         // R2 (the data is the flag): each partial float travels as a granule
         // {value, epoch}, two per 16-byte write-through store; block (wave w = unit
         // block 64w = destination member w, cb, rb), lane, 4 rows -> 4 granules
@@ -533,9 +535,34 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
         for (int cb = 0; cb < 4; ++cb)
           st_sc1_x4(Xp + ((((w * 4 + cb) * 2 + rb) * 64 + lane) * 4),
                     __builtin_bit_cast(u32x4, acc[rb][cb]));
-      publish_flag(fl + m, ep);
-      poll_flags(fl, ep, tmo, &abort_lds, spin_max);
-      if (abort_lds) return;
+      if (tagged == 2) {
+        // per-wave flags: wave w's partial is member w's alone, so each wave drains its
+        // own stores and raises its own flag, and reader wave w of member m waits only
+        // for wave m of every member -- no workgroup barrier on either side
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+          __hip_atomic_store((gu32*)(fl + m * NW + w), ep, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        for (unsigned spins = 0;;) {
+          bool ok = true;
+          if (lane < P)
+            ok = __hip_atomic_load((gu32*)(fl + lane * NW + m), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) >= ep;
+          if (__all(ok) && spin_max) break;
+          if (++spins > spin_max) {
+            if (lane == 0) {
+              __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              abort_lds = 1;
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      } else {
+        publish_flag(fl + m * NW, ep);
+        poll_flags(fl, ep, tmo, &abort_lds, spin_max);
+        if (abort_lds) return;
+      }
       // own units live in every member's block m, cb = w: sum in member order
       u32x4 v[P][2];
 #pragma unroll
@@ -656,7 +683,7 @@ extern "C" int64_t irc_lstm_coop_sizes(int64_t B, int64_t L, int64_t H, int64_t 
     case 1: return ndir * ngrp * L * lstmc::CSTEP;
     case 2: return ndir * ngrp * 2 * lstmc::BG * (H / 2) * 8;   // granules
     case 3: return ndir * ngrp * 2 * lstmc::P * lstmc::PART * 8;  // fp32 partials as granules
-    case 4: return ((ndir * ngrp * lstmc::P + 1) * 4 + 15) / 16 * 16;
+    case 4: return ((ndir * ngrp * lstmc::NFLAG + 1) * 4 + 15) / 16 * 16;
   }
   return -1;
 }
@@ -715,7 +742,7 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
   const char* se = getenv("IRC_LSTM_COOP_SENTINELS");
   const int sentinels = se ? atoi(se) : 0;
   unsigned* flags = static_cast<unsigned*>(sync);
-  unsigned* tmo = flags + ndir * ngrp * lstmc::P;
+  unsigned* tmo = flags + ndir * ngrp * lstmc::NFLAG;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
   hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 2), st);
   prof_begin(st);
@@ -742,14 +769,15 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
   const int gpl = coop_groups_per_launch(ndir);
   const unsigned spin_max = coop_spin_max();
   unsigned* flags = static_cast<unsigned*>(sync);
-  unsigned* tmo = flags + ndir * ngrp * lstmc::P;
+  unsigned* tmo = flags + ndir * ngrp * lstmc::NFLAG;
+  // IRC_LSTM_COOP_BWD_TAGGED=2: per-wave flags (no workgroup barrier in the hand-off);
   // IRC_LSTM_COOP_BWD_TAGGED=1: tagged granules (R2) instead of the flag hand-off (R1);
   // bit-identical, but 505 vs 350 us per layer at C2 (16 granule loads per lane per
   // sweep pass against 8 plain loads after one flag poll)
   const char* te = getenv("IRC_LSTM_COOP_BWD_TAGGED");
   const int tagged = te ? atoi(te) : 0;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
-  if (tagged) hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 3), st);
+  if (tagged == 1) hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 3), st);
   prof_begin(st);
   for (int g0 = 0; g0 < ngrp; g0 += gpl) {
     const int n = ngrp - g0 < gpl ? ngrp - g0 : gpl;
@@ -767,7 +795,7 @@ extern "C" int irc_lstm_coop_fault(const void* sync, int64_t B, int64_t ndir, vo
                                    irc_stream_t stream) {
   IRC_REQUIRE(sync != nullptr && fault != nullptr, "lstm_coop_fault: null pointer");
   const int64_t ngrp = (B + lstmc::BG - 1) / lstmc::BG;
-  const unsigned* tmo = static_cast<const unsigned*>(sync) + ndir * ngrp * lstmc::P;
+  const unsigned* tmo = static_cast<const unsigned*>(sync) + ndir * ngrp * lstmc::NFLAG;
   hipLaunchKernelGGL(lstmc::fault_or_kernel, dim3(1), dim3(64), 0, as_stream(stream), tmo,
                      static_cast<unsigned*>(fault));
   return check_launch("lstm_coop_fault");

@@ -334,7 +334,7 @@ def lstm_coop_fault(sync, B, ndir, fault):
 
 def lstm_coop_timed_out(sync, B, ndir):
     """Host check (synchronising) of a coop call's timeout word."""
-    n = ndir * ((B + 31) // 32) * 4
+    n = ndir * ((B + 31) // 32) * 16  # after the P * NW = 16 flag words per (dir, group)
     return int(sync[n].item()) != 0
 
 
