@@ -244,6 +244,8 @@ int irc_lstm_bwd(int dtype, const float* dy, const void* whh, const float* gsave
  *   unit interleaved (packed column 4u+g <- original g*H+u) plus the matching
  *   b_ih + b_hh, and W_hh -> bf16 B-operand fragments for the forward and the
  *   backward recurrence (4H*H elements per direction each; private layout).
+ *   whh_bf16 and whhT_bf16 may both be NULL (W_ih / bias pack only: the cluster
+ *   recurrence packs W_hh itself with irc_lstm_coop_pack).
  * irc_lstm_fwd_mfma: xp_packed = x . wih_packed^T + bias_packed (irc_gemm, fp32),
  *   hout bf16 [B*L][ndir*H]; gsave/csave (sizes from irc_lstm_mfma_save_floats,
  *   which 0 = gates, 1 = c; a layout private to these two kernels) and hprev bf16

@@ -370,6 +370,8 @@ extern "C" int irc_lstm_pack(const float* wih, const float* bih, const float* bh
   const int64_t n1 = ndir * 4 * H * In;
     hipLaunchKernelGGL(lstmm::pack_wih_kernel<256>, dim3(nb256(n1)), dim3(256), 0, st, wih, bih,
                        bhh, (unsigned short*)wih_packed, bias_packed, (int)In, (int)ndir);
+  IRC_REQUIRE((whh_bf16 == nullptr) == (whhT_bf16 == nullptr), "lstm_pack: whh outputs together");
+  if (whh_bf16 == nullptr) return check_launch("lstm_pack");  // the cluster path packs W_hh itself
   const int64_t n2 = ndir * 4 * H * H;
   hipLaunchKernelGGL(lstmm::pack_whh_kernel<256>, dim3(nb256(n2)), dim3(256), 0, st, whh,
                      (unsigned short*)whh_bf16, (unsigned short*)whhT_bf16, (int)ndir);

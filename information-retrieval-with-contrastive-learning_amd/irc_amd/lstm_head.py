@@ -207,7 +207,7 @@ class LSTMHead(nn.Module):
         if kind in ("coop", "mfma"):
             # MFMA recurrence: packed W_ih columns so xp is read as per-unit float4s
             wih, bih, bhh, whh = self._layer_fp32(l)
-            wp, bp, w, wT = ops.lstm_pack(wih, bih, bhh, whh, H, nd)
+            wp, bp, w, wT = ops.lstm_pack(wih, bih, bhh, whh, H, nd, whh_packs=kind != "coop")
             xp = ops.gemm(x, wp, bias=bp, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
             if kind == "coop":
                 wf, wb = ops.lstm_coop_pack(whh, H, nd)

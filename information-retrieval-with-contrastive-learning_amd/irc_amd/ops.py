@@ -239,15 +239,17 @@ def lstm_mfma_supported(H):
     return bool(_lib.load().irc_lstm_mfma_supported(H))
 
 
-def lstm_pack(wih, bih, bhh, whh, H, ndir):
-    """fp32 weights of one layer -> (wih_packed bf16, bias_packed fp32, whh bf16, whhT bf16)."""
+def lstm_pack(wih, bih, bhh, whh, H, ndir, whh_packs=True):
+    """fp32 weights of one layer -> (wih_packed bf16, bias_packed fp32, whh bf16, whhT bf16);
+    whh_packs=False skips the single-CU recurrence's W_hh packs (None, None): the cluster
+    recurrence packs W_hh itself (lstm_coop_pack)."""
     require_hip(wih, bih, bhh, whh)
     dev = wih.device
     In = wih.shape[1]
     wp = torch.empty((ndir * 4 * H, In), dtype=BF16, device=dev)
     bp = torch.empty((ndir * 4 * H,), dtype=F32, device=dev)
-    w = torch.empty((ndir, 4 * H, H), dtype=BF16, device=dev)
-    wT = torch.empty((ndir, H, 4 * H), dtype=BF16, device=dev)
+    w = torch.empty((ndir, 4 * H, H), dtype=BF16, device=dev) if whh_packs else None
+    wT = torch.empty((ndir, H, 4 * H), dtype=BF16, device=dev) if whh_packs else None
     _lib.call("irc_lstm_pack", ptr(wih), ptr(bih), ptr(bhh), ptr(whh), In, H, ndir, ptr(wp),
               ptr(bp), ptr(w), ptr(wT), stream_ptr(dev))
     return wp, bp, w, wT
