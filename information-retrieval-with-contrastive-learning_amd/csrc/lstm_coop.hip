@@ -39,7 +39,7 @@ namespace lstmc {
 
 constexpr int H = 256;
 constexpr int P = 4;            // workgroups per cluster
-constexpr int BG32 = 32;        // sequences per group of the RB = 2 form (sizes, flags)
+constexpr int BG = 32;          // sequences per group
 constexpr int NW = 4;           // waves per workgroup
 constexpr int NTH = NW * 64;
 constexpr int UPW = H / P;      // 64 units per member
@@ -47,6 +47,8 @@ constexpr int UPV = UPW / NW;   // 16 units per wave (forward)
 constexpr int KKF = H / 32;     // forward k-steps (K = 256)
 constexpr int HP = H + 8;       // LDS row pitch (bf16) of h / dgates
 constexpr int WSLICE = 4 * UPW * H;          // bf16 elements of one member's W slice (64K)
+constexpr int GSTEP = BG * 4 * H;            // floats of gates per (dir, group, t)
+constexpr int CSTEP = BG * H;                // floats of c per (dir, group, t)
 constexpr int MAX_GROUPS = 16;               // per launch (co-residency bound)
 constexpr unsigned SPIN_MAX = 1u << 24;      // default spin bound (IRC_LSTM_COOP_SPIN_MAX)
 constexpr int NFLAG = P * NW;                // backward flag words per (dir, group)
@@ -198,17 +200,11 @@ __device__ __forceinline__ Member decode() {
 // hout [B*L][ndir*H] bf16; gsave/csave (may be null) in the member-fragment
 // order read back by lstm_bwd_coop; xch [ndir][ngrp][2][BG][H] bf16, flags
 // [ndir][ngrp][P] (zeroed), tmo [1].
-// RB row blocks of 16: BG = 16 * RB sequences per cluster (2 or 3; 4 would not fit
-// the 160 KB of LDS next to the 128 KB W slice).
-template <int RB>
 __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     const float* __restrict__ xp, const unsigned short* __restrict__ wpk,
     unsigned short* __restrict__ hout, float* __restrict__ gsave, float* __restrict__ csave,
     unsigned short* __restrict__ hprev, unsigned short* xch, unsigned* flags, unsigned* tmo, int B,
     int L, int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max, int sentinels) {
-  constexpr int BG = 16 * RB;
-  constexpr int GSTEP = BG * 4 * H;  // floats of gates per (dir, group, t)
-  constexpr int CSTEP = BG * H;      // floats of c per (dir, group, t)
   __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
   __shared__ __attribute__((aligned(16))) unsigned short hb[BG][HP];
   __shared__ int abort_lds;
@@ -239,14 +235,14 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     }
   }
   const int u = m * UPW + w * UPV + r16;  // this lane's hidden unit
-  float c[RB][4];
+  float c[2][4];
 #pragma unroll
-  for (int rb = 0; rb < RB; ++rb)
+  for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) c[rb][i] = 0.f;
-  auto load_xp = [&](int t, f32x4 (&dst)[RB][4]) {
+  auto load_xp = [&](int t, f32x4 (&dst)[2][4]) {
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
+    for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         int b = b0 + rb * 16 + 4 * q4 + i;
@@ -255,7 +251,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
                                                      (int64_t)dir * 4 * H + 4 * u);
       }
   };
-  f32x4 xr[RB][4];
+  f32x4 xr[2][4];
   load_xp(dir == 0 ? 0 : L - 1, xr);
   // granules [2 parity][BG][H/2]: {epoch, two bf16 of units 2c, 2c+1}
   unsigned long long* X =
@@ -265,9 +261,9 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
 
   for (int s = 0; s < L; ++s) {
     const int t = dir == 0 ? s : L - 1 - s;
-    f32x4 acc[RB][4];
+    f32x4 acc[2][4];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
+    for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
@@ -276,24 +272,24 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     if (s > 0) {
 #pragma unroll 2
       for (int kk = 0; kk < KKF; ++kk) {
-        bf16x8 a[RB];
+        bf16x8 a[2];
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
+        for (int rb = 0; rb < 2; ++rb)
           a[rb] = *reinterpret_cast<const bf16x8*>(&hb[rb * 16 + r16][kk * 32 + 8 * q4]);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const bf16x8 bw = *reinterpret_cast<const bf16x8*>(
               &wl[(((w * 4 + g) * KKF + kk) * 64 + lane) * 8]);
 #pragma unroll
-          for (int rb = 0; rb < RB; ++rb)
+          for (int rb = 0; rb < 2; ++rb)
             acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw, acc[rb][g], 0, 0, 0);
         }
       }
     }
     __syncthreads();  // every read of h_{t-1} done
-    f32x4 gv[RB][4], cv[RB];
+    f32x4 gv[2][4], cv[2];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
+    for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float ig = sigm(acc[rb][0][i]);
@@ -346,12 +342,12 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
       float* gs = gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP;
       float* cs = csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP;
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
+      for (int rb = 0; rb < 2; ++rb) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          *reinterpret_cast<f32x4*>(gs + ((((m * NW + w) * RB + rb) * 4 + i) * 64 + lane) * 4) =
+          *reinterpret_cast<f32x4*>(gs + ((((m * NW + w) * 2 + rb) * 4 + i) * 64 + lane) * 4) =
               gv[rb][i];
-        *reinterpret_cast<f32x4*>(cs + (((m * NW + w) * RB + rb) * 64 + lane) * 4) = cv[rb];
+        *reinterpret_cast<f32x4*>(cs + (((m * NW + w) * 2 + rb) * 64 + lane) * 4) = cv[rb];
       }
     }
     for (int p = threadIdx.x; p < BG * UPW / 8; p += NTH) {  // h_t -> hout (own slice)
@@ -378,17 +374,13 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
 // lstm_fwd_coop; dg out [B*L][ndir*4H] bf16 (original gate order); xch fp32
 // [ndir][ngrp][2][P][64 units/wave-block ... fragment order] partials, flags, tmo.
 constexpr int KKB = 4 * UPW / 32;  // 8 k-steps over the member's 256 gate columns
+constexpr int PART = BG * H;       // floats of one member's partial dh
 
-template <int RB>
 __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     const float* __restrict__ dy, const unsigned short* __restrict__ wtpk,
     const float* __restrict__ gsave, const float* __restrict__ csave,
     unsigned short* __restrict__ dg, float* xch, unsigned* flags, unsigned* tmo, int B, int L,
     int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max, int tagged) {
-  constexpr int BG = 16 * RB;
-  constexpr int GSTEP = BG * 4 * H;
-  constexpr int CSTEP = BG * H;
-  constexpr int PART = BG * H;  // floats of one member's partial dh
   __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
   __shared__ __attribute__((aligned(16))) unsigned short dgl[BG][HP];  // own dgates, k = g*64+lu
   __shared__ int abort_lds;
@@ -410,9 +402,9 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
   // cell ownership as in the forward: lane -> unit u (own), rows rb*16 + 4*q4 + i
   const int lu = w * UPV + r16;  // local unit 0..63
   const int u = m * UPW + lu;
-  float dc[RB][4];
+  float dc[2][4];
 #pragma unroll
-  for (int rb = 0; rb < RB; ++rb)
+  for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) dc[rb][i] = 0.f;
   // partials [2 parity][P member][block = (w*4 + cb)*2 + rb][64 lanes][4] fp32
@@ -426,53 +418,53 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     const bool has_prev = tp >= 0 && tp < L;
     // this step's saved gates / c / c_prev / dy: issued now, consumed after the
     // MFMAs and the exchange (their latency hides behind both)
-    f32x4 pgv[RB][4], pcv[RB], pcp[RB];
-    float pdy[RB][4];
+    f32x4 pgv[2][4], pcv[2], pcp[2];
+    float pdy[2][4];
     {
       const float* gs = gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP;
       const float* cs = csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP;
       const float* csp =
           has_prev ? csave + ((int64_t)(dir * ngrp_total + grp) * L + tp) * CSTEP : nullptr;
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        const int64_t co = (((m * NW + w) * RB + rb) * 64 + lane) * 4;
+      for (int rb = 0; rb < 2; ++rb) {
+        const int64_t co = (((m * NW + w) * 2 + rb) * 64 + lane) * 4;
         pcv[rb] = *reinterpret_cast<const f32x4*>(cs + co);
         pcp[rb] = csp ? *reinterpret_cast<const f32x4*>(csp + co) : (f32x4)0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           pgv[rb][i] = *reinterpret_cast<const f32x4*>(
-              gs + ((((m * NW + w) * RB + rb) * 4 + i) * 64 + lane) * 4);
+              gs + ((((m * NW + w) * 2 + rb) * 4 + i) * 64 + lane) * 4);
           const int b = b0 + rb * 16 + 4 * q4 + i;
           pdy[rb][i] = b < B ? dy[((int64_t)b * L + t) * hld + dir * H + u] : 0.f;
         }
       }
     }
     // dh from dgates of the step after (K-split partial over own gate columns)
-    f32x4 dh[RB];  // own cells' summed recurrent gradient
+    f32x4 dh[2];  // own cells' summed recurrent gradient
     dh[0] = dh[1] = (f32x4)0.f;
     if (s > 0) {
-      f32x4 acc[RB][4];  // partial for units 64w + 16cb + r16
+      f32x4 acc[2][4];  // partial for units 64w + 16cb + r16
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
+      for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = (f32x4)0.f;
 #pragma unroll 2
       for (int kk = 0; kk < KKB; ++kk) {
-        bf16x8 a[RB];
+        bf16x8 a[2];
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
+        for (int rb = 0; rb < 2; ++rb)
           a[rb] = *reinterpret_cast<const bf16x8*>(&dgl[rb * 16 + r16][kk * 32 + 8 * q4]);
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
           const bf16x8 bw = *reinterpret_cast<const bf16x8*>(
               &wl[(((w * 4 + cb) * KKB + kk) * 64 + lane) * 8]);
 #pragma unroll
-          for (int rb = 0; rb < RB; ++rb)
+          for (int rb = 0; rb < 2; ++rb)
             acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw, acc[rb][cb], 0, 0, 0);
         }
       }
       const unsigned ep = (unsigned)s;
-      if (RB == 2 && tagged == 1) {
+      if (tagged == 1) {
         // R2 (the data is the flag): each partial float travels as a granule
         // {value, epoch}, two per 16-byte write-through store; block (wave w = unit
         // block 64w = destination member w, cb, rb), lane, 4 rows -> 4 granules
@@ -484,7 +476,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
           for (int cb = 0; cb < 4; ++cb) {
-            unsigned long long* q = Gp + ((((w * 4 + cb) * RB + rb) * 64 + lane) * 4);
+            unsigned long long* q = Gp + ((((w * 4 + cb) * 2 + rb) * 64 + lane) * 4);
             st_sc1_pair(q, granule(ep, __float_as_uint(acc[rb][cb][0])),
                         granule(ep, __float_as_uint(acc[rb][cb][1])));
             st_sc1_pair(q + 2, granule(ep, __float_as_uint(acc[rb][cb][2])),
@@ -500,7 +492,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
 #pragma unroll
               for (int j = 0; j < 2; ++j)
                 v[mm][rb][j] =
-                    ld_sc1_x4(Gs + (int64_t)mm * PART + ((((m * 4 + w) * RB + rb) * 64 + lane) * 4) + 2 * j);
+                    ld_sc1_x4(Gs + (int64_t)mm * PART + ((((m * 4 + w) * 2 + rb) * 64 + lane) * 4) + 2 * j);
           asm volatile("s_waitcnt vmcnt(0)"
                        : "+v"(v[0][0][0]), "+v"(v[0][0][1]), "+v"(v[0][1][0]), "+v"(v[0][1][1]),
                          "+v"(v[1][0][0]), "+v"(v[1][0][1]), "+v"(v[1][1][0]), "+v"(v[1][1][1]),
@@ -538,10 +530,10 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
       float* Xs = X + (int64_t)(s & 1) * P * PART;
       float* Xp = Xs + (int64_t)m * PART;
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
+      for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
-          st_sc1_x4(Xp + ((((w * 4 + cb) * RB + rb) * 64 + lane) * 4),
+          st_sc1_x4(Xp + ((((w * 4 + cb) * 2 + rb) * 64 + lane) * 4),
                     __builtin_bit_cast(u32x4, acc[rb][cb]));
       if (tagged == 2) {
         // per-wave flags: wave w's partial is member w's alone, so each wave drains its
@@ -572,29 +564,21 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
         if (abort_lds) return;
       }
       // own units live in every member's block m, cb = w: sum in member order
-      u32x4 v[P][RB];
+      u32x4 v[P][2];
 #pragma unroll
       for (int mm = 0; mm < P; ++mm)
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-          v[mm][rb] = ld_sc1_x4(Xs + (int64_t)mm * PART + ((((m * 4 + w) * RB + rb) * 64 + lane) * 4));
-      if constexpr (RB == 2)
-        asm volatile("s_waitcnt vmcnt(0)"
-                     : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[1][0]), "+v"(v[1][1]), "+v"(v[2][0]),
-                       "+v"(v[2][1]), "+v"(v[3][0]), "+v"(v[3][1])
-                     :
-                     : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)"
-                     : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[0][2]), "+v"(v[1][0]), "+v"(v[1][1]),
-                       "+v"(v[1][2]), "+v"(v[2][0]), "+v"(v[2][1]), "+v"(v[2][2]), "+v"(v[3][0]),
-                       "+v"(v[3][1]), "+v"(v[3][2])
-                     :
-                     : "memory");
+        for (int rb = 0; rb < 2; ++rb)
+          v[mm][rb] = ld_sc1_x4(Xs + (int64_t)mm * PART + ((((m * 4 + w) * 2 + rb) * 64 + lane) * 4));
+      asm volatile("s_waitcnt vmcnt(0)"
+                   : "+v"(v[0][0]), "+v"(v[0][1]), "+v"(v[1][0]), "+v"(v[1][1]), "+v"(v[2][0]),
+                     "+v"(v[2][1]), "+v"(v[3][0]), "+v"(v[3][1])
+                   :
+                   : "memory");
 #pragma unroll
       for (int mm = 0; mm < P; ++mm)
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
+        for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
           for (int i = 0; i < 4; ++i) dh[rb][i] += __uint_as_float(v[mm][rb][i]);
       }
@@ -602,7 +586,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     __syncthreads();  // all reads of dgl (MFMA) done before it is overwritten
     if (abort_lds) return;
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
+    for (int rb = 0; rb < 2; ++rb) {
       const f32x4 cv = pcv[rb], cp = pcp[rb];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -692,17 +676,13 @@ using namespace irc;
 extern "C" int irc_lstm_coop_supported(int64_t H) { return H == lstmc::H; }
 
 extern "C" int64_t irc_lstm_coop_sizes(int64_t B, int64_t L, int64_t H, int64_t ndir, int which) {
-  // 0: gates floats, 1: c floats, 2: fwd exchange bytes, 3: bwd exchange bytes, 4: flag bytes.
-  // Sized for either cluster height (32 or 48 sequences): rows = the padded batch of the
-  // larger, flags for the 32-row grouping (the most groups).
-  const int64_t ngrp = (B + lstmc::BG32 - 1) / lstmc::BG32;
-  const int64_t r32 = ngrp * 32, r48 = (B + 47) / 48 * 48;
-  const int64_t rows = r32 > r48 ? r32 : r48;
+  // 0: gates floats, 1: c floats, 2: fwd exchange bytes, 3: bwd exchange bytes, 4: flag bytes
+  const int64_t ngrp = (B + lstmc::BG - 1) / lstmc::BG;
   switch (which) {
-    case 0: return ndir * rows * L * 4 * H;
-    case 1: return ndir * rows * L * H;
-    case 2: return ndir * 2 * rows * (H / 2) * 8;         // granules
-    case 3: return ndir * 2 * lstmc::P * rows * H * 8;    // fp32 partials as granules
+    case 0: return ndir * ngrp * L * lstmc::GSTEP;
+    case 1: return ndir * ngrp * L * lstmc::CSTEP;
+    case 2: return ndir * ngrp * 2 * lstmc::BG * (H / 2) * 8;   // granules
+    case 3: return ndir * ngrp * 2 * lstmc::P * lstmc::PART * 8;  // fp32 partials as granules
     case 4: return ((ndir * ngrp * lstmc::NFLAG + 1) * 4 + 15) / 16 * 16;
   }
   return -1;
@@ -746,14 +726,7 @@ static void coop_poison(const unsigned* tmo, void* out, int64_t n, hipStream_t s
                      (unsigned short*)out, n, (unsigned short*)out2, n2);
 }
 
-// Rows per cluster: 32 (RB = 2) or 48 (RB = 3, IRC_LSTM_COOP_RB=3); the forward and the
-// backward of one layer must use the same value (the saved state's layout follows it).
-static int coop_rb() {
-  const char* e = getenv("IRC_LSTM_COOP_RB");
-  return (e && atoi(e) == 3) ? 3 : 2;
-}
-
-// sync: flags (ndir*ngrp32*P*NW words) followed by the timeout word; zeroed here.
+// sync: flags (ndir*ngrp*P words) followed by the timeout word; zeroed here.
 extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* hout, float* gsave,
                                  float* csave, void* hprev, void* xch, void* sync, int64_t B,
                                  int64_t L, int64_t H, int64_t ndir, irc_stream_t stream) {
@@ -761,9 +734,7 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
   IRC_REQUIRE((gsave == nullptr) == (csave == nullptr), "lstm_fwd_coop: gsave/csave together");
   if (B == 0 || L == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
-  const int rb = coop_rb(), bg = 16 * rb;
-  const int ngrp = (int)((B + bg - 1) / bg);
-  const int64_t ngrp32 = (B + lstmc::BG32 - 1) / lstmc::BG32;
+  const int ngrp = (int)((B + lstmc::BG - 1) / lstmc::BG);
   const int gpl = coop_groups_per_launch(ndir);
   const unsigned spin_max = coop_spin_max();
   // The granule sweep polls by itself: 287 vs 316 us per layer at C2 with the wave-0
@@ -771,23 +742,17 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
   const char* se = getenv("IRC_LSTM_COOP_SENTINELS");
   const int sentinels = se ? atoi(se) : 0;
   unsigned* flags = static_cast<unsigned*>(sync);
-  unsigned* tmo = flags + ndir * ngrp32 * lstmc::NFLAG;
+  unsigned* tmo = flags + ndir * ngrp * lstmc::NFLAG;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
   hipMemsetAsync(xch, 0, irc_lstm_coop_sizes(B, L, H, ndir, 2), st);
   prof_begin(st);
   for (int g0 = 0; g0 < ngrp; g0 += gpl) {
     const int n = ngrp - g0 < gpl ? ngrp - g0 : gpl;
     const dim3 grid((unsigned)((n + 7) / 8 * 32), (unsigned)ndir);
-    if (rb == 3)
-      hipLaunchKernelGGL(lstmc::lstm_fwd_coop<3>, grid, dim3(lstmc::NTH), 0, st, xp_packed,
-                         (const unsigned short*)wf, (unsigned short*)hout, gsave, csave,
-                         (unsigned short*)hprev, (unsigned short*)xch, flags, tmo, (int)B, (int)L,
-                         (int)ndir, g0, n, ngrp, spin_max, sentinels);
-    else
-      hipLaunchKernelGGL(lstmc::lstm_fwd_coop<2>, grid, dim3(lstmc::NTH), 0, st, xp_packed,
-                         (const unsigned short*)wf, (unsigned short*)hout, gsave, csave,
-                         (unsigned short*)hprev, (unsigned short*)xch, flags, tmo, (int)B, (int)L,
-                         (int)ndir, g0, n, ngrp, spin_max, sentinels);
+    hipLaunchKernelGGL(lstmc::lstm_fwd_coop, grid, dim3(lstmc::NTH), 0, st, xp_packed,
+                       (const unsigned short*)wf, (unsigned short*)hout, gsave, csave,
+                       (unsigned short*)hprev, (unsigned short*)xch, flags, tmo, (int)B, (int)L,
+                       (int)ndir, g0, n, ngrp, spin_max, sentinels);
   }
   prof_end("lstm_fwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
   coop_poison(tmo, hout, B * L * ndir * H, st, hprev, hprev ? B * L * ndir * H : 0);
@@ -800,13 +765,11 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
   IRC_REQUIRE(H == lstmc::H, "lstm_bwd_coop: H=%lld", (long long)H);
   if (B == 0 || L == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
-  const int rb = coop_rb(), bg = 16 * rb;
-  const int ngrp = (int)((B + bg - 1) / bg);
-  const int64_t ngrp32 = (B + lstmc::BG32 - 1) / lstmc::BG32;
+  const int ngrp = (int)((B + lstmc::BG - 1) / lstmc::BG);
   const int gpl = coop_groups_per_launch(ndir);
   const unsigned spin_max = coop_spin_max();
   unsigned* flags = static_cast<unsigned*>(sync);
-  unsigned* tmo = flags + ndir * ngrp32 * lstmc::NFLAG;
+  unsigned* tmo = flags + ndir * ngrp * lstmc::NFLAG;
   // IRC_LSTM_COOP_BWD_TAGGED=2: per-wave flags (no workgroup barrier in the hand-off);
   // IRC_LSTM_COOP_BWD_TAGGED=1: tagged granules (R2) instead of the flag hand-off (R1);
   // bit-identical, but 505 vs 350 us per layer at C2 (16 granule loads per lane per
@@ -819,14 +782,9 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
   for (int g0 = 0; g0 < ngrp; g0 += gpl) {
     const int n = ngrp - g0 < gpl ? ngrp - g0 : gpl;
     const dim3 grid((unsigned)((n + 7) / 8 * 32), (unsigned)ndir);
-    if (rb == 3)
-      hipLaunchKernelGGL(lstmc::lstm_bwd_coop<3>, grid, dim3(lstmc::NTH), 0, st, dy,
-                         (const unsigned short*)wb, gsave, csave, (unsigned short*)dg, (float*)xch,
-                         flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp, spin_max, tagged);
-    else
-      hipLaunchKernelGGL(lstmc::lstm_bwd_coop<2>, grid, dim3(lstmc::NTH), 0, st, dy,
-                         (const unsigned short*)wb, gsave, csave, (unsigned short*)dg, (float*)xch,
-                         flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp, spin_max, tagged);
+    hipLaunchKernelGGL(lstmc::lstm_bwd_coop, grid, dim3(lstmc::NTH), 0, st, dy,
+                       (const unsigned short*)wb, gsave, csave, (unsigned short*)dg, (float*)xch,
+                       flags, tmo, (int)B, (int)L, (int)ndir, g0, n, ngrp, spin_max, tagged);
   }
   prof_end("lstm_bwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
   coop_poison(tmo, dg, B * L * ndir * 4 * H, st);
@@ -836,7 +794,7 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
 extern "C" int irc_lstm_coop_fault(const void* sync, int64_t B, int64_t ndir, void* fault,
                                    irc_stream_t stream) {
   IRC_REQUIRE(sync != nullptr && fault != nullptr, "lstm_coop_fault: null pointer");
-  const int64_t ngrp = (B + lstmc::BG32 - 1) / lstmc::BG32;
+  const int64_t ngrp = (B + lstmc::BG - 1) / lstmc::BG;
   const unsigned* tmo = static_cast<const unsigned*>(sync) + ndir * ngrp * lstmc::NFLAG;
   hipLaunchKernelGGL(lstmc::fault_or_kernel, dim3(1), dim3(64), 0, as_stream(stream), tmo,
                      static_cast<unsigned*>(fault));
