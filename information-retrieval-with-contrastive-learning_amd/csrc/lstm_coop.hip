@@ -204,7 +204,8 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     const float* __restrict__ xp, const unsigned short* __restrict__ wpk,
     unsigned short* __restrict__ hout, float* __restrict__ gsave, float* __restrict__ csave,
     unsigned short* __restrict__ hprev, unsigned short* xch, unsigned* flags, unsigned* tmo, int B,
-    int L, int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max, int sentinels) {
+    int L, int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max, int sentinels,
+    int wpub) {
   __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
   __shared__ __attribute__((aligned(16))) unsigned short hb[BG][HP];
   __shared__ int abort_lds;
@@ -302,13 +303,39 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         gv[rb][i] = f32x4{ig, fg, g2, og};
         cv[rb][i] = cn;
       }
-    __syncthreads();  // own slice of h_t complete in LDS
+    if (wpub) {
+      // per-wave publish: this wave's 16 units x 32 rows go out as soon as the wave
+      // has written them (LDS ops of one wave complete in order: no barrier), as 2
+      // granule pairs per lane, and its hout / hprev rows as one 16-byte store per lane
+      const int row = lane >> 1, col = m * UPW + w * UPV + 8 * (lane & 1);
+      if (s + 1 < L) {
+        unsigned long long* Xp = X + (s & 1) * BG * (H / 2);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int idx = k * 64 + lane, pr = idx >> 2, pc = m * UPW + w * UPV + 4 * (idx & 3);
+          const uint2 hv = *reinterpret_cast<const uint2*>(&hb[pr][pc]);
+          st_sc1_pair(Xp + pr * (H / 2) + pc / 2, granule((unsigned)(s + 1), hv.x),
+                      granule((unsigned)(s + 1), hv.y));
+        }
+      }
+      if (b0 + row < B) {
+        const u16x8 hv = *reinterpret_cast<const u16x8*>(&hb[row][col]);
+        *reinterpret_cast<u16x8*>(hout + ((int64_t)(b0 + row) * L + t) * hld + dir * H + col) = hv;
+        const int tn = dir == 0 ? t + 1 : t - 1;
+        if (hprev && tn >= 0 && tn < L)
+          *reinterpret_cast<u16x8*>(hprev + (((int64_t)dir * B + b0 + row) * L + tn) * H + col) =
+              hv;
+      }
+    } else {
+      __syncthreads();  // own slice of h_t complete in LDS
+    }
     if (s + 1 < L) {
       // publish the own 32 x 64 slice as 1024 granules (2 pairs per thread) ...
       const unsigned ep = (unsigned)(s + 1);
       unsigned long long* Xp = X + (s & 1) * BG * (H / 2);
 #pragma unroll
       for (int k = 0; k < BG * UPW / 4 / NTH; ++k) {
+        if (wpub) break;
         const int p = k * NTH + threadIdx.x;
         const int row = p / (UPW / 4), c2 = m * (UPW / 2) + (p % (UPW / 4)) * 2;
         const uint2 hv = *reinterpret_cast<const uint2*>(&hb[row][2 * c2]);
@@ -350,7 +377,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         *reinterpret_cast<f32x4*>(cs + (((m * NW + w) * 2 + rb) * 64 + lane) * 4) = cv[rb];
       }
     }
-    for (int p = threadIdx.x; p < BG * UPW / 8; p += NTH) {  // h_t -> hout (own slice)
+    for (int p = threadIdx.x; p < BG * UPW / 8 && !wpub; p += NTH) {  // h_t -> hout (own slice)
       const int row = p / (UPW / 8), col = m * UPW + (p % (UPW / 8)) * 8;
       if (b0 + row < B) {
         const u16x8 hv = *reinterpret_cast<const u16x8*>(&hb[row][col]);
@@ -741,6 +768,10 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
   // sentinel pass + barrier in front of it (IRC_LSTM_COOP_SENTINELS=1 restores that)
   const char* se = getenv("IRC_LSTM_COOP_SENTINELS");
   const int sentinels = se ? atoi(se) : 0;
+  // IRC_LSTM_COOP_WAVE_PUBLISH=1: each wave publishes its own units right after its cell
+  // update (no workgroup barrier between the cell update and the hand-off)
+  const char* we = getenv("IRC_LSTM_COOP_WAVE_PUBLISH");
+  const int wpub = we ? atoi(we) : 0;
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::NFLAG;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
@@ -752,7 +783,7 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
     hipLaunchKernelGGL(lstmc::lstm_fwd_coop, grid, dim3(lstmc::NTH), 0, st, xp_packed,
                        (const unsigned short*)wf, (unsigned short*)hout, gsave, csave,
                        (unsigned short*)hprev, (unsigned short*)xch, flags, tmo, (int)B, (int)L,
-                       (int)ndir, g0, n, ngrp, spin_max, sentinels);
+                       (int)ndir, g0, n, ngrp, spin_max, sentinels, wpub);
   }
   prof_end("lstm_fwd", st, 2.0 * B * L * ndir * 4.0 * H * H);
   coop_poison(tmo, hout, B * L * ndir * H, st, hprev, hprev ? B * L * ndir * H : 0);
