@@ -768,10 +768,11 @@ extern "C" int irc_lstm_fwd_coop(const float* xp_packed, const void* wf, void* h
   // sentinel pass + barrier in front of it (IRC_LSTM_COOP_SENTINELS=1 restores that)
   const char* se = getenv("IRC_LSTM_COOP_SENTINELS");
   const int sentinels = se ? atoi(se) : 0;
-  // IRC_LSTM_COOP_WAVE_PUBLISH=1: each wave publishes its own units right after its cell
-  // update (no workgroup barrier between the cell update and the hand-off)
+  // Each wave publishes its own units right after its cell update (no workgroup barrier
+  // between the cell update and the hand-off): 287 vs 297 us per layer at C2,
+  // bit-identical; IRC_LSTM_COOP_WAVE_PUBLISH=0 restores the workgroup publish
   const char* we = getenv("IRC_LSTM_COOP_WAVE_PUBLISH");
-  const int wpub = we ? atoi(we) : 0;
+  const int wpub = we ? atoi(we) : 1;
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::NFLAG;
   hipMemsetAsync(sync, 0, irc_lstm_coop_sizes(B, L, H, ndir, 4), st);
