@@ -1,6 +1,6 @@
-# Round 4 job aj (closing): cluster-LSTM backward forms (repro + timing A/B: workgroup flag
-# vs per-wave flags), then the full GPU suite, smoke, the default bench line and the
-# kernel-trace summaries (tools/r4_c.sh, TAG=aj).
+# Round 4 job aj (closing): cluster-LSTM reproducibility, the per-wave publish A/B, then the
+# full GPU suite, smoke, the default bench line and the kernel-trace summaries
+# (tools/r4_c.sh, TAG=aj).
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/r4aj
