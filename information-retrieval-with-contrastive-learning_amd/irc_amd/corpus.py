@@ -12,8 +12,6 @@ for those sentences with padding=True, truncation=True.
 """
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import torch
 
@@ -36,35 +34,9 @@ class DeviceCorpus:
         self.flat, self.offsets, self.lens = self.wp.tokenize_corpus(sents, chunk)
         require_hip(self.flat, self.offsets)
         self.n_sentences = len(sents)
-        # pinned staging ring for the per-micro-batch sentence indices: a fresh
-        # pin_memory() per call can fall through the caching host allocator to a
-        # device-synchronising host allocation while earlier copies are in flight
-        self._ring = []      # [pinned int64 buffer, event or None]
-        self._ring_pos = 0
 
     def sentence_index(self, doc: int, sent: int) -> int:
         return int(self.doc_start[doc] + sent)
-
-    def _to_device(self, sel: np.ndarray) -> torch.Tensor:
-        """sel (int64, host) -> device copy on the current stream, staged through a
-        ring of 4 pinned buffers reused once their previous copy has completed."""
-        n = sel.shape[0]
-        if not self._ring:
-            self._ring = [[None, None] for _ in range(4)]
-        slot = self._ring[self._ring_pos]
-        self._ring_pos = (self._ring_pos + 1) % len(self._ring)
-        if slot[1] is not None:
-            slot[1].synchronize()  # the copy 4 calls ago: long done in a pipelined loop
-        if slot[0] is None or slot[0].numel() < n:
-            slot[0] = torch.empty((max(n, 1024),), dtype=torch.int64, pin_memory=True)
-        host = slot[0][:n]
-        host.numpy()[:] = sel
-        out = torch.empty((n,), dtype=torch.int64, device=self.device)
-        out.copy_(host, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        slot[1] = ev
-        return out
 
     def batch(self, sel):
         """(input_ids, attention_mask) int64 [len(sel), L] of the selected sentences,
@@ -74,10 +46,7 @@ class DeviceCorpus:
         n = sel.shape[0]
         longest = int(self.lens[sel].max()) if n else 0
         L = max(min(longest, self.wp.max_tokens) + 2, 2)
-        if os.environ.get("IRC_CORPUS_PIN_RING", "1") == "0":  # the per-call pin_memory() form
-            sel_d = torch.from_numpy(sel).pin_memory().to(self.device, non_blocking=True)
-        else:
-            sel_d = self._to_device(sel)
+        sel_d = torch.from_numpy(sel).pin_memory().to(self.device, non_blocking=True)
         ids = torch.empty((n, L), dtype=torch.int64, device=self.device)
         mask = torch.empty((n, L), dtype=torch.int64, device=self.device)
         _lib.call("irc_pair_batch", ptr(self.flat), ptr(self.offsets), ptr(sel_d), n, L,
