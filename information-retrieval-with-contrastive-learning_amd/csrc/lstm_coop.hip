@@ -585,15 +585,6 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
           }
           __builtin_amdgcn_s_sleep(1);
         }
-      } else if (tagged == 3) {
-        // counted member flag: each wave drains its own stores and adds 1 to its member's
-        // word (no producer-side barrier); wave 0 waits for NW * ep on all P words
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-          __hip_atomic_fetch_add((gu32*)(fl + m * NW), 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-        poll_flags(fl, ep * NW, tmo, &abort_lds, spin_max);
-        if (abort_lds) return;
       } else {
         publish_flag(fl + m * NW, ep);
         poll_flags(fl, ep, tmo, &abort_lds, spin_max);
@@ -811,7 +802,6 @@ extern "C" int irc_lstm_bwd_coop(const float* dy, const void* wb, const float* g
   const unsigned spin_max = coop_spin_max();
   unsigned* flags = static_cast<unsigned*>(sync);
   unsigned* tmo = flags + ndir * ngrp * lstmc::NFLAG;
-  // IRC_LSTM_COOP_BWD_TAGGED=3: counted member flags (no producer-side barrier);
   // IRC_LSTM_COOP_BWD_TAGGED=2: per-wave flags (no workgroup barrier in the hand-off);
   // IRC_LSTM_COOP_BWD_TAGGED=1: tagged granules (R2) instead of the flag hand-off (R1);
   // bit-identical, but 505 vs 350 us per layer at C2 (16 granule loads per lane per
