@@ -436,6 +436,16 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     for (int i = 0; i < 4; ++i) dc[rb][i] = 0.f;
   // partials [2 parity][P member][block = (w*4 + cb)*2 + rb][64 lanes][4] fp32
   float* X = reinterpret_cast<float*>(xch) + (int64_t)(dir * ngrp_total + grp) * 2 * P * PART;
+  auto store_dg = [&](int tt) {  // own dgates rows (LDS) -> dg at time tt
+    for (int p = threadIdx.x; p < BG * 4 * UPW / 8; p += NTH) {
+      const int row = p / (4 * UPW / 8), r = p % (4 * UPW / 8);
+      const int g = r / (UPW / 8), c8 = (r % (UPW / 8)) * 8;
+      if (b0 + row < B)
+        *reinterpret_cast<u16x8*>(dg + ((int64_t)(b0 + row) * L + tt) * gld + dir * 4 * H +
+                                  g * H + m * UPW + c8) =
+            *reinterpret_cast<const u16x8*>(&dgl[row][g * UPW + c8]);
+    }
+  };
   unsigned* fl = flags + (dir * ngrp_total + grp) * NFLAG;
   __syncthreads();
 
@@ -610,6 +620,11 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
           for (int i = 0; i < 4; ++i) dh[rb][i] += __uint_as_float(v[mm][rb][i]);
       }
     }
+#ifdef IRC_COOP_DG_LATE
+    // the previous step's dg rows leave after this step's hand-off, so the publish's
+    // vmcnt(0) does not wait for them (diagnostic build)
+    if (s > 0) store_dg(dir == 0 ? t + 1 : t - 1);
+#endif
     __syncthreads();  // all reads of dgl (MFMA) done before it is overwritten
     if (abort_lds) return;
 #pragma unroll
@@ -630,15 +645,13 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
       }
     }
     __syncthreads();  // own dgates complete: next step's A operand, and the dg rows
-    for (int p = threadIdx.x; p < BG * 4 * UPW / 8; p += NTH) {
-      const int row = p / (4 * UPW / 8), r = p % (4 * UPW / 8);
-      const int g = r / (UPW / 8), c8 = (r % (UPW / 8)) * 8;
-      if (b0 + row < B)
-        *reinterpret_cast<u16x8*>(dg + ((int64_t)(b0 + row) * L + t) * gld + dir * 4 * H + g * H +
-                                  m * UPW + c8) =
-            *reinterpret_cast<const u16x8*>(&dgl[row][g * UPW + c8]);
-    }
+#ifndef IRC_COOP_DG_LATE
+    store_dg(t);
+#endif
   }
+#ifdef IRC_COOP_DG_LATE
+  store_dg(dir == 0 ? 0 : L - 1);
+#endif
 }
 
 // W_hh [ndir][4H][H] fp32 -> the resident slices of both recurrences (bf16).
