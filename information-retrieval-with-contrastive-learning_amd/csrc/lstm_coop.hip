@@ -106,7 +106,9 @@ __device__ __forceinline__ void sweep(F addr, unsigned epoch, unsigned (&v)[N], 
       }
       return;
     }
+#ifndef IRC_COOP_SWEEP_NOSLEEP
     __builtin_amdgcn_s_sleep(1);
+#endif
   }
 }
 
