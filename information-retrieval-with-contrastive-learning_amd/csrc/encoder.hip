@@ -345,70 +345,77 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned shor
   }
 }
 
-// Attention: one workgroup per (sequence b, head a).  qkv is the fused
-// projection output [B*L, 3H] (cols [0,H)=Q, [H,2H)=K, [2H,3H)=V, head a at
-// a*dh); ctx [B*L, H].  K and V of the (b, a) pair are staged in LDS as fp32;
-// each thread owns one query row (q in registers) and runs an online softmax
-// over the unmasked keys.  dh <= 128, L <= 512.
+// Attention, any element type / head dim (the fp32 parity mode, head dims other
+// than 64): one workgroup per (sequence b, head a, 256 queries).  qkv is the fused
+// projection output [B*L, 3H] (cols [0,H)=Q, [H,2H)=K, [2H,3H)=V, head a at a*dh);
+// ctx [B*L, H].  Each thread owns one query row (q and the output in registers) and
+// runs an online softmax over the unmasked keys in ascending order; K and V are
+// streamed through LDS as fp32 tiles of AKT keys, so any L fits (the reference pads
+// a batch jointly up to 512 tokens, contrastive_module.py:38).  dh <= 128.
+constexpr int AKT = 64;
 template <typename T, int DH>
 __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qkv,
                                                        const int64_t* __restrict__ mask,
                                                        T* __restrict__ ctx, int L, int H,
                                                        int heads, float scale) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* Ks = reinterpret_cast<float*>(smem);          // [L][DH]
-  float* Vs = Ks + (size_t)L * DH;                     // [L][DH]
-  int* valid = reinterpret_cast<int*>(Vs + (size_t)L * DH);  // [L] compacted key list
+  __shared__ __attribute__((aligned(16))) float Ks[AKT][DH];
+  __shared__ __attribute__((aligned(16))) float Vs[AKT][DH];
+  __shared__ int kvis[AKT];
   __shared__ int nvalid;
-  const int b = blockIdx.x / heads, a = blockIdx.x % heads;
+  const int nqc = (L + 255) / 256;
+  const int qc = blockIdx.x % nqc;
+  const int a = (blockIdx.x / nqc) % heads, b = blockIdx.x / nqc / heads;
   const int64_t base = (int64_t)b * L;
   const int64_t ld3 = 3LL * H;
-  for (int e = threadIdx.x; e < L * DH; e += blockDim.x) {
-    const int j = e / DH, d = e % DH;
-    Ks[e] = ld(qkv, (base + j) * ld3 + H + a * DH + d);
-    Vs[e] = ld(qkv, (base + j) * ld3 + 2 * H + a * DH + d);
-  }
-  if (threadIdx.x == 0) {
-    int n = 0;
-    for (int j = 0; j < L; ++j)
-      if (mask == nullptr || mask[base + j] != 0) valid[n++] = j;
-    nvalid = n;
-  }
+  if (threadIdx.x == 0) nvalid = 0;
+  __syncthreads();
+  int cnt = 0;
+  for (int j = threadIdx.x; j < L; j += blockDim.x)
+    cnt += (mask == nullptr || mask[base + j] != 0) ? 1 : 0;
+  if (cnt) atomicAdd(&nvalid, cnt);
   __syncthreads();
   // all keys masked: HF's finfo.min bias swamps every score -> uniform weights
   const bool uniform = nvalid == 0;
-  if (uniform)
-    for (int j = threadIdx.x; j < L; j += blockDim.x) valid[j] = j;
-  __syncthreads();
-  const int nv = uniform ? L : nvalid;
-  for (int i = threadIdx.x; i < L; i += blockDim.x) {
-    float qv[DH];
+  const int i = qc * 256 + threadIdx.x;
+  const bool act = i < L;
+  float qv[DH], o[DH];
 #pragma unroll
-    for (int d = 0; d < DH; ++d) qv[d] = ld(qkv, (base + i) * ld3 + a * DH + d) * scale;
-    float m = -INFINITY, l = 0.f;
-    float o[DH];
-#pragma unroll
-    for (int d = 0; d < DH; ++d) o[d] = 0.f;
-    for (int t = 0; t < nv; ++t) {
-      const int j = valid[t];
-      const float* kr = Ks + j * DH;
+  for (int d = 0; d < DH; ++d) {
+    qv[d] = act ? ld(qkv, (base + i) * ld3 + a * DH + d) * scale : 0.f;
+    o[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int j0 = 0; j0 < L; j0 += AKT) {
+    const int n = min(AKT, L - j0);
+    __syncthreads();  // the previous tile's readers are done
+    for (int e = threadIdx.x; e < n * DH; e += blockDim.x) {
+      const int j = e / DH, d = e % DH;
+      Ks[j][d] = ld(qkv, (base + j0 + j) * ld3 + H + a * DH + d);
+      Vs[j][d] = ld(qkv, (base + j0 + j) * ld3 + 2 * H + a * DH + d);
+    }
+    for (int j = threadIdx.x; j < n; j += blockDim.x)
+      kvis[j] = (uniform || mask == nullptr || mask[base + j0 + j] != 0) ? 1 : 0;
+    __syncthreads();
+    if (!act) continue;
+    for (int t = 0; t < n; ++t) {
+      if (!kvis[t]) continue;
       float s = 0.f;
 #pragma unroll
-      for (int d = 0; d < DH; ++d) s += qv[d] * kr[d];
+      for (int d = 0; d < DH; ++d) s += qv[d] * Ks[t][d];
       if (uniform) s = 0.f;
       const float mn = fmaxf(m, s);
       const float corr = __expf(m - mn);
       const float p = __expf(s - mn);
       l = l * corr + p;
-      const float* vr = Vs + j * DH;
 #pragma unroll
-      for (int d = 0; d < DH; ++d) o[d] = o[d] * corr + p * vr[d];
+      for (int d = 0; d < DH; ++d) o[d] = o[d] * corr + p * Vs[t][d];
       m = mn;
     }
-    const float inv = 1.f / l;
-#pragma unroll
-    for (int d = 0; d < DH; ++d) st(ctx, (base + i) * H + a * DH + d, o[d] * inv);
   }
+  if (!act) return;
+  const float inv = 1.f / l;
+#pragma unroll
+  for (int d = 0; d < DH; ++d) st(ctx, (base + i) * H + a * DH + d, o[d] * inv);
 }
 
 // MFMA attention, bf16, head dim 64, L <= 32*NJ (NJ <= 4, any L: the joint
@@ -593,6 +600,181 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
     }
 }
 
+// Long-sequence MFMA attention (bf16 QKV, head dim 64, any L; attention_mfma_kernel
+// holds a whole row of scores in registers and covers L <= 128, this one streams the
+// keys, for the joint padding of a batch up to 512 tokens, contrastive_module.py:38).
+// One wave per (sequence, head, block of 32 queries), no workgroup barrier; keys in
+// tiles of 32 with an online softmax:
+//  * S^T tile = K Q^T on v_mfma_f32_32x32x16_bf16 as attention_mfma_kernel: lane
+//    (i, half) holds query i's scores for keys (e&3) + 8(e>>2) + 4*half of the tile;
+//  * running (max, sum) per query, lane-local plus one exchange with lane ^ 32;
+//  * O^T = V^T P^T: P goes from registers into the B operand (lane = query), so the
+//    rescale of the accumulator by exp(m_old - m_new) is lane-local; the A operand is
+//    the tile's V^T read from this wave's LDS slot in the lanes' permuted key order;
+//  * key bias per tile (0 / -1e30 masked / -3e30 past L): masked keys get exactly
+//    zero weight, an all-masked row averages its L keys (HF's finfo.min bias);
+//  * probabilities rounded to bf16 before P.V (unnormalised, <= 1), O / sum at the end;
+//  * the next tile's K fragments and V rows are loaded while this tile computes.
+//  * MXO (config C5): the context leaves as MX-fp8 (e4m3 ctx8 [B*L][H], one E8M0
+//    scale per (token, 32 head columns) in the MX layout with mpad rows), the values
+//    rounded to bf16 first, so the codes equal quantising the bf16 context.
+template <bool MXO>
+__global__ __launch_bounds__(256) void attention_flash_kernel(
+    const unsigned short* __restrict__ qkv, const int64_t* __restrict__ mask,
+    unsigned short* __restrict__ ctx, int B, int L, int H, int heads, float scale,
+    unsigned char* __restrict__ ctx8, unsigned char* __restrict__ cs, int64_t mpad) {
+  constexpr int DH = 64, VP = 36;  // V^T tile row pitch (u16): 8-byte aligned b64 reads
+  __shared__ __attribute__((aligned(16))) unsigned short vt[4][DH][VP];
+  __shared__ __attribute__((aligned(16))) float mb[4][32];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int nqb = (L + 31) / 32;
+  const int64_t item = (int64_t)blockIdx.x * 4 + wv;  // (b, head, ib), ib fastest
+  if (item >= (int64_t)B * heads * nqb) return;       // no workgroup barrier below
+  const int ib = (int)(item % nqb);
+  const int a = (int)(item / nqb % heads);
+  const int b = (int)(item / nqb / heads);
+  const int64_t ld3 = 3LL * H;
+  const unsigned short* base = qkv + (int64_t)b * L * ld3 + a * DH;  // + j*ld3: Q | +H: K | +2H: V
+  const int64_t* mrow = mask == nullptr ? nullptr : mask + (int64_t)b * L;
+
+  bf16x8 qf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk)
+    qf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)min(32 * ib + r32, L - 1) * ld3 +
+                                               16 * kk + 8 * h);
+  // tile loads: K fragments (row 32jt + r32, clamped), V rows for the V^T image
+  // (lane -> key pair 2*(lane >> 3) + {0, 1} + 16*u, 8-wide d chunk lane & 7), mask
+  const int dc = lane & 7, jp = (lane >> 3) * 2;
+  bf16x8 kf[4];
+  u16x8 vr[2][2];
+  float mbias = 0.f;
+  auto load_tile = [&](int jt) {
+    const int j0 = 32 * jt;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      kf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)min(j0 + r32, L - 1) * ld3 + H +
+                                                 16 * kk + 8 * h);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const int j = j0 + 16 * u + jp + w;
+        vr[u][w] = j < L ? *reinterpret_cast<const u16x8*>(base + (int64_t)j * ld3 + 2 * H + dc * 8)
+                         : (u16x8)0;
+      }
+    const int jm = j0 + r32;
+    mbias = jm >= L ? -3e30f : ((mrow == nullptr || mrow[jm] != 0) ? 0.f : -1e30f);
+  };
+
+  f32x16 o[2] = {(f32x16)0.f, (f32x16)0.f};  // O^T: lane = query, rows d
+  float m = -INFINITY, l = 0.f;
+  const int nkt = (L + 31) / 32;
+  load_tile(0);
+  for (int jt = 0; jt < nkt; ++jt) {
+    // this tile's V^T and key bias into the wave's LDS slot (the previous tile's
+    // reads were consumed by its MFMAs: LDS operations of a wave complete in order)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int dd = 0; dd < 8; ++dd)
+        *reinterpret_cast<uint32_t*>(&vt[wv][dc * 8 + dd][16 * u + jp]) =
+            (uint32_t)vr[u][0][dd] | ((uint32_t)vr[u][1][dd] << 16);
+    if (h == 0) mb[wv][r32] = mbias;
+    f32x16 s = (f32x16)0.f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk], qf[kk], s, 0, 0, 0);
+    if (jt + 1 < nkt) load_tile(jt + 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    float tmx = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 bias = *reinterpret_cast<const f32x4*>(&mb[wv][8 * q + 4 * h]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = s[4 * q + r] * scale + bias[r];
+        s[4 * q + r] = v;
+        tmx = fmaxf(tmx, v);
+      }
+    }
+    tmx = fmaxf(tmx, __shfl_xor(tmx, 32, 64));
+    const float mn = fmaxf(m, tmx);
+    const float corr = __expf(m - mn);  // 0 on the first tile (m = -inf)
+    float ts = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float p = __expf(s[e] - mn);
+      s[e] = p;
+      ts += p;
+    }
+    ts += __shfl_xor(ts, 32, 64);
+    l = l * corr + ts;
+    m = mn;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[db][e] *= corr;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      bf16x8 pb;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) pb[t] = (__bf16)s[8 * k2 + t];
+      const int j0 = 16 * k2 + 4 * h;  // keys of slots t<4: j0+t; t>=4: j0+8+t-4
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const int d = 32 * db + r32;
+        const u16x4 lo = *reinterpret_cast<const u16x4*>(&vt[wv][d][j0]);
+        const u16x4 hi = *reinterpret_cast<const u16x4*>(&vt[wv][d][j0 + 8]);
+        const u16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vv), pb, o[db],
+                                                        0, 0, 0);
+      }
+    }
+  }
+  // O^T C layout: lane column = query 32ib + r32; rows d = 32db + 8q + 4h + r (e = 4q + r)
+  const int i = 32 * ib + r32;
+  const float inv = 1.f / l;
+  const int64_t row = (int64_t)b * L + i;
+  if constexpr (MXO) {
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      float v[16];
+      float am = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        v[e] = bf16_to_f32(f32_to_bf16(o[db][e] * inv));
+        am = fmaxf(am, fabsf(v[e]));
+      }
+      am = fmaxf(am, __shfl_xor(am, 32, 64));  // the 32-column block: both halves
+      const int p = gpp::mx_exponent(am);
+      const float sc = ldexpf(1.f, -p);
+      if (i < L) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t x = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * q] * sc, v[4 * q + 1] * sc, 0u, false);
+          x = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * q + 2] * sc, v[4 * q + 3] * sc, x, true);
+          *reinterpret_cast<uint32_t*>(ctx8 + row * H + a * DH + 32 * db + 8 * q + 4 * h) = x;
+        }
+        if (h == 0) cs[gpp::mx_scale_index(row, a * DH + 32 * db, mpad)] = (unsigned char)(p + 127);
+      }
+    }
+    return;
+  }
+  if (i >= L) return;
+  unsigned short* out = ctx + row * H + a * DH;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint2 w;
+      w.x = (uint32_t)f32_to_bf16(o[db][4 * q] * inv) | ((uint32_t)f32_to_bf16(o[db][4 * q + 1] * inv) << 16);
+      w.y = (uint32_t)f32_to_bf16(o[db][4 * q + 2] * inv) |
+            ((uint32_t)f32_to_bf16(o[db][4 * q + 3] * inv) << 16);
+      *reinterpret_cast<uint2*>(out + 32 * db + 8 * q + 4 * h) = w;
+    }
+}
+
 }  // namespace enc
 }  // namespace irc
 
@@ -701,14 +883,14 @@ extern "C" int irc_layernorm_mx(const void* x, void* y, const float* gamma, cons
   return check_launch("layernorm_mx");
 }
 
-// MFMA attention (bf16 QKV, head dim 64, L <= 128) whose context
+// MFMA attention (bf16 QKV, head dim 64, any L) whose context
 // leaves as MX-fp8 (ctx8 e4m3 [B*L][H], cs E8M0 scales in the MX layout, mpad rows):
 // the fp8 out-projection's A operand (config C5).
 extern "C" int irc_attention_mx(const void* qkv, const int64_t* mask, void* ctx8, void* cs,
                                 int64_t mpad, int64_t B, int64_t L, int64_t H, int64_t heads,
                                 irc_stream_t stream) {
-  IRC_REQUIRE(heads >= 1 && H % heads == 0 && H / heads == 64 && L >= 1 && L <= 128,
-              "attention_mx: head dim 64 and L <= 128 required");
+  IRC_REQUIRE(heads >= 1 && H % heads == 0 && H / heads == 64 && L >= 1,
+              "attention_mx: head dim 64 required");
   IRC_REQUIRE(mpad >= (B * L + 255) / 256 * 256, "attention_mx: mpad must cover B*L rounded to 256");
   IRC_REQUIRE((uintptr_t)ctx8 % 16 == 0 && H % 16 == 0, "attention_mx: 16-byte aligned ctx8 rows");
   if (B == 0) return IRC_OK;
@@ -719,6 +901,13 @@ extern "C" int irc_attention_mx(const void* qkv, const int64_t* mask, void* ctx8
   auto* c8 = static_cast<unsigned char*>(ctx8);
   auto* css = static_cast<unsigned char*>(cs);
   prof_begin(st);
+  if (L > 128) {  // keys streamed (online softmax)
+    hipLaunchKernelGGL((enc::attention_flash_kernel<true>), grid, dim3(256), 0, st,
+                       (const unsigned short*)qkv, mask, (unsigned short*)nullptr, (int)B, (int)L,
+                       (int)H, (int)heads, sc, c8, css, mpad);
+    prof_end("attention", st, (double)B * L * (3 * H * 2.0 + H));
+    return check_launch("attention_mx");
+  }
   switch ((L + 31) / 32) {
 #define IRC_ATTX(NJ)                                                                             \
   case NJ:                                                                                       \
@@ -772,8 +961,8 @@ extern "C" int irc_embed_ln(int dtype, const int64_t* ids, const void* word, con
 template <typename T, int DH>
 static int attn_launch(const void* qkv, const int64_t* mask, void* ctx, int64_t B, int64_t L,
                        int64_t H, int64_t heads, hipStream_t st) {
-  const size_t lds = (size_t)2 * L * DH * 4 + (size_t)L * 4;
-  hipLaunchKernelGGL((enc::attention_kernel<T, DH>), dim3((unsigned)(B * heads)), dim3(256), lds,
+  const int64_t nqc = (L + 255) / 256;
+  hipLaunchKernelGGL((enc::attention_kernel<T, DH>), dim3((unsigned)(B * heads * nqc)), dim3(256), 0,
                      st, (const T*)qkv, mask, (T*)ctx, (int)L, (int)H, (int)heads,
                      1.0f / sqrtf((float)DH));
   return check_launch("attention_kernel");
@@ -786,15 +975,22 @@ extern "C" int irc_attention(int dtype, const void* qkv, const int64_t* mask, vo
   const int64_t dh = H / heads;
   IRC_REQUIRE(dh == 16 || dh == 32 || dh == 64 || dh == 128, "attention: head dim %lld",
               (long long)dh);
-  IRC_REQUIRE(L >= 1 && (size_t)2 * L * dh * 4 + L * 4 <= (size_t)IRC_LDS_BYTES,
-              "attention: L=%lld too long for LDS staging", (long long)L);
+  IRC_REQUIRE(L >= 1, "attention: L=%lld", (long long)L);
   if (B == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
-  if (dtype == 0 && dh == 64 && L <= 128) {  // production shape: MFMA (any L <= 128)
+  if (dtype == 0 && dh == 64) {  // production shape: MFMA, any L
     const int64_t waves = B * heads * ((L + 31) / 32);
     const dim3 grid((unsigned)((waves + 3) / 4));
     const float sc = 0.125f;  // 1/sqrt(64)
     prof_begin(st);
+    if (L > 128) {  // whole score rows no longer fit in registers: keys streamed
+      hipLaunchKernelGGL((enc::attention_flash_kernel<false>), grid, dim3(256), 0, st,
+                         (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B, (int)L,
+                         (int)H, (int)heads, sc, (unsigned char*)nullptr, (unsigned char*)nullptr,
+                         (int64_t)0);
+      prof_end("attention", st, (double)B * L * (3 * H + H) * 2.0);
+      return check_launch("attention_flash_kernel");
+    }
     switch ((L + 31) / 32) {
 #define IRC_ATTB(NJ)                                                                             \
   case NJ:                                                                                       \

@@ -280,11 +280,16 @@ __global__ void ln_bwd_final_kernel(const float* __restrict__ partial2, int ns, 
 }
 
 // ---------------------------------------------------------------- attention bwd
-// Generic (any dtype, DH <= 128, LDS-resident (b, a) tiles): one workgroup per
-// (sequence, head).  Phase 1, thread = query row i: P_i (recomputed softmax with
-// the additive key bias, as the forward), D_i = dO_i . O_i, dS_ij = P_ij (dO_i . V_j
-// - D_i), dQ_i = scale sum_j dS_ij K_j.  Phase 2, thread = key j: dK_j = scale
-// sum_i dS_ij Q_i, dV_j = sum_i P_ij dO_i.
+// Generic (any element type, DH <= 128, any L): one workgroup per (sequence, head),
+// K / V (phase 1) and Q / dO (phase 2) streamed through LDS as fp32 tiles of BKT
+// rows, the per-query statistics in dynamic LDS (3 L floats), so nothing L x L is
+// stored.  Phase 1, thread = query i: the row max m_i and sum l_i of the softmax with
+// the additive key bias (as the forward), D_i = dO_i . O_i, then P_ij, dS_ij = P_ij
+// (dO_i . V_j - D_i) and dQ_i = scale sum_j dS_ij K_j.  Phase 2, thread = key j:
+// P_ij and dS_ij recomputed from the saved statistics, dK_j = scale sum_i dS_ij Q_i,
+// dV_j = sum_i P_ij dO_i.
+constexpr int BKT = 32;
+constexpr int DH_MF = 64;
 template <typename T, int DH>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(const T* __restrict__ qkv,
                                                       const int64_t* __restrict__ mask,
@@ -293,88 +298,117 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const T* __restrict__ qkv
                                                       T* __restrict__ dqkv, int L, int H,
                                                       int heads, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* Qs = reinterpret_cast<float*>(smem);  // [L][DH]
-  float* Ks = Qs + (size_t)L * DH;
-  float* Vs = Ks + (size_t)L * DH;
-  float* Os = Vs + (size_t)L * DH;  // dO
-  float* P = Os + (size_t)L * DH;   // [L][L]
-  float* dS = P + (size_t)L * L;    // [L][L]
-  float* bias = dS + (size_t)L * L;  // [L]
+  __shared__ __attribute__((aligned(16))) float A_s[BKT][DH];  // K (phase 1) / Q (phase 2)
+  __shared__ __attribute__((aligned(16))) float B_s[BKT][DH];  // V (phase 1) / dO (phase 2)
+  __shared__ float bt[BKT];
+  float* mrow = reinterpret_cast<float*>(smem);  // [L]
+  float* irow = mrow + L;
+  float* drow = irow + L;
   const int b = blockIdx.x / heads, a = blockIdx.x % heads;
   const int64_t base = (int64_t)b * L;
   const int64_t ld3 = 3LL * H;
-  for (int e = threadIdx.x; e < L * DH; e += blockDim.x) {
-    const int j = e / DH, d = e % DH;
-    Qs[e] = ld(qkv, (base + j) * ld3 + a * DH + d);
-    Ks[e] = ld(qkv, (base + j) * ld3 + H + a * DH + d);
-    Vs[e] = ld(qkv, (base + j) * ld3 + 2 * H + a * DH + d);
-    Os[e] = ld(dctx, (base + j) * H + a * DH + d);
-  }
-  for (int j = threadIdx.x; j < L; j += blockDim.x)
-    bias[j] = (mask == nullptr || mask[base + j] != 0) ? 0.f : -1e30f;
-  __syncthreads();
-  for (int i = threadIdx.x; i < L; i += blockDim.x) {
-    const float* qi = Qs + i * DH;
-    const float* oi = Os + i * DH;
-    float* pr = P + (size_t)i * L;
-    float* sr = dS + (size_t)i * L;
-    float m = -INFINITY;
-    for (int j = 0; j < L; ++j) {
-      const float* kj = Ks + j * DH;
-      float s = 0.f;
-#pragma unroll 8
-      for (int d = 0; d < DH; ++d) s += qi[d] * kj[d];
-      s = s * scale + bias[j];
-      pr[j] = s;
-      m = fmaxf(m, s);
-    }
-    float l = 0.f;
-    for (int j = 0; j < L; ++j) {
-      const float p = __expf(pr[j] - m);
-      pr[j] = p;
-      l += p;
-    }
-    const float inv = 1.f / l;
+  const int tid = threadIdx.x;
+  // phase 1: queries
+  for (int i0 = 0; i0 < L; i0 += blockDim.x) {
+    const int i = i0 + tid;
+    const bool act = i < L;
+    const int ic = act ? i : L - 1;
+    float qv[DH], dov[DH], dq[DH];
     float Di = 0.f;
-    for (int d = 0; d < DH; ++d) Di += oi[d] * ld(ctx, (base + i) * H + a * DH + d);
-    float dq[DH];
-#pragma unroll
-    for (int d = 0; d < DH; ++d) dq[d] = 0.f;
-    for (int j = 0; j < L; ++j) {
-      const float p = pr[j] * inv;
-      pr[j] = p;
-      const float* vj = Vs + j * DH;
-      float dp = 0.f;
-#pragma unroll 8
-      for (int d = 0; d < DH; ++d) dp += oi[d] * vj[d];
-      const float ds = p * (dp - Di);
-      sr[j] = ds;
-      const float* kj = Ks + j * DH;
-#pragma unroll
-      for (int d = 0; d < DH; ++d) dq[d] += ds * kj[d];
-    }
-#pragma unroll
-    for (int d = 0; d < DH; ++d) st(dqkv, (base + i) * ld3 + a * DH + d, dq[d] * scale);
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < L; j += blockDim.x) {
-    float dk[DH], dv[DH];
-#pragma unroll
-    for (int d = 0; d < DH; ++d) dk[d] = dv[d] = 0.f;
-    for (int i = 0; i < L; ++i) {
-      const float ds = dS[(size_t)i * L + j], p = P[(size_t)i * L + j];
-      const float* qi = Qs + i * DH;
-      const float* oi = Os + i * DH;
-#pragma unroll
-      for (int d = 0; d < DH; ++d) {
-        dk[d] += ds * qi[d];
-        dv[d] += p * oi[d];
-      }
-    }
 #pragma unroll
     for (int d = 0; d < DH; ++d) {
-      st(dqkv, (base + j) * ld3 + H + a * DH + d, dk[d] * scale);
-      st(dqkv, (base + j) * ld3 + 2 * H + a * DH + d, dv[d]);
+      qv[d] = ld(qkv, (base + ic) * ld3 + a * DH + d);
+      dov[d] = ld(dctx, (base + ic) * H + a * DH + d);
+      Di += dov[d] * ld(ctx, (base + ic) * H + a * DH + d);
+      dq[d] = 0.f;
+    }
+    float m = -INFINITY, l = 0.f;
+    for (int pass = 0; pass < 3; ++pass) {  // 0: max, 1: sum, 2: dS and dQ
+      const float inv = 1.f / l;
+      for (int j0 = 0; j0 < L; j0 += BKT) {
+        const int n = min(BKT, L - j0);
+        __syncthreads();
+        for (int e = tid; e < n * DH; e += blockDim.x) {
+          const int j = e / DH, d = e % DH;
+          A_s[j][d] = ld(qkv, (base + j0 + j) * ld3 + H + a * DH + d);
+          if (pass == 2) B_s[j][d] = ld(qkv, (base + j0 + j) * ld3 + 2 * H + a * DH + d);
+        }
+        for (int j = tid; j < n; j += blockDim.x)
+          bt[j] = (mask == nullptr || mask[base + j0 + j] != 0) ? 0.f : -1e30f;
+        __syncthreads();
+        for (int t = 0; t < n; ++t) {
+          float s = 0.f;
+#pragma unroll
+          for (int d = 0; d < DH; ++d) s += qv[d] * A_s[t][d];
+          s = s * scale + bt[t];
+          if (pass == 0) {
+            m = fmaxf(m, s);
+          } else if (pass == 1) {
+            l += __expf(s - m);
+          } else {
+            const float p = __expf(s - m) * inv;
+            float dp = 0.f;
+#pragma unroll
+            for (int d = 0; d < DH; ++d) dp += dov[d] * B_s[t][d];
+            const float ds = p * (dp - Di);
+#pragma unroll
+            for (int d = 0; d < DH; ++d) dq[d] += ds * A_s[t][d];
+          }
+        }
+      }
+    }
+    if (act) {
+      mrow[i] = m;
+      irow[i] = 1.f / l;
+      drow[i] = Di;
+#pragma unroll
+      for (int d = 0; d < DH; ++d) st(dqkv, (base + i) * ld3 + a * DH + d, dq[d] * scale);
+    }
+  }
+  // phase 2: keys
+  for (int j00 = 0; j00 < L; j00 += blockDim.x) {
+    const int j = j00 + tid;
+    const bool act = j < L;
+    const int jc = act ? j : L - 1;
+    float kv[DH], vv[DH], dk[DH], dv[DH];
+#pragma unroll
+    for (int d = 0; d < DH; ++d) {
+      kv[d] = ld(qkv, (base + jc) * ld3 + H + a * DH + d);
+      vv[d] = ld(qkv, (base + jc) * ld3 + 2 * H + a * DH + d);
+      dk[d] = dv[d] = 0.f;
+    }
+    const float bj = (mask == nullptr || mask[base + jc] != 0) ? 0.f : -1e30f;
+    for (int q0 = 0; q0 < L; q0 += BKT) {
+      const int n = min(BKT, L - q0);
+      __syncthreads();  // phase 1's statistics / the previous tile's readers
+      for (int e = tid; e < n * DH; e += blockDim.x) {
+        const int r = e / DH, d = e % DH;
+        A_s[r][d] = ld(qkv, (base + q0 + r) * ld3 + a * DH + d);
+        B_s[r][d] = ld(dctx, (base + q0 + r) * H + a * DH + d);
+      }
+      __syncthreads();
+      for (int t = 0; t < n; ++t) {
+        float s = 0.f, dp = 0.f;
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          s += A_s[t][d] * kv[d];
+          dp += B_s[t][d] * vv[d];
+        }
+        const float p = __expf(s * scale + bj - mrow[q0 + t]) * irow[q0 + t];
+        const float ds = p * (dp - drow[q0 + t]);
+#pragma unroll
+        for (int d = 0; d < DH; ++d) {
+          dk[d] += ds * A_s[t][d];
+          dv[d] += p * B_s[t][d];
+        }
+      }
+    }
+    if (act) {
+#pragma unroll
+      for (int d = 0; d < DH; ++d) {
+        st(dqkv, (base + j) * ld3 + H + a * DH + d, dk[d] * scale);
+        st(dqkv, (base + j) * ld3 + 2 * H + a * DH + d, dv[d]);
+      }
     }
   }
 }
@@ -609,6 +643,227 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
   }
 }
 
+// MFMA (bf16, DH = 64, any L <= 512: the joint padding of a batch, e.g. L = 72 or 300;
+// attn_bwd_mfma_kernel takes L = 32, 64, 96, 128): one workgroup of NW waves per
+// (sequence, head), the same two phases with loops over 32-row blocks.  Dynamic LDS:
+// the key bias and the per-query statistics [Lp] (Lp = L rounded up to 32), then one
+// or two transposed [64][Lp + 4] bf16 images: K^T in phase A, Q^T and dO^T in phase B
+// (140 KB at L = 512).
+//  phase A, wave = query block: pass 1 the row max / sum (online) over key blocks,
+//    pass 2 P, dP^T = V dO^T, dS^T and dQ = scale dS K per key block;
+//  phase B, wave = key block: per query block S = Q K^T, P from the saved statistics,
+//    dP = dO V^T, dS, dV += P^T dO, dK += scale dS^T Q.
+// Rows past L: keys carry a -3e30 bias (P = 0), queries get (m, 1/l, D) = (3e30, 0, 0)
+// and zero dO (P = dS = 0); reads are clamped and nothing past L is stored.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_long_kernel(
+    const unsigned short* __restrict__ qkv, const int64_t* __restrict__ mask,
+    const unsigned short* __restrict__ ctx, const unsigned short* __restrict__ dctx,
+    unsigned short* __restrict__ dqkv, int L, int H, int heads, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Lp = (L + 31) & ~31, VP = Lp + 4, nb = Lp / 32;
+  float* mb = reinterpret_cast<float*>(smem);
+  float* mrow = mb + Lp;
+  float* irow = mrow + Lp;
+  float* drow = irow + Lp;
+  unsigned short* T0 = reinterpret_cast<unsigned short*>(drow + Lp);  // K^T (A) / Q^T (B)
+  unsigned short* T1 = T0 + 64 * VP;                                  // dO^T (B)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int h = lane >> 5, r32 = lane & 31;
+  const int b = blockIdx.x / heads, a = blockIdx.x % heads;
+  const int64_t ld3 = 3LL * H;
+  const unsigned short* base = qkv + (int64_t)b * L * ld3 + a * DH_MF;  // Q | +H: K | +2H: V
+  const unsigned short* dob = dctx + (int64_t)b * L * H + a * DH_MF;
+  const unsigned short* ob = ctx + (int64_t)b * L * H + a * DH_MF;
+  unsigned short* gb = dqkv + (int64_t)b * L * ld3 + a * DH_MF;
+  auto stage_t = [&](unsigned short* T, const unsigned short* src, int64_t ld) {
+    for (int p = threadIdx.x; p < (Lp / 2) * 8; p += 64 * NW) {
+      const int dc = p & 7, j = (p >> 3) * 2;
+      const u16x8 v0 = j < L ? *reinterpret_cast<const u16x8*>(src + (int64_t)j * ld + dc * 8) : (u16x8)0;
+      const u16x8 v1 =
+          j + 1 < L ? *reinterpret_cast<const u16x8*>(src + (int64_t)(j + 1) * ld + dc * 8) : (u16x8)0;
+#pragma unroll
+      for (int dd = 0; dd < 8; ++dd)
+        *reinterpret_cast<uint32_t*>(&T[(dc * 8 + dd) * VP + j]) = (uint32_t)v0[dd] | ((uint32_t)v1[dd] << 16);
+    }
+  };
+  auto frag = [&](const unsigned short* p) { return *reinterpret_cast<const bf16x8*>(p); };
+  stage_t(T0, base + H, ld3);
+  for (int j = threadIdx.x; j < Lp; j += 64 * NW)
+    mb[j] = j >= L ? -3e30f : ((mask == nullptr || mask[(int64_t)b * L + j] != 0) ? 0.f : -1e30f);
+  __syncthreads();
+
+  // ---------------- phase A: query blocks
+  for (int ib = wv; ib < nb; ib += NW) {
+    const int i = 32 * ib + r32, ic = min(i, L - 1);
+    bf16x8 qf[4], df[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      qf[kk] = frag(base + (int64_t)ic * ld3 + 16 * kk + 8 * h);
+      df[kk] = frag(dob + (int64_t)ic * H + 16 * kk + 8 * h);
+    }
+    float dsum = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const u16x8 o8 = *reinterpret_cast<const u16x8*>(ob + (int64_t)ic * H + 32 * h + 8 * c);
+      const u16x8 d8 = *reinterpret_cast<const u16x8*>(dob + (int64_t)ic * H + 32 * h + 8 * c);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) dsum += bf16_to_f32(o8[t]) * bf16_to_f32(d8[t]);
+    }
+    dsum += __shfl_xor(dsum, 32, 64);
+    auto scores = [&](int jb) {
+      f32x16 s = (f32x16)0.f;
+      const int jr = min(32 * jb + r32, L - 1);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(base + (int64_t)jr * ld3 + H + 16 * kk + 8 * h),
+                                                    qf[kk], s, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(&mb[32 * jb + 8 * q + 4 * h]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[4 * q + r] = s[4 * q + r] * scale + bias[r];
+      }
+      return s;
+    };
+    float m = -INFINITY, l = 0.f;
+    for (int jb = 0; jb < nb; ++jb) {
+      const f32x16 s = scores(jb);
+      float tmx = -INFINITY;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) tmx = fmaxf(tmx, s[e]);
+      tmx = fmaxf(tmx, __shfl_xor(tmx, 32, 64));
+      const float mn = fmaxf(m, tmx);
+      float ts = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) ts += __expf(s[e] - mn);
+      ts += __shfl_xor(ts, 32, 64);
+      l = l * __expf(m - mn) + ts;
+      m = mn;
+    }
+    const float inv = 1.f / l;
+    if (h == 0) {
+      mrow[i] = i < L ? m : 3e30f;
+      irow[i] = i < L ? inv : 0.f;
+      drow[i] = i < L ? dsum : 0.f;
+    }
+    f32x16 dq[2] = {(f32x16)0.f, (f32x16)0.f};
+    for (int jb = 0; jb < nb; ++jb) {
+      f32x16 s = scores(jb);
+      f32x16 dp = (f32x16)0.f;
+      const int jr = min(32 * jb + r32, L - 1);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(base + (int64_t)jr * ld3 + 2 * H + 16 * kk + 8 * h),
+                                                     df[kk], dp, 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s[e] = __expf(s[e] - m) * inv * (dp[e] - dsum);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        bf16x8 pa;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) pa[t] = (__bf16)s[8 * k2 + t];
+        const int j0 = 32 * jb + 16 * k2 + 4 * h;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const unsigned short* tr = T0 + (32 * db + r32) * VP;
+          const u16x4 lo = *reinterpret_cast<const u16x4*>(tr + j0);
+          const u16x4 hi = *reinterpret_cast<const u16x4*>(tr + j0 + 8);
+          const u16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(bf16x8, vv), dq[db], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int ii = 32 * ib + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (ii < L) gb[(int64_t)ii * ld3 + 32 * db + r32] = f32_to_bf16(dq[db][e] * scale);
+      }
+  }
+  __syncthreads();  // K^T readers done, statistics complete
+  stage_t(T0, base, ld3);
+  stage_t(T1, dob, H);
+  __syncthreads();
+
+  // ---------------- phase B: key blocks
+  for (int jb = wv; jb < nb; jb += NW) {
+    const int j = 32 * jb + r32, jc = min(j, L - 1);
+    bf16x8 kf[4], vf[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      kf[kk] = frag(base + (int64_t)jc * ld3 + H + 16 * kk + 8 * h);
+      vf[kk] = frag(base + (int64_t)jc * ld3 + 2 * H + 16 * kk + 8 * h);
+    }
+    const float bj = mb[j];
+    f32x16 dv[2] = {(f32x16)0.f, (f32x16)0.f};
+    f32x16 dk[2] = {(f32x16)0.f, (f32x16)0.f};
+    for (int ib = 0; ib < nb; ++ib) {
+      const int ir = 32 * ib + r32;
+      f32x16 sc = (f32x16)0.f, dp = (f32x16)0.f;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const bf16x8 qa = frag(base + (int64_t)min(ir, L - 1) * ld3 + 16 * kk + 8 * h);
+        const bf16x8 da = ir < L ? frag(dob + (int64_t)ir * H + 16 * kk + 8 * h) : (bf16x8)0;
+        sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[kk], sc, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], dp, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r0 = 32 * ib + 8 * q + 4 * h;
+        const f32x4 mm = *reinterpret_cast<const f32x4*>(&mrow[r0]);
+        const f32x4 iv = *reinterpret_cast<const f32x4*>(&irow[r0]);
+        const f32x4 dd = *reinterpret_cast<const f32x4*>(&drow[r0]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int e = 4 * q + r;
+          const float p = __expf(sc[e] * scale + bj - mm[r]) * iv[r];
+          sc[e] = p;
+          dp[e] = p * (dp[e] - dd[r]);
+        }
+      }
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        bf16x8 pa, sa;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          pa[t] = (__bf16)sc[8 * k2 + t];
+          sa[t] = (__bf16)dp[8 * k2 + t];
+        }
+        const int i0 = 32 * ib + 16 * k2 + 4 * h;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const int d = 32 * db + r32;
+          const u16x4 olo = *reinterpret_cast<const u16x4*>(T1 + d * VP + i0);
+          const u16x4 ohi = *reinterpret_cast<const u16x4*>(T1 + d * VP + i0 + 8);
+          const u16x8 ov = {olo[0], olo[1], olo[2], olo[3], ohi[0], ohi[1], ohi[2], ohi[3]};
+          dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(bf16x8, ov), dv[db], 0, 0, 0);
+          const u16x4 qlo = *reinterpret_cast<const u16x4*>(T0 + d * VP + i0);
+          const u16x4 qhi = *reinterpret_cast<const u16x4*>(T0 + d * VP + i0 + 8);
+          const u16x8 qv = {qlo[0], qlo[1], qlo[2], qlo[3], qhi[0], qhi[1], qhi[2], qhi[3]};
+          dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, __builtin_bit_cast(bf16x8, qv), dk[db], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int jj = 32 * jb + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (jj < L) {
+          gb[(int64_t)jj * ld3 + H + 32 * db + r32] = f32_to_bf16(dk[db][e] * scale);
+          gb[(int64_t)jj * ld3 + 2 * H + 32 * db + r32] = f32_to_bf16(dv[db][e]);
+        }
+      }
+  }
+}
+
+static size_t attn_bwd_long_lds(int64_t L) {
+  const int64_t Lp = (L + 31) & ~31LL;
+  return (size_t)(4 * Lp * 4 + 2 * 64 * (Lp + 4) * 2);
+}
+
 // ---------------------------------------------------------------- embedding bwd
 // dword[ids[r]] += dx[r] (fp32 atomics; rows holding pad_id skipped: nn.Embedding's
 // padding_idx row never receives a gradient).  One wave per row.
@@ -756,7 +1011,7 @@ template <typename T, int DH>
 static int attn_bwd_launch(const void* qkv, const int64_t* mask, const void* ctx, const void* dctx,
                            void* dqkv, int64_t B, int64_t L, int64_t H, int64_t heads,
                            hipStream_t st) {
-  const size_t lds = (size_t)4 * L * DH * 4 + (size_t)2 * L * L * 4 + (size_t)L * 4;
+  const size_t lds = (size_t)3 * L * 4;  // per-query statistics (the tiles are static)
   hipLaunchKernelGGL((encb::attn_bwd_kernel<T, DH>), dim3((unsigned)(B * heads)), dim3(256), lds,
                      st, (const T*)qkv, mask, (const T*)ctx, (const T*)dctx, (T*)dqkv, (int)L,
                      (int)H, (int)heads, 1.0f / sqrtf((float)DH));
@@ -774,7 +1029,23 @@ extern "C" int irc_attention_bwd(int dtype, const void* qkv, const int64_t* mask
   if (B == 0 || L == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
   using u16 = unsigned short;
-  if (dtype == 0 && dh == 64 && L % 32 == 0 && L <= 128) {
+  if (dtype == 0 && dh == 64 && (L % 32 != 0 || L > 128)) {
+    IRC_REQUIRE(L <= 512, "attention_bwd: L=%lld > 512 (BERT's position table)", (long long)L);
+    const size_t lds = encb::attn_bwd_long_lds(L);
+    const dim3 grid((unsigned)(B * heads));
+    prof_begin(st);
+    if (L <= 128)
+      hipLaunchKernelGGL(encb::attn_bwd_long_kernel<4>, grid, dim3(256), lds, st, (const u16*)qkv,
+                         mask, (const u16*)ctx, (const u16*)dctx, (u16*)dqkv, (int)L, (int)H,
+                         (int)heads, 0.125f);
+    else
+      hipLaunchKernelGGL(encb::attn_bwd_long_kernel<8>, grid, dim3(512), lds, st, (const u16*)qkv,
+                         mask, (const u16*)ctx, (const u16*)dctx, (u16*)dqkv, (int)L, (int)H,
+                         (int)heads, 0.125f);
+    prof_end("attention_bwd", st, (double)B * L * (3 * H + 2 * H + 3 * H) * 2.0);
+    return check_launch("attention_bwd_long_kernel");
+  }
+  if (dtype == 0 && dh == 64) {  // L = 32, 64, 96, 128
     const float sc = 0.125f;
     const dim3 grid((unsigned)(B * heads));
     prof_begin(st);
@@ -796,10 +1067,8 @@ extern "C" int irc_attention_bwd(int dtype, const void* qkv, const int64_t* mask
     prof_end("attention_bwd", st, (double)B * L * (3 * H + 2 * H + 3 * H) * 2.0);
     return check_launch("attention_bwd_mfma_kernel");
   }
-  const size_t lds = (size_t)4 * L * dh * 4 + (size_t)2 * L * L * 4 + (size_t)L * 4;
-  IRC_REQUIRE(lds <= (size_t)IRC_LDS_BYTES,
-              "attention_bwd: L=%lld, head dim %lld too large for the LDS-resident kernel",
-              (long long)L, (long long)dh);
+  IRC_REQUIRE((size_t)3 * L * 4 <= (size_t)IRC_LDS_BYTES / 2,
+              "attention_bwd: L=%lld too long for the per-query statistics", (long long)L);
 #define IRC_ATTB(DH)                                                                          \
   if (dh == DH)                                                                               \
     return dtype == 0                                                                         \

@@ -28,13 +28,18 @@ def synthetic_vocab_file(vocab_size: int = 30522) -> str:
     return path
 
 
+# bert-base-uncased's tokenizer_config: `truncation=True` (contrastive_module.py:38,97)
+# cuts at model_max_length, so a bare vocab file gets the same 512 limit
+MODEL_MAX_LENGTH = 512
+
+
 def load_tokenizer(name_or_path: str | None, vocab_size: int = 30522):
     from transformers import BertTokenizer
 
     if name_or_path and os.path.isdir(name_or_path):
         return BertTokenizer.from_pretrained(name_or_path, local_files_only=True)
     if name_or_path and os.path.isfile(name_or_path):
-        return BertTokenizer(name_or_path)
+        return BertTokenizer(name_or_path, model_max_length=MODEL_MAX_LENGTH)
     warnings.warn("no local BERT vocab given: using a synthetic offline vocabulary "
                   f"({vocab_size} tokens)", stacklevel=2)
-    return BertTokenizer(synthetic_vocab_file(vocab_size))
+    return BertTokenizer(synthetic_vocab_file(vocab_size), model_max_length=MODEL_MAX_LENGTH)

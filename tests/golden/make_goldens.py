@@ -70,9 +70,10 @@ def _write_vocab(path, vocab_size):
         f.write("\n".join(toks) + "\n")
 
 
-def _install_bert_shims(vocab_path, bert_kw):
+def _install_bert_shims(vocab_path, bert_kw, tok_kw=None):
     from transformers import BertConfig, BertModel, BertTokenizer
     import src.contrastor.contrastive_module as cm
+    tok_kw = tok_kw or {}
 
     class _Model:
         @staticmethod
@@ -83,7 +84,7 @@ def _install_bert_shims(vocab_path, bert_kw):
     class _Tok:
         @staticmethod
         def from_pretrained(name, *a, **k):
-            return BertTokenizer(vocab_path)
+            return BertTokenizer(vocab_path, **tok_kw)
 
     cm.BertModel = _Model
     cm.BertTokenizer = _Tok
@@ -339,6 +340,59 @@ def gen_bert(out, tmp):
     print("bert:", hs.shape)
 
 
+LONG_BERT = dict(vocab_size=300, hidden_size=128, num_hidden_layers=2, num_attention_heads=2,
+                 intermediate_size=256, max_position_embeddings=512)
+
+
+def gen_bert_long(out, tmp):
+    """The reference's own bert_extract and ctx2vec (contrastive_module.py:36-41,
+    96-112) on sentences long enough that the joint padding reaches the 512-token
+    truncation: d1 + d2 holds a 600-word sentence, so the batch is cut to L = 512;
+    ctx2vec(d2) pads to its longest, 500 words + [CLS] / [SEP] = 502.  The tokenizer
+    carries bert-base-uncased's model_max_length (512), which `truncation=True` reads.
+    Local 2-layer config with head dim 64 (the MFMA attention path) and
+    max_position_embeddings = 512; a 2-layer BiLSTM head 128 -> 16 -> 8."""
+    from src.model import LSTM
+    from src.contrastor.contrastive_module import RetrievalModelWrapper
+    from src.contrastor.contrastive_loss import NCELoss
+
+    vocab = os.path.join(tmp, "vocab_long.txt")
+    _write_vocab(vocab, LONG_BERT["vocab_size"])
+    _install_bert_shims(vocab, LONG_BERT, {"model_max_length": 512})
+    torch.manual_seed(3)
+    enc = LSTM(_lstm_cfg(128, 16, 2, 8))
+    lc = {"temperature": 0.05, "use_momentum": True, "momentum": 0.9, "use_queue": True,
+          "queue_size": 12, "dim": 8}
+    model = RetrievalModelWrapper(enc, NCELoss(lc), lc)
+    rng = np.random.default_rng(512)
+
+    def sent(n):
+        return " ".join(f"w{i}" for i in rng.integers(0, LONG_BERT["vocab_size"] - 5, n))
+
+    d1 = [sent(600), sent(3), sent(40)]
+    d2 = [sent(250), sent(500), sent(1)]
+    t = model.bert_tokenizer(d1 + d2, padding=True, truncation=True, return_tensors="pt")
+    a, p = model.bert_extract(d1, d2, "cpu")
+    with torch.no_grad():
+        c2v = model.ctx2vec(d2, "cpu")
+    tc = model.bert_tokenizer(d2, padding=True, truncation=True, return_tensors="pt")
+    res = {"d1": np.array(d1), "d2": np.array(d2), "input_ids": _np(t["input_ids"]),
+           "attention_mask": _np(t["attention_mask"]), "anchor_hs": _np(a), "positive_hs": _np(p),
+           "ctx_input_ids": _np(tc["input_ids"]), "ctx_attention_mask": _np(tc["attention_mask"]),
+           "ctx2vec": _np(c2v),
+           "cfg": np.array([LONG_BERT[k] for k in ("vocab_size", "hidden_size",
+                                                   "num_hidden_layers", "num_attention_heads",
+                                                   "intermediate_size",
+                                                   "max_position_embeddings")]),
+           "head_dims": np.array([128, 16, 2, 8])}
+    for kname, v in model.bert_model.state_dict().items():
+        res["w_" + kname] = _np(v)
+    for kname, v in model.encoder_q.state_dict().items():
+        res["h_" + kname] = _np(v)
+    np.savez_compressed(os.path.join(out, "bert_long.npz"), **res)
+    print("bert_long:", tuple(t["input_ids"].shape), tuple(tc["input_ids"].shape))
+
+
 def _ref_ranker(docs_f64):
     """The reference's TfidfDocRanker.closest_docs ranking over a dense corpus.
 
@@ -526,6 +580,7 @@ def main():
         gen_lstm_init(HERE)
         gen_seq2vec(HERE, tmp)
         gen_bert(HERE, tmp)
+        gen_bert_long(HERE, tmp)
         gen_scan(HERE)
         gen_train_traj(HERE, tmp)
         gen_train_traj_nomom(HERE, tmp)

@@ -2,9 +2,12 @@
 in eval mode (modeling_bert, reached from contrastive_module.py:39):
 softmax(Q K^T / sqrt(dh) + (1 - mask) * finfo.min) V over the fused [B*L, 3H] QKV rows.
 
-bf16 with head dim 64 and L <= 128 runs the MFMA kernel (L not a multiple of 32,
-e.g. a joint-padded batch's L = 72: clamped key rows with a pad bias, zero V rows,
-query rows past L never stored); other shapes / fp32 run the VALU kernel.  Tolerance: bf16 inputs and bf16-rounded
+bf16 with head dim 64 runs an MFMA kernel at every L the reference's tokenizer can
+produce (joint padding up to 512, contrastive_module.py:38): whole score rows in
+registers for L <= 128 (L not a multiple of 32, e.g. a joint-padded batch's L = 72:
+clamped key rows with a pad bias, zero V rows, query rows past L never stored), keys
+streamed with an online softmax above; other shapes / fp32 run the key-tiled VALU
+kernel, also at any L.  Tolerance: bf16 inputs and bf16-rounded
 probabilities -> 2e-2 absolute on O(1) outputs; fp32 -> 1e-5.
 """
 import pytest
@@ -34,7 +37,8 @@ def _case(B, L, H, heads, dtype, seed, all_masked_row=False):
     return qkv, mask
 
 
-@pytest.mark.parametrize("L", [1, 17, 32, 40, 64, 72, 96, 100, 128])
+@pytest.mark.parametrize("L", [1, 17, 32, 40, 64, 72, 93, 96, 100, 128,
+                               129, 160, 200, 317, 318, 400, 512])
 def test_attention_mfma_bf16(gpu, L):
     from irc_amd import ops
 
@@ -49,7 +53,10 @@ def test_attention_mfma_bf16(gpu, L):
 @pytest.mark.parametrize("dtype,L,H,heads", [(torch.float32, 64, 768, 12),
                                              (torch.bfloat16, 40, 768, 12),
                                              (torch.bfloat16, 64, 256, 8),
-                                             (torch.float32, 17, 128, 2)])
+                                             (torch.float32, 17, 128, 2),
+                                             (torch.float32, 300, 768, 12),
+                                             (torch.float32, 512, 32, 2),
+                                             (torch.bfloat16, 257, 256, 8)])
 def test_attention_valu_shapes(gpu, dtype, L, H, heads):
     from irc_amd import ops
 
@@ -59,3 +66,20 @@ def test_attention_valu_shapes(gpu, dtype, L, H, heads):
     ref = _ref(qkv, mask, B, L, H, heads)
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     assert (out.float().cpu() - ref).abs().max().item() <= tol
+
+
+def test_attention_long_rows_all_masked_and_single_key(gpu):
+    """L = 512 with an all-masked row (uniform average over all 512 keys, HF's finfo.min
+    bias) and a row whose only unmasked key is the last one (online-softmax rescale
+    across 16 key tiles)."""
+    from irc_amd import ops
+
+    B, L, H, heads = 3, 512, 768, 12
+    g = torch.Generator().manual_seed(512)
+    qkv = (torch.randn((B * L, 3 * H), generator=g) * 4).bfloat16()
+    mask = torch.ones(B, L, dtype=torch.int64)
+    mask[1] = 0
+    mask[2, :-1] = 0
+    out = ops.attention(qkv.to(gpu), mask.to(gpu), B, L, H, heads)
+    ref = _ref(qkv, mask, B, L, H, heads)
+    assert (out.float().cpu() - ref).abs().max().item() <= 2e-2

@@ -47,7 +47,17 @@ def _attn_ref(qkv, mask, B, L, H, heads):
                                              (torch.bfloat16, 128, 256, 4),
                                              (torch.float32, 64, 128, 2),
                                              (torch.float32, 24, 96, 3),
-                                             (torch.bfloat16, 40, 128, 2)])
+                                             (torch.bfloat16, 40, 128, 2),
+                                             (torch.bfloat16, 93, 768, 12),
+                                             (torch.bfloat16, 100, 256, 4),
+                                             (torch.bfloat16, 129, 256, 4),
+                                             (torch.bfloat16, 200, 256, 4),
+                                             (torch.bfloat16, 317, 128, 2),
+                                             (torch.bfloat16, 318, 128, 2),
+                                             (torch.bfloat16, 400, 128, 2),
+                                             (torch.bfloat16, 512, 768, 12),
+                                             (torch.float32, 300, 128, 2),
+                                             (torch.float32, 512, 32, 2)])
 def test_attention_bwd(gpu, dtype, L, H, heads):
     from irc_amd import ops
 
@@ -189,9 +199,16 @@ def _encoder_grads(gpu, precision, cfg, B, L, seed):
 
 
 @pytest.mark.parametrize("precision,L,tol", [("fp32", 32, 1e-4), ("fp32", 20, 1e-4),
-                                             ("bf16", 64, 3e-2), ("bf16", 32, 3e-2)])
+                                             ("bf16", 64, 3e-2), ("bf16", 32, 3e-2),
+                                             ("bf16", 93, 3e-2), ("bf16", 100, 3e-2),
+                                             ("bf16", 129, 3e-2), ("bf16", 318, 3e-2),
+                                             ("bf16", 512, 3e-2), ("fp32", 200, 1e-4)])
 def test_bert_encoder_grads(gpu, precision, L, tol):
-    cfg = _tiny_cfg()
+    """Whole-encoder gradients at the lengths a joint-padded batch can take (the
+    reference pads to the longest of 2B sentences and truncates at 512,
+    contrastive_module.py:38): L > 128 runs the streamed attention forward and the
+    block-looped attention backward."""
+    cfg = _tiny_cfg(maxpos=max(64, L))
     enc, emb, ref, P = _encoder_grads(gpu, precision, cfg, B=6, L=L, seed=L)
     emb_tol = 1e-5 if precision == "fp32" else 2e-2
     assert (emb.cpu() - ref.detach()).abs().max().item() <= emb_tol

@@ -184,7 +184,7 @@ def test_layernorm_mx_equals_quantised_layernorm(gpu, H):
     assert torch.equal(ym.codes, ref.codes) and torch.equal(ym.scales, ref.scales)
 
 
-@pytest.mark.parametrize("L", [64, 72, 17])
+@pytest.mark.parametrize("L", [64, 72, 17, 129, 200, 512])
 def test_attention_mx_equals_quantised_attention(gpu, L):
     from irc_amd import ops
 

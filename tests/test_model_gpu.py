@@ -54,6 +54,57 @@ def test_bert_tiny_bf16(gpu):
     np.testing.assert_allclose(out.float().cpu().numpy(), g["last_hidden_state"], atol=6e-2)
 
 
+@pytest.mark.parametrize("mode,atol", [("fp32", 3e-4), ("bf16", 6e-2)])
+def test_bert_long_512_matches_reference(gpu, mode, atol):
+    """The reference's own bert_extract at the 512-token truncation
+    (tests/golden/bert_long.npz, a 600-word sentence in the joint batch): L = 512
+    runs the streamed MFMA attention (bf16) / the key-tiled kernel (fp32)."""
+    from irc_amd.precision import get_precision, set_precision
+
+    g = load_golden("bert_long.npz")
+    old = get_precision()
+    set_precision(mode)
+    try:
+        m = _bert_from_golden(g, gpu)
+        out = m.encode(torch.from_numpy(g["input_ids"]).to(gpu),
+                       torch.from_numpy(g["attention_mask"]).to(gpu))
+    finally:
+        set_precision(old)
+    ref = np.concatenate([g["anchor_hs"], g["positive_hs"]])
+    kw = {"rtol": 1e-4} if mode == "fp32" else {}
+    np.testing.assert_allclose(out.float().cpu().numpy(), ref, atol=atol, **kw)
+
+
+def test_ctx2vec_long_matches_reference(gpu):
+    """The reference's ctx2vec at L = 502 (bert_long.npz): GPU WordPiece + joint
+    padding token-exact against the reference tokenizer, then BERT -> BiLSTM head ->
+    mean over all 502 positions (PAD included) -> L2 norm, bf16 (tolerance 2e-2 on
+    unit vectors)."""
+    from irc_amd.lstm_head import LSTMHead, seq2vec
+    from irc_amd.tokenizer import load_tokenizer, synthetic_vocab_file
+    from irc_amd.wordpiece import GpuWordPiece
+
+    g = load_golden("bert_long.npz")
+    vocab = int(g["cfg"][0])
+    wp = GpuWordPiece(load_tokenizer(synthetic_vocab_file(vocab), vocab), gpu)
+    ids, mask = wp(list(g["d2"]))
+    assert torch.equal(ids.cpu(), torch.from_numpy(g["ctx_input_ids"]))
+    assert torch.equal(mask.cpu(), torch.from_numpy(g["ctx_attention_mask"]))
+    ids_j, mask_j = wp(list(g["d1"]) + list(g["d2"]))
+    assert torch.equal(ids_j.cpu(), torch.from_numpy(g["input_ids"]))
+    m = _bert_from_golden(g, gpu)
+    inp, hid, layers, outd = (int(x) for x in g["head_dims"])
+    h = LSTMHead({"model": {"LSTM": {"num_layers": layers, "bidirectional": True,
+                                     "input_size": inp, "hidden_size": hid,
+                                     "output_size": outd, "activation": "Identity"}}},
+                 init=False)
+    h.load_state_dict({k[2:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("h_")})
+    h = h.to(gpu)
+    with torch.no_grad():
+        emb = seq2vec(h, m.encode(ids, mask), grad=False)
+    assert (emb.float().cpu() - torch.from_numpy(g["ctx2vec"])).abs().max().item() <= 2e-2
+
+
 def _head_from_golden(g, tag, dev):
     from irc_amd.lstm_head import LSTMHead
 

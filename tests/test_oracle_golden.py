@@ -65,6 +65,32 @@ def test_bert_forward():
     np.testing.assert_allclose(out, g["last_hidden_state"], rtol=1e-4, atol=1e-4)
 
 
+def test_bert_long_matches_reference_at_512():
+    """The reference's bert_extract / ctx2vec at the 512-token truncation
+    (tests/golden/bert_long.npz): the oracle reproduces both, and the host tokenizer
+    (irc_amd.tokenizer, bert-base-uncased's model_max_length) cuts the joint batch at
+    the same 512 tokens."""
+    g = load_golden("bert_long.npz")
+    w = {k[2:]: v for k, v in g.items() if k.startswith("w_")}
+    vocab, hid, nl, nh, inter, maxpos = (int(x) for x in g["cfg"])
+    ids, mask = g["input_ids"], g["attention_mask"]
+    assert ids.shape == (6, 512) and maxpos == 512
+    out = O.bert_forward(ids, mask, w, nl, nh)
+    np.testing.assert_allclose(out, np.concatenate([g["anchor_hs"], g["positive_hs"]]),
+                               rtol=1e-4, atol=1e-4)
+    hidden = O.bert_forward(g["ctx_input_ids"], g["ctx_attention_mask"], w, nl, nh)
+    p = {k[2:]: v.astype(np.float64) for k, v in g.items() if k.startswith("h_")}
+    emb, _ = O.seq2vec(hidden.astype(np.float64), p, int(g["head_dims"][2]))
+    np.testing.assert_allclose(emb, g["ctx2vec"], rtol=1e-4, atol=1e-5)
+
+    from irc_amd.tokenizer import load_tokenizer, synthetic_vocab_file
+
+    tok = load_tokenizer(synthetic_vocab_file(vocab), vocab)
+    t = tok(list(g["d1"]) + list(g["d2"]), padding=True, truncation=True, return_tensors="np")
+    np.testing.assert_array_equal(t["input_ids"], ids)
+    np.testing.assert_array_equal(t["attention_mask"], mask)
+
+
 def test_bert_ref_matches_golden():
     """The torch fp32 BERT used as the trainable encoder's gradient reference
     (tests/bert_ref.py) reproduces the reference's own HF last_hidden_state."""

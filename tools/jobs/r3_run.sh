@@ -1,5 +1,5 @@
 # Round-3 GPU job: full -m gpu suite (no -x: every failure listed), smoke, bench.
-# usage: tools/r3_run.sh TAG [pytest args...]
+# usage: tools/jobs/r3_run.sh TAG [pytest args...]
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 tag=$1; shift

@@ -1,5 +1,5 @@
 # Round-3 GPU job: selected -m gpu tests (no -x), then optional bench parts.
-# usage: tools/r3_sel.sh TAG "pytest targets" [bench parts...]
+# usage: tools/jobs/r3_sel.sh TAG "pytest targets" [bench parts...]
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 tag=$1; targets=$2; shift 2

@@ -1,7 +1,7 @@
 """HBM traffic per GEMM shape against its algorithmic bytes (the
 trainable-BERT step's GEMM families, fwd / dX / dW, one shape per family member).
 
-tools/r4_h.sh runs `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes of
+tools/jobs/r4_h.sh runs `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes of
 `tools/gemm_bench.py --only <shape>` into <root>/<shape>_<COUNTER>/; this sums the
 counter over the GEMM dispatches (the split-K reduce included), divides by the number of
 GEMM calls, and prints HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 as
