@@ -355,6 +355,24 @@ int irc_adam_step_bf16(float* p, const float* g, float* m, float* v, int64_t n, 
                        void* p_bf16, irc_stream_t stream);
 int irc_momentum_update_bf16(float* pk, const float* pq, int64_t n, float mom, void* pk_bf16,
                              irc_stream_t stream);
+/* SGD step (the reference's --opt sgd: torch.optim.SGD(lr, momentum, weight_decay),
+ * src/model.py:45-51), clip coefficient / gate read from coef (NULL: none) as in
+ * irc_adam_step: d = g * coef[1] + weight_decay * p; buf = first_step ? d :
+ * momentum * buf + d; p -= lr * buf.  p_bf16 (NULL: none): bf16 shadow of p. */
+int irc_sgd_step(float* p, const float* g, float* buf, int64_t n, const float* coef, float lr,
+                 float momentum, float weight_decay, int first_step, void* p_bf16,
+                 irc_stream_t stream);
+/* The head's output activation (src/model.py:23-26, eval(f"nn.{act}()") with torch's
+ * default arguments): y = act(u) elementwise; the backward scales g by act'(u) in
+ * place.  fp32. */
+enum {
+  IRC_ACT_IDENTITY = 0, IRC_ACT_RELU, IRC_ACT_RELU6, IRC_ACT_LEAKY_RELU, IRC_ACT_ELU,
+  IRC_ACT_CELU, IRC_ACT_SELU, IRC_ACT_GELU, IRC_ACT_SILU, IRC_ACT_MISH, IRC_ACT_SIGMOID,
+  IRC_ACT_TANH, IRC_ACT_SOFTPLUS, IRC_ACT_SOFTSIGN, IRC_ACT_HARDTANH, IRC_ACT_HARDSIGMOID,
+  IRC_ACT_HARDSWISH, IRC_ACT_TANHSHRINK, IRC_ACT_COUNT
+};
+int irc_activation(int kind, const float* u, float* y, int64_t n, irc_stream_t stream);
+int irc_activation_bwd(int kind, const float* u, float* g, int64_t n, irc_stream_t stream);
 /* Fault gate of a training step (no host sync; replaces nothing in the reference,
  * whose cuDNN LSTM cannot time out): coef[2] = 1 when *fault_a or *fault_b (uint32
  * sticky timeout words of irc_lstm_coop_fault; either may be NULL) is set, else 0.

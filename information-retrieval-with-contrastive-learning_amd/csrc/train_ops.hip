@@ -215,6 +215,112 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
   if (pb) pb[i] = f32_to_bf16(np);
 }
 
+// SGD (torch.optim.SGD, dampening 0, nesterov False; the reference's --opt sgd,
+// model.py:45-51) with the clip coefficient applied to the gradient:
+// d = g * coef[1] + wd * p; buf = first ? d : mom * buf + d; p -= lr * buf.
+// pb (may be null): bf16 shadow of the updated parameters.
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                           float* __restrict__ buf, int64_t n, const float* __restrict__ coef,
+                           float lr, float mom, float wd, int first, unsigned short* __restrict__ pb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (coef && coef[2] != 0.f) return;  // gated: a recurrence timed out in this step
+  const float c = coef ? coef[1] : 1.f;
+  const float pi = p[i];
+  const float d = g[i] * c + wd * pi;
+  const float b = first ? d : buf[i] * mom + d;
+  buf[i] = b;
+  const float np = pi - lr * b;
+  p[i] = np;
+  if (pb) pb[i] = f32_to_bf16(np);
+}
+
+// The head's output activation (model.py:23-26: nn.Sequential(Linear, eval(f"nn.{act}()")),
+// torch's default constructor arguments).  Kind codes: include/irc.h IRC_ACT_*.
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float softplus1(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+constexpr float SELU_SCALE = 1.0507009873554804934193349852946f;
+constexpr float SELU_ALPHA = 1.6732632423543772848170429916717f;
+
+__device__ __forceinline__ float act_fwd(int k, float u) {
+  switch (k) {
+    case IRC_ACT_RELU: return u > 0.f ? u : 0.f;
+    case IRC_ACT_RELU6: return fminf(fmaxf(u, 0.f), 6.f);
+    case IRC_ACT_LEAKY_RELU: return u > 0.f ? u : 0.01f * u;
+    case IRC_ACT_ELU:
+    case IRC_ACT_CELU: return u > 0.f ? u : expm1f(u);
+    case IRC_ACT_SELU: return SELU_SCALE * (u > 0.f ? u : SELU_ALPHA * expm1f(u));
+    case IRC_ACT_GELU: return 0.5f * u * (1.f + erff(u * 0.70710678118654752f));
+    case IRC_ACT_SILU: return u * sigm(u);
+    case IRC_ACT_MISH: return u * tanhf(softplus1(u));
+    case IRC_ACT_SIGMOID: return sigm(u);
+    case IRC_ACT_TANH: return tanhf(u);
+    case IRC_ACT_SOFTPLUS: return softplus1(u);
+    case IRC_ACT_SOFTSIGN: return u / (1.f + fabsf(u));
+    case IRC_ACT_HARDTANH: return fminf(fmaxf(u, -1.f), 1.f);
+    case IRC_ACT_HARDSIGMOID: return fminf(fmaxf(u + 3.f, 0.f), 6.f) / 6.f;
+    case IRC_ACT_HARDSWISH: return u * fminf(fmaxf(u + 3.f, 0.f), 6.f) / 6.f;
+    case IRC_ACT_TANHSHRINK: return u - tanhf(u);
+    default: return u;  // IRC_ACT_IDENTITY
+  }
+}
+
+// d act / d u at u (torch autograd's conventions at the kinks)
+__device__ __forceinline__ float act_grad(int k, float u) {
+  switch (k) {
+    case IRC_ACT_RELU: return u > 0.f ? 1.f : 0.f;
+    case IRC_ACT_RELU6: return (u > 0.f && u < 6.f) ? 1.f : 0.f;
+    case IRC_ACT_LEAKY_RELU: return u > 0.f ? 1.f : 0.01f;
+    case IRC_ACT_ELU:
+    case IRC_ACT_CELU: return u > 0.f ? 1.f : expf(u);
+    case IRC_ACT_SELU: return u > 0.f ? SELU_SCALE : SELU_SCALE * SELU_ALPHA * expf(u);
+    case IRC_ACT_GELU:
+      return 0.5f * (1.f + erff(u * 0.70710678118654752f)) +
+             u * 0.39894228040143268f * expf(-0.5f * u * u);
+    case IRC_ACT_SILU: {
+      const float s = sigm(u);
+      return s * (1.f + u * (1.f - s));
+    }
+    case IRC_ACT_MISH: {
+      const float t = tanhf(softplus1(u));
+      return t + u * (1.f - t * t) * sigm(u);
+    }
+    case IRC_ACT_SIGMOID: {
+      const float s = sigm(u);
+      return s * (1.f - s);
+    }
+    case IRC_ACT_TANH: {
+      const float t = tanhf(u);
+      return 1.f - t * t;
+    }
+    case IRC_ACT_SOFTPLUS: return u > 20.f ? 1.f : sigm(u);
+    case IRC_ACT_SOFTSIGN: {
+      const float a = 1.f + fabsf(u);
+      return 1.f / (a * a);
+    }
+    case IRC_ACT_HARDTANH: return (u > -1.f && u < 1.f) ? 1.f : 0.f;
+    case IRC_ACT_HARDSIGMOID: return (u > -3.f && u < 3.f) ? 1.f / 6.f : 0.f;
+    case IRC_ACT_HARDSWISH: return u < -3.f ? 0.f : (u <= 3.f ? u / 3.f + 0.5f : 1.f);
+    case IRC_ACT_TANHSHRINK: {
+      const float t = tanhf(u);
+      return t * t;
+    }
+    default: return 1.f;
+  }
+}
+
+__global__ void act_fwd_kernel(int kind, const float* __restrict__ u, float* __restrict__ y,
+                               int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = act_fwd(kind, u[i]);
+}
+
+__global__ void act_bwd_kernel(int kind, const float* __restrict__ u, float* __restrict__ g,
+                               int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) g[i] *= act_grad(kind, u[i]);
+}
+
 __global__ void momentum_kernel(float* __restrict__ pk, const float* __restrict__ pq, int64_t n,
                                 float mom, unsigned short* __restrict__ pb,
                                 const float* __restrict__ gate) {
@@ -551,6 +657,30 @@ extern "C" int irc_momentum_update_bf16(float* pk, const float* pq, int64_t n, f
   hipLaunchKernelGGL(momentum_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), pk, pq, n,
                      mom, (unsigned short*)pk_bf16, nullptr);
   return check_launch("momentum_bf16");
+}
+
+extern "C" int irc_sgd_step(float* p, const float* g, float* buf, int64_t n, const float* coef,
+                            float lr, float momentum, float weight_decay, int first_step,
+                            void* p_bf16, irc_stream_t stream) {
+  if (n == 0) return IRC_OK;
+  hipLaunchKernelGGL(sgd_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), p, g, buf, n,
+                     coef, lr, momentum, weight_decay, first_step, (unsigned short*)p_bf16);
+  return check_launch("sgd");
+}
+
+extern "C" int irc_activation(int kind, const float* u, float* y, int64_t n, irc_stream_t stream) {
+  IRC_REQUIRE(kind >= 0 && kind < IRC_ACT_COUNT, "activation: kind %d", kind);
+  if (n == 0) return IRC_OK;
+  hipLaunchKernelGGL(act_fwd_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), kind, u, y, n);
+  return check_launch("activation");
+}
+
+extern "C" int irc_activation_bwd(int kind, const float* u, float* g, int64_t n,
+                                  irc_stream_t stream) {
+  IRC_REQUIRE(kind >= 0 && kind < IRC_ACT_COUNT, "activation_bwd: kind %d", kind);
+  if (n == 0) return IRC_OK;
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(nblk(n)), dim3(256), 0, as_stream(stream), kind, u, g, n);
+  return check_launch("activation_bwd");
 }
 
 extern "C" int irc_momentum_update_gated(float* pk, const float* pq, int64_t n, float mom,

@@ -91,6 +91,9 @@ SIGNATURES = {
     "irc_axpby": (I32, [P, P, P, F32, F32, I64, P]),
     "irc_sum": (I32, [P, I64, F32, P, P, P]),
     "irc_grad_norm_clip": (I32, [P, I64, F32, P, P, P]),
+    "irc_sgd_step": (I32, [P, P, P, I64, P, F32, F32, F32, I32, P, P]),
+    "irc_activation": (I32, [I32, P, P, I64, P]),
+    "irc_activation_bwd": (I32, [I32, P, P, I64, P]),
     "irc_adam_step": (I32, [P, P, P, P, I64, P, F32, F32, F32, F32, F32, P]),
     "irc_fault_gate": (I32, [P, P, P, P]),
     "irc_momentum_update_gated": (I32, [P, P, I64, F32, P, P, P]),

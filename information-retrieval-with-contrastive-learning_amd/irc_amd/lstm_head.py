@@ -89,8 +89,11 @@ class LSTMHead(nn.Module):
         self.bidirectional = bool(c["bidirectional"])
         self.output_size = int(c["output_size"])
         act = c.get("activation", "Identity")
-        if act != "Identity":
-            raise NotImplementedError(f"activation {act!r}: the reference config uses Identity")
+        if act not in ops.ACTIVATIONS:
+            raise ValueError(f"activation {act!r}: supported nn activations are "
+                             f"{sorted(ops.ACTIVATIONS)}")
+        self.activation = act
+        self.act_kind = ops.ACTIVATIONS[act]
         self.ndir = 2 if self.bidirectional else 1
         self.specs = lstm_param_specs(self.input_size, self.hidden, self.num_layers,
                                       self.bidirectional, self.output_size)
@@ -241,10 +244,18 @@ class LSTMHead(nn.Module):
         for l in range(self.num_layers):
             x, st = self._layer_fwd(l, x, B, L, dt, save)
             layers.append(st)
-        mh = ops.mean_rows(x, B, L, nd * H)  # [B, 2H] fp32
         wl = self.view("scaling_layer.0.weight")
         bl = self.view("scaling_layer.0.bias")
-        m = ops.gemm(mh, wl, bias=bl, epilogue=ops.EPI_BIAS)
+        if self.act_kind == 0:
+            # Identity: the mean over L commutes with the Linear, so the small GEMM
+            # runs on the [B, 2H] means instead of all B*L rows
+            mh = ops.mean_rows(x, B, L, nd * H)  # [B, 2H] fp32
+            m = ops.gemm(mh, wl, bias=bl, epilogue=ops.EPI_BIAS)
+        else:  # y = act(x W^T + b) on every row, then the mean
+            xf = (x if x.dtype == torch.float32 else x.float()).contiguous()
+            u = ops.gemm(xf, wl, bias=bl, epilogue=ops.EPI_BIAS)  # [B*L, D] fp32
+            m = ops.mean_rows(ops.activation(self.act_kind, u), B, L, u.shape[1])
+            mh = (xf, u)
         emb, nrm = ops.l2norm_fwd(m)
         saved = (B, L, layers, mh, emb, nrm) if save else None
         return emb, saved
@@ -255,11 +266,19 @@ class LSTMHead(nn.Module):
         H, nd = self.hidden, self.ndir
         g = self.flat_grad
         dm = ops.l2norm_bwd(demb.contiguous(), emb, nrm)
-        ops.gemm(dm, mh, trans_a=True, b_is_nk=False, accumulate=True,
-                 out=self.view("scaling_layer.0.weight", g))
-        ops.colsum(dm, out=self.view("scaling_layer.0.bias", g), accumulate=True)
-        dmh = ops.gemm(dm, self.view("scaling_layer.0.weight"), b_is_nk=False)  # [B, 2H]
-        dy = ops.bcast_rows(dmh, B, L, 1.0 / L)  # [B*L, 2H] fp32
+        if self.act_kind == 0:
+            ops.gemm(dm, mh, trans_a=True, b_is_nk=False, accumulate=True,
+                     out=self.view("scaling_layer.0.weight", g))
+            ops.colsum(dm, out=self.view("scaling_layer.0.bias", g), accumulate=True)
+            dmh = ops.gemm(dm, self.view("scaling_layer.0.weight"), b_is_nk=False)  # [B, 2H]
+            dy = ops.bcast_rows(dmh, B, L, 1.0 / L)  # [B*L, 2H] fp32
+        else:
+            xf, u = mh
+            du = ops.activation_bwd(self.act_kind, u, ops.bcast_rows(dm, B, L, 1.0 / L))
+            ops.gemm(du, xf, trans_a=True, b_is_nk=False, accumulate=True,
+                     out=self.view("scaling_layer.0.weight", g))
+            ops.colsum(du, out=self.view("scaling_layer.0.bias", g), accumulate=True)
+            dy = ops.gemm(du, self.view("scaling_layer.0.weight"), b_is_nk=False)  # [B*L, 2H]
         for l in range(self.num_layers - 1, -1, -1):
             kind, x, wih, whh, gsave, csave, hprev = layers[l]
             if kind in ("coop", "mfma"):
@@ -352,7 +371,10 @@ class LSTMHead(nn.Module):
         wl = self.view("scaling_layer.0.weight")
         bl = self.view("scaling_layer.0.bias")
         xf = x if x.dtype == torch.float32 else x.float()
-        return ops.gemm(xf.contiguous(), wl, bias=bl, epilogue=ops.EPI_BIAS).view(B, L, -1)
+        y = ops.gemm(xf.contiguous(), wl, bias=bl, epilogue=ops.EPI_BIAS)
+        if self.act_kind != 0:
+            y = ops.activation(self.act_kind, y)
+        return y.view(B, L, -1)
 
 
 class _Seq2VecFn(torch.autograd.Function):

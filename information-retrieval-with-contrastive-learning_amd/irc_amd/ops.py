@@ -426,6 +426,42 @@ def adam_step(p, g, m, v, coef, b1, b2, step_size, bc2_sqrt, eps):
               float(b2), float(step_size), float(bc2_sqrt), float(eps), stream_ptr(p.device))
 
 
+def sgd_step(p, g, buf, coef, lr, momentum, weight_decay, first, shadow=None):
+    """torch.optim.SGD step (dampening 0, nesterov False) over a flat buffer, the clip
+    coefficient / gate read from coef (None: unclipped); shadow: bf16 copy of p."""
+    require_hip(p, g, buf)
+    _lib.call("irc_sgd_step", ptr(p), ptr(g), ptr(buf), p.numel(),
+              ptr(coef) if coef is not None else None, float(lr), float(momentum),
+              float(weight_decay), int(bool(first)), ptr(shadow) if shadow is not None else None,
+              stream_ptr(p.device))
+
+
+# nn activation name -> irc kind code (include/irc.h IRC_ACT_*), torch default arguments
+ACTIVATIONS = {name: i for i, name in enumerate(
+    ["Identity", "ReLU", "ReLU6", "LeakyReLU", "ELU", "CELU", "SELU", "GELU", "SiLU", "Mish",
+     "Sigmoid", "Tanh", "Softplus", "Softsign", "Hardtanh", "Hardsigmoid", "Hardswish",
+     "Tanhshrink"])}
+
+
+def activation(kind: int, u, out=None):
+    """y = act(u) elementwise, fp32."""
+    require_hip(u)
+    if u.dtype != F32 or not u.is_contiguous():
+        raise TypeError("activation: contiguous fp32 input")
+    y = torch.empty_like(u) if out is None else out
+    _lib.call("irc_activation", int(kind), ptr(u), ptr(y), u.numel(), stream_ptr(u.device))
+    return y
+
+
+def activation_bwd(kind: int, u, g):
+    """g *= act'(u) in place (fp32)."""
+    require_hip(u, g)
+    if u.dtype != F32 or g.dtype != F32 or g.numel() != u.numel():
+        raise TypeError("activation_bwd: fp32 u / g of equal size")
+    _lib.call("irc_activation_bwd", int(kind), ptr(u), ptr(g), u.numel(), stream_ptr(u.device))
+    return g
+
+
 def fault_gate(coef, *faults):
     """coef[2] = 1 if any of the (<= 2) uint32 fault words is set: the gated updates
     of this step are skipped on the device."""

@@ -1,9 +1,10 @@
 """Fused optimizers over the flat fp32 parameter buffer of the encoder head.
 
 Reference semantics (src/model.py:44-58, src/train.py:150-169): Adam(lr, betas)
-(eps 1e-8, no weight decay) over model.parameters(); parameters without a
-gradient (frozen BERT, the momentum encoder) are skipped, so only encoder_q
-moves.  clip_grad_norm_(max_norm) is fused into the step: the global norm and
+(eps 1e-8, no weight decay) or SGD(lr, momentum, weight_decay) over
+model.parameters(); parameters without a gradient (frozen BERT, the momentum
+encoder) are skipped, so only encoder_q moves.  ``param_groups[0]["lr"]`` is live
+(the reference's cosine adjust_learning_rate writes it, src/train.py:18-23).  clip_grad_norm_(max_norm) is fused into the step: the global norm and
 the clip coefficient are computed on the device and applied inside the update
 kernel (no host sync).  The optimizer follows the module across .to(device):
 it reads head.flat / head.flat_grad at step time and keeps its moments on the
@@ -18,10 +19,22 @@ import torch
 from . import ops
 
 
-class FusedAdam:
+class _LiveLR:
+    """``lr`` backed by ``param_groups[0]["lr"]``, as torch.optim exposes it."""
+
+    @property
+    def lr(self):
+        return float(self.param_groups[0]["lr"])
+
+    @lr.setter
+    def lr(self, v):
+        self.param_groups[0]["lr"] = float(v)
+
+
+class FusedAdam(_LiveLR):
     def __init__(self, head, lr=2.5e-4, betas=(0.9, 0.999), eps=1e-8):
         self.head = head
-        self.lr = float(lr)
+        self.param_groups = [{"lr": float(lr)}]
         self.b1, self.b2 = (float(b) for b in betas)
         self.eps = float(eps)
         self.step_count = 0
@@ -112,6 +125,82 @@ class FusedAdam:
         self.b1, self.b2 = (float(b) for b in pg["betas"])
         self.eps = float(pg.get("eps", self.eps))
 
-    @property
-    def param_groups(self):
-        return [{"lr": self.lr}]
+
+
+class FusedSGD(_LiveLR):
+    """torch.optim.SGD(params, lr, momentum, weight_decay) (dampening 0, nesterov
+    False; src/model.py:45-51) as one fused launch over the flat buffer, with
+    clip_grad_norm_ and the fault gate fused like FusedAdam.  The momentum buffer is
+    created by the first step (torch: ``buf = d.clone()``)."""
+
+    def __init__(self, head, lr=3e-4, momentum=0.9, weight_decay=1e-4):
+        self.head = head
+        self.param_groups = [{"lr": float(lr)}]
+        self.momentum = float(momentum)
+        self.weight_decay = float(weight_decay)
+        self.buf = None
+        self.started = False  # the momentum buffer holds a first step
+        self.last_norm = None
+
+    def _buffer(self):
+        flat = self.head.flat
+        if self.buf is None:
+            self.buf = torch.zeros(flat.shape, dtype=torch.float32, device=flat.device)
+        elif self.buf.device != flat.device:
+            self.to(flat.device)
+        return self.buf
+
+    def to(self, device):
+        if self.buf is not None:
+            self.buf = self.buf.to(device)
+        return self
+
+    def clip_and_step(self, max_norm: float | None = None, faults=()):
+        g = self.head.flat_grad
+        buf = self._buffer()
+        coef = ops.grad_norm_clip(g, max_norm if max_norm is not None else float("inf"))
+        faults = [f for f in faults if f is not None]
+        if faults:
+            ops.fault_gate(coef, *faults)
+        self.last_norm = coef
+        shadow = self.head.shadow_buffer() if hasattr(self.head, "shadow_buffer") else None
+        ops.sgd_step(self.head.flat.detach(), g, buf, coef, self.lr, self.momentum,
+                     self.weight_decay, not self.started, shadow)
+        # a gated first step leaves the zero buffer unwritten: the next step's
+        # mom * 0 + d is then exactly torch's first-step d, so no host check is needed
+        self.started = True
+        if hasattr(self.head, "after_update"):
+            self.head.after_update(shadow is not None)
+        return coef
+
+    def step(self):
+        return self.clip_and_step(None)
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.head.flat_grad.zero_()
+
+    def state_dict(self):
+        st = {0: {"momentum_buffer": self._buffer()}} if self.started else {}
+        return {"state": st,
+                "param_groups": [{"lr": self.lr, "momentum": self.momentum, "dampening": 0,
+                                  "weight_decay": self.weight_decay, "nesterov": False,
+                                  "maximize": False, "params": [0]}]}
+
+    def load_state_dict(self, sd):
+        """This class's dict, or a reference torch.optim.SGD dict whose parameter
+        indices 0..n-1 are encoder_q's parameters in nn.LSTM order."""
+        buf = self._buffer()
+        st = sd.get("state", {})
+        if 0 in st and st[0].get("momentum_buffer") is not None and \
+                st[0]["momentum_buffer"].numel() == buf.numel():
+            buf.copy_(st[0]["momentum_buffer"])
+            self.started = True
+        elif st:
+            for i, (name, shape) in enumerate(self.head.specs):
+                if i in st and st[i].get("momentum_buffer") is not None:
+                    self.head.view(name, buf).copy_(st[i]["momentum_buffer"].reshape(shape))
+                    self.started = True
+        pg = sd["param_groups"][0]
+        self.lr = float(pg["lr"])
+        self.momentum = float(pg.get("momentum", self.momentum))
+        self.weight_decay = float(pg.get("weight_decay", self.weight_decay))

@@ -2,7 +2,7 @@
 
 ``LSTM`` keeps the reference's config keys, parameter names and initialisation
 (src/model.py:7-41) on the flat-buffer head of irc_amd.lstm_head.
-``get_optimizer`` returns the fused Adam over encoder_q's flat buffer
+``get_optimizer`` returns the fused SGD or Adam over encoder_q's flat buffer
 (model.py:44-58 semantics); checkpoints keep the reference layout
 {Model, Optimizer, Current_step, Args} and file name (model.py:76-99).
 """
@@ -12,13 +12,14 @@ import torch
 
 from irc_amd.bert_train import BertEncoder
 from irc_amd.lstm_head import LSTMHead
-from irc_amd.optim import FusedAdam
+from irc_amd.optim import FusedAdam, FusedSGD
 from src.contrastor.contrastive_loss import NCELoss
 from src.contrastor.contrastive_module import RetrievalModelWrapper
 
 
 class LSTM(LSTMHead):
-    """nn.LSTM(input, hidden, layers, batch_first, bidirectional) + Linear + Identity."""
+    """nn.LSTM(input, hidden, layers, batch_first, bidirectional) + Linear + the
+    configured activation (``eval(f"nn.{act}()")``, model.py:23-26)."""
 
 
 class BERT(BertEncoder):
@@ -33,11 +34,15 @@ class BERT(BertEncoder):
 
 
 def get_optimizer(args, model):
+    if args.opt == "sgd":
+        c = args.config["optimizer"]["SGD"]
+        return FusedSGD(model.encoder_q, lr=float(c["learning_rate"]),
+                        momentum=float(c["momentum"]), weight_decay=float(c["weight_decay"]))
     if args.opt == "adam":
         return FusedAdam(model.encoder_q,
                          lr=float(args.config["optimizer"]["Adam"]["learning_rate"]),
                          betas=tuple(args.config["optimizer"]["Adam"]["betas"]))
-    raise NotImplementedError("--opt sgd is not built yet (Adam is the reference default)")
+    raise ValueError(f"unknown optimizer {args.opt!r} (sgd or adam)")
 
 
 def build_model(args):

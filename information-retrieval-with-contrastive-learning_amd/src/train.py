@@ -31,6 +31,15 @@ from src.model import build_model, get_optimizer, load_model, save_model
 OOM_MARKERS = ("CUDA out of memory", "HIP out of memory", "out of memory")
 
 
+def adjust_learning_rate(optimizer, steps, config):
+    """Cosine decay of the SGD learning rate (reference src/train.py:18-23), applied
+    once per pass over the data when --opt sgd (train.py:90-91)."""
+    lr = float(config["optimizer"]["SGD"]["learning_rate"])
+    lr *= 0.5 * (1.0 + math.cos(math.pi * steps / config["train"]["total_steps"]))
+    for param_group in optimizer.param_groups:
+        param_group["lr"] = lr
+
+
 class _NullWriter:
     def add_scalar(self, tag, value, step):
         pass
@@ -256,6 +265,8 @@ def train(args):
         if hasattr(sampler, "set_epoch"):  # DistributedSampler: a new permutation per pass
             sampler.set_epoch(epoch)
         epoch += 1
+        if args.opt == "sgd":  # scheduler, once per pass (train.py:90-91)
+            adjust_learning_rate(optimizer, st.step_sum, args.config)
         it = iter(train_loader)
         nxt = next(it, None)
         pending = _issue(nxt) if (prefetch and nxt is not None) else None

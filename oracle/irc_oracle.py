@@ -397,8 +397,68 @@ def lstm_param_names(num_layers: int, bidirectional: bool):
     return out
 
 
-def lstm_head_fwd(features, p, num_layers: int, bidirectional: bool = True):
-    """``LSTM.forward`` (model.py:38-41): nn.LSTM then Linear (+Identity)."""
+_SELU = (1.0507009873554804934193349852946, 1.6732632423543772848170429916717)
+
+
+def _softplus(u):
+    return np.where(u > 20.0, u, np.log1p(np.exp(np.minimum(u, 20.0))))
+
+
+def act_fwd(name: str, u):
+    """``eval(f"nn.{act}()")`` (model.py:25) with torch's default arguments."""
+    if name == "Identity":
+        return u
+    sg = 1.0 / (1.0 + np.exp(-u))
+    return {
+        "ReLU": lambda: np.maximum(u, 0.0),
+        "ReLU6": lambda: np.clip(u, 0.0, 6.0),
+        "LeakyReLU": lambda: np.where(u > 0, u, 0.01 * u),
+        "ELU": lambda: np.where(u > 0, u, np.expm1(np.minimum(u, 0.0))),
+        "CELU": lambda: np.where(u > 0, u, np.expm1(np.minimum(u, 0.0))),
+        "SELU": lambda: _SELU[0] * np.where(u > 0, u, _SELU[1] * np.expm1(np.minimum(u, 0.0))),
+        "GELU": lambda: gelu(u),
+        "SiLU": lambda: u * sg,
+        "Mish": lambda: u * np.tanh(_softplus(u)),
+        "Sigmoid": lambda: sg,
+        "Tanh": lambda: np.tanh(u),
+        "Softplus": lambda: _softplus(u),
+        "Softsign": lambda: u / (1.0 + np.abs(u)),
+        "Hardtanh": lambda: np.clip(u, -1.0, 1.0),
+        "Hardsigmoid": lambda: np.clip(u + 3.0, 0.0, 6.0) / 6.0,
+        "Hardswish": lambda: u * np.clip(u + 3.0, 0.0, 6.0) / 6.0,
+        "Tanhshrink": lambda: u - np.tanh(u),
+    }[name]()
+
+
+def act_grad(name: str, u):
+    """d act / du (torch autograd's values at the kinks)."""
+    if name == "Identity":
+        return np.ones_like(u)
+    sg = 1.0 / (1.0 + np.exp(-u))
+    t = np.tanh(u)
+    return {
+        "ReLU": lambda: (u > 0).astype(u.dtype),
+        "ReLU6": lambda: ((u > 0) & (u < 6)).astype(u.dtype),
+        "LeakyReLU": lambda: np.where(u > 0, 1.0, 0.01),
+        "ELU": lambda: np.where(u > 0, 1.0, np.exp(np.minimum(u, 0.0))),
+        "CELU": lambda: np.where(u > 0, 1.0, np.exp(np.minimum(u, 0.0))),
+        "SELU": lambda: np.where(u > 0, _SELU[0], _SELU[0] * _SELU[1] * np.exp(np.minimum(u, 0.0))),
+        "GELU": lambda: 0.5 * (1.0 + _erf(u / np.sqrt(2.0))) + u * np.exp(-0.5 * u * u) / np.sqrt(2 * np.pi),
+        "SiLU": lambda: sg * (1.0 + u * (1.0 - sg)),
+        "Mish": lambda: np.tanh(_softplus(u)) + u * (1.0 - np.tanh(_softplus(u)) ** 2) * sg,
+        "Sigmoid": lambda: sg * (1.0 - sg),
+        "Tanh": lambda: 1.0 - t * t,
+        "Softplus": lambda: np.where(u > 20.0, 1.0, sg),
+        "Softsign": lambda: 1.0 / (1.0 + np.abs(u)) ** 2,
+        "Hardtanh": lambda: ((u > -1) & (u < 1)).astype(u.dtype),
+        "Hardsigmoid": lambda: np.where((u > -3) & (u < 3), 1.0 / 6.0, 0.0),
+        "Hardswish": lambda: np.where(u < -3, 0.0, np.where(u <= 3, u / 3.0 + 0.5, 1.0)),
+        "Tanhshrink": lambda: t * t,
+    }[name]()
+
+
+def lstm_head_fwd(features, p, num_layers: int, bidirectional: bool = True, act="Identity"):
+    """``LSTM.forward`` (model.py:38-41): nn.LSTM then Linear + the activation (:23-26)."""
     x = np.asarray(features)
     caches = []
     for l in range(num_layers):
@@ -413,12 +473,13 @@ def lstm_head_fwd(features, p, num_layers: int, bidirectional: bool = True):
             lc.append(cache)
         caches.append((x, lc))
         x = np.concatenate(outs, axis=2)
-    y = x @ p["scaling_layer.0.weight"].T + p["scaling_layer.0.bias"]
-    return y, (caches, x)
+    u = x @ p["scaling_layer.0.weight"].T + p["scaling_layer.0.bias"]
+    return act_fwd(act, u), (caches, x, u, act)
 
 
 def lstm_head_bwd(dy, p, cache, num_layers: int, bidirectional: bool = True):
-    caches, xlast = cache
+    caches, xlast, u, act = cache
+    dy = dy * act_grad(act, u)
     grads = {}
     grads["scaling_layer.0.weight"] = np.einsum("blo,bli->oi", dy, xlast)
     grads["scaling_layer.0.bias"] = dy.sum(axis=(0, 1))
@@ -448,10 +509,10 @@ def l2_normalize(x, eps: float = 1e-12):
     return x / np.maximum(n, eps)
 
 
-def seq2vec(features, p, num_layers: int, bidirectional: bool = True):
+def seq2vec(features, p, num_layers: int, bidirectional: bool = True, act="Identity"):
     """``seq2vec`` (contrastive_module.py:102-112): head -> mean over ALL L
     positions (PAD included) -> L2 normalise."""
-    y, cache = lstm_head_fwd(features, p, num_layers, bidirectional)
+    y, cache = lstm_head_fwd(features, p, num_layers, bidirectional, act)
     m = y.mean(axis=1)
     return l2_normalize(m), (y, m, cache)
 
@@ -548,6 +609,19 @@ def adam_step(p, g, m, v, step: int, lr: float, b1: float, b2: float, eps: float
     denom = np.sqrt(v) / np.sqrt(bc2) + eps
     p = p - (lr / bc1) * m / denom
     return p, m, v
+
+
+def sgd_step(p, g, buf, lr: float, momentum: float, weight_decay: float):
+    """torch.optim.SGD (model.py:45-51), dampening 0, nesterov False, one tensor;
+    buf None on the first step (torch: buf = d.clone())."""
+    d = g + weight_decay * p
+    buf = d.copy() if buf is None else momentum * buf + d
+    return p - lr * buf, buf
+
+
+def cosine_lr(lr0: float, steps: int, total_steps: int) -> float:
+    """adjust_learning_rate (src/train.py:18-23)."""
+    return lr0 * 0.5 * (1.0 + np.cos(np.pi * steps / total_steps))
 
 
 def momentum_update(pk, pq, m: float):

@@ -1,8 +1,9 @@
 """CPU oracle for one full reference training step sequence (TEST INFRASTRUCTURE ONLY).
 
 Restates src/train.py:86-175 (micro-batch loop, /acml_batch_size, gradient
-accumulation, clip_grad_norm_(1.0), Adam, momentum update, queue switch-on at
-queue_start_steps) on top of the numpy pieces in ``irc_oracle``.  Used by the
+accumulation, clip_grad_norm_(1.0), Adam or SGD with the per-pass cosine learning
+rate, momentum update, queue switch-on at queue_start_steps, the head activation)
+on top of the numpy pieces in ``irc_oracle``.  Used by the
 CPU tests (pinned against tests/golden/train_traj.npz, which was produced by
 running the reference's own ``train()``) and by bench.py's cpu_baseline leg.
 """
@@ -33,6 +34,14 @@ def run_trajectory(fx: dict):
     use_mom = int(fx["use_momentum"]) if "use_momentum" in fx else 1
     B, acml, total, log_step = (int(x) for x in fx["train_cfg"])
     lr, b1, b2, clip = fx["adam"]
+    act = str(fx["activation"]) if "activation" in fx else "Identity"
+    sgd = fx["sgd"] if "sgd" in fx else None  # [lr0, momentum, weight_decay, clip]
+    if sgd is not None:
+        clip = sgd[3]
+    # micro-batch index -> step count at which adjust_learning_rate ran (once per pass)
+    lr_at = {int(i): int(st) for i, st in fx["sgd_epoch_mb"]} if sgd is not None else {}
+    sgd_lr = float(sgd[0]) if sgd is not None else 0.0
+    bufs = {k: None for k in split_state(init, "encoder_q.")}
     pq = split_state(init, "encoder_q.")
     pk = split_state(init, "encoder_k.")
     queue = np.asarray(init["queue"], np.float64)
@@ -45,6 +54,8 @@ def run_trajectory(fx: dict):
     step, bs = 0, 0
     add_q = False
     for i in range(int(fx["mb_len"].shape[0])):
+        if i in lr_at:
+            sgd_lr = O.cosine_lr(float(sgd[0]), lr_at[i], total)
         L = int(fx["mb_len"][i])
         nb = int(fx["mb_B"][i])
         ids = fx["mb_ids"][i, :2 * nb, :L]
@@ -53,12 +64,12 @@ def run_trajectory(fx: dict):
             add_q = True
         feats = O.bert_forward(ids, mask, bert_w, nl_bert, nheads).astype(np.float64)
         a, p = feats[:nb], feats[nb:]
-        emb_q, cq = O.seq2vec(a, pq, nlayers)
+        emb_q, cq = O.seq2vec(a, pq, nlayers, act=act)
         if use_mom:
-            emb_k, _ = O.seq2vec(p, pk, nlayers)
+            emb_k, _ = O.seq2vec(p, pk, nlayers, act=act)
             loss, dq = O.nce_info_loss(emb_q, emb_k, queue if add_q else None, float(T))
         else:  # keys through encoder_q with autograd (contrastive_module.py:82-83)
-            emb_k, ck = O.seq2vec(p, pq, nlayers)
+            emb_k, ck = O.seq2vec(p, pq, nlayers, act=act)
             loss, dq, dk = O.nce_info_loss(emb_q, emb_k, queue if add_q else None, float(T),
                                            want_dk=True)
             gk = O.seq2vec_bwd(dk / acml, pq, ck, nlayers)
@@ -74,9 +85,13 @@ def run_trajectory(fx: dict):
             O.clip_grad_norm(grads, float(clip))
             adam_t += 1
             for k in pq:
-                pq[k], m_state[k], v_state[k] = O.adam_step(pq[k], grads[k], m_state[k],
-                                                            v_state[k], adam_t, float(lr),
-                                                            float(b1), float(b2))
+                if sgd is not None:
+                    pq[k], bufs[k] = O.sgd_step(pq[k], grads[k], bufs[k], sgd_lr,
+                                                float(sgd[1]), float(sgd[2]))
+                else:
+                    pq[k], m_state[k], v_state[k] = O.adam_step(pq[k], grads[k], m_state[k],
+                                                                v_state[k], adam_t, float(lr),
+                                                                float(b1), float(b2))
             for k in pk:
                 pk[k] = O.momentum_update(pk[k], pq[k], float(mom))
             grads = {k: np.zeros_like(v) for k, v in pq.items()}

@@ -461,10 +461,20 @@ def gen_train_traj_nomom(out, tmp):
     gen_train_traj(out, tmp, use_momentum=False, fname="train_traj_nomom.npz")
 
 
-def gen_train_traj(out, tmp, use_momentum=True, fname="train_traj.npz"):
+def gen_train_traj_sgd(out, tmp):
+    """The same run with --opt sgd (torch.optim.SGD with momentum and weight decay,
+    model.py:45-51) over two passes of the data, so the per-pass cosine
+    adjust_learning_rate (train.py:18-23, 90-91) changes the rate, and a Tanh head
+    activation (model.py:25, eval(f"nn.{act}()"))."""
+    gen_train_traj(out, tmp, fname="train_traj_sgd.npz", opt="sgd", act="Tanh", total_steps=6)
+
+
+def gen_train_traj(out, tmp, use_momentum=True, fname="train_traj.npz", opt="adam",
+                   act="Identity", total_steps=4):
     """Run the reference train() loop on a tiny config; record the trajectory."""
     import yaml
     import src.contrastor.contrastive_module as cm
+    import src.train as rtrain
     from src.train import train
 
     vocab = os.path.join(tmp, "vocab.txt")
@@ -485,14 +495,17 @@ def gen_train_traj(out, tmp, use_momentum=True, fname="train_traj.npz"):
     with open(os.path.join(REF, "config.yaml")) as f:
         cfg = yaml.load(f, Loader=yaml.FullLoader)
     cfg["model"]["LSTM"].update(input_size=TINY_BERT["hidden_size"], hidden_size=16,
-                                num_layers=2, output_size=8)
+                                num_layers=2, output_size=8, activation=act)
     cfg["loss"]["InfoNCE"].update(queue_size=32, queue_start_steps=2, use_momentum=use_momentum)
-    cfg["train"].update(batch_size=8, acml_batch_size=16, total_steps=4, log_step=2, n_jobs=0)
+    cfg["train"].update(batch_size=8, acml_batch_size=16, total_steps=total_steps, log_step=2,
+                        n_jobs=0)
     cfg["dataset"]["docs_sentence"] = dpath
+    if opt == "sgd":  # a rate large enough to move the tiny head visibly
+        cfg["optimizer"]["SGD"].update(learning_rate="0.05", momentum=0.9, weight_decay="1e-2")
 
     args = argparse.Namespace(config=cfg, log=False, logdir=os.path.join(tmp, "log"), data="doc",
                               ckptdir=os.path.join(tmp, "ckpt"), seed=1337, gpu="-1", ckpt=None,
-                              model="LSTM", loss="InfoNCE", opt="adam", sample="uniform")
+                              model="LSTM", loss="InfoNCE", opt=opt, sample="uniform")
     args.device = torch.device("cpu")
     torch.manual_seed(1337)
     np.random.seed(1337)
@@ -520,16 +533,24 @@ def gen_train_traj(out, tmp, use_momentum=True, fname="train_traj.npz"):
         rec.setdefault("addq", []).append(int(self.add_queue_to_loss))
         return loss
 
+    orig_adjust = rtrain.adjust_learning_rate
+
+    def adjust(optimizer, steps, config):  # records where each pass starts
+        rec.setdefault("epoch_mb", []).append((len(rec["loss"]), int(steps)))
+        return orig_adjust(optimizer, steps, config)
+
     cm.RetrievalModelWrapper.bert_extract = bert_extract
     cm.RetrievalModelWrapper.forward = forward
+    rtrain.adjust_learning_rate = adjust
     try:
         train(args)
     finally:
         cm.RetrievalModelWrapper.bert_extract = orig_extract
         cm.RetrievalModelWrapper.forward = orig_forward
+        rtrain.adjust_learning_rate = orig_adjust
 
-    ck_path = os.path.join(args.ckptdir, "uniform_InfoNCE_LSTM_4.pth")
-    if use_momentum:  # the reference-written checkpoint itself: load_model parity fixture
+    ck_path = os.path.join(args.ckptdir, f"uniform_InfoNCE_LSTM_{total_steps}.pth")
+    if use_momentum and opt == "adam":  # the reference-written checkpoint: load_model fixture
         import shutil
 
         shutil.copyfile(ck_path, os.path.join(out, "ref_ckpt_InfoNCE_LSTM_4.pth"))
@@ -555,8 +576,15 @@ def gen_train_traj(out, tmp, use_momentum=True, fname="train_traj.npz"):
                mb_loss=np.array(rec["loss"]), mb_addq=np.array(rec["addq"]),
                lstm_cfg=np.array([TINY_BERT["hidden_size"], 16, 2, 8]),
                loss_cfg=np.array([0.05, 0.9, 32, 2]),
-               train_cfg=np.array([8, 16, 4, 2]),
+               train_cfg=np.array([8, 16, total_steps, 2]),
                adam=np.array([2.5e-4, 0.9, 0.999, 1.0]))
+    if opt == "sgd":
+        c = cfg["optimizer"]["SGD"]
+        res.update(sgd=np.array([float(c["learning_rate"]), float(c["momentum"]),
+                                 float(c["weight_decay"]), 1.0]),
+                   sgd_epoch_mb=np.array(rec["epoch_mb"], np.int64))
+    if act != "Identity":
+        res["activation"] = np.array(act)
     if not use_momentum:
         res["use_momentum"] = np.int64(0)
     np.savez_compressed(os.path.join(out, fname), **res)
@@ -584,6 +612,7 @@ def main():
         gen_scan(HERE)
         gen_train_traj(HERE, tmp)
         gen_train_traj_nomom(HERE, tmp)
+        gen_train_traj_sgd(HERE, tmp)
 
 
 if __name__ == "__main__":

@@ -158,7 +158,8 @@ def test_merge_equals_global():
     np.testing.assert_array_equal(ms, full_s)
 
 
-@pytest.mark.parametrize("fixture", ["train_traj.npz", "train_traj_nomom.npz"])
+@pytest.mark.parametrize("fixture", ["train_traj.npz", "train_traj_nomom.npz",
+                                     "train_traj_sgd.npz"])
 def test_train_trajectory_matches_reference(fixture):
     fx = load_golden(fixture)
     losses, final = train_oracle.run_trajectory(fx)

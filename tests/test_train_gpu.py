@@ -25,7 +25,14 @@ def _args_from_golden(fx):
     T, mom, qsize, qstart = fx["loss_cfg"]
     B, acml, total, log_step = (int(x) for x in fx["train_cfg"])
     cfg["model"]["LSTM"].update(input_size=in_dim, hidden_size=hsz, num_layers=nlayers,
-                                output_size=outd)
+                                output_size=outd,
+                                activation=str(fx["activation"]) if "activation" in fx
+                                else "Identity")
+    opt = "adam"
+    if "sgd" in fx:
+        opt = "sgd"
+        lr, m, wd, _ = (float(x) for x in fx["sgd"])
+        cfg["optimizer"]["SGD"].update(learning_rate=lr, momentum=m, weight_decay=wd)
     cfg["loss"]["InfoNCE"].update(temperature=float(T), momentum=float(mom),
                                   queue_size=int(qsize), queue_start_steps=int(qstart),
                                   use_momentum=bool(int(fx["use_momentum"]))
@@ -40,14 +47,14 @@ def _args_from_golden(fx):
         "num_attention_heads": 2, "intermediate_size": int(
             init["encoder.layer.0.intermediate.dense.weight"].shape[0]),
         "max_position_embeddings": int(init["embeddings.position_embeddings.weight"].shape[0])}}
-    return argparse.Namespace(config=cfg, loss="InfoNCE", model="LSTM", opt="adam",
+    return argparse.Namespace(config=cfg, loss="InfoNCE", model="LSTM", opt=opt,
                               sample="uniform")
 
 
 def _replay(gpu, precision, pipelined=False, fixture="train_traj.npz"):
     from irc_amd.precision import get_precision, set_precision
     from src.model import build_model, get_optimizer
-    from src.train import TrainState
+    from src.train import TrainState, adjust_learning_rate
 
     fx = load_golden(fixture)
     old = get_precision()
@@ -77,7 +84,12 @@ def _replay(gpu, precision, pipelined=False, fixture="train_traj.npz"):
         if pipelined:  # src/train.py's loop: BERT of micro-batch i+1 overlaps heads of i
             nb0, ids0, mask0 = batch(0)
             pending = model.bert_extract_async(ids0, mask0, nb0)
+        epoch_at = {int(a): int(b) for a, b in fx["sgd_epoch_mb"]} if "sgd_epoch_mb" in fx \
+            else {}
         for i in range(n_mb):
+            if i in epoch_at:  # src/train.py: the cosine rate, once per pass (--opt sgd)
+                assert st.step_sum == epoch_at[i]
+                adjust_learning_rate(opt, st.step_sum, args.config)
             nb, ids, mask = batch(i)
             if pipelined:
                 handle = pending
@@ -101,10 +113,13 @@ def _replay(gpu, precision, pipelined=False, fixture="train_traj.npz"):
         set_precision(old)
 
 
-@pytest.mark.parametrize("fixture", ["train_traj.npz", "train_traj_nomom.npz"])
+@pytest.mark.parametrize("fixture", ["train_traj.npz", "train_traj_nomom.npz",
+                                     "train_traj_sgd.npz"])
 def test_train_trajectory_fp32(gpu, fixture):
     """fixture train_traj_nomom: loss.use_momentum False -- no encoder_k, the keys
-    come from encoder_q with autograd, so the InfoNCE backward feeds dk too."""
+    come from encoder_q with autograd, so the InfoNCE backward feeds dk too.
+    train_traj_sgd: --opt sgd (momentum + weight decay, the per-pass cosine rate over
+    two passes) with a Tanh head activation (src/model.py:25,45-51)."""
     fx, losses, model = _replay(gpu, "fp32", fixture=fixture)
     np.testing.assert_allclose(losses, fx["mb_loss"], rtol=2e-4, atol=1e-4)
     sd = model.state_dict()
@@ -117,13 +132,14 @@ def test_train_trajectory_fp32(gpu, fixture):
                                        err_msg=name)
 
 
-def test_train_trajectory_bf16(gpu):
+@pytest.mark.parametrize("fixture", ["train_traj.npz", "train_traj_sgd.npz"])
+def test_train_trajectory_bf16(gpu, fixture):
     """Production precision: bf16 BERT/LSTM operands, fp32 state/loss/optimizer.
     Micro-batch losses (~25-45) within 5e-3 relative of the reference's fp32 run
     (achieved <= 2.7e-3 on MI355X: a 2-layer H=32 BERT, where one bf16 rounding is
     a larger share of each feature; at the C2 shapes the bf16 step's loss is
     within 1.2e-5 of fp32 mode, tests/test_configs_gpu.py)."""
-    fx, losses, model = _replay(gpu, "bf16")
+    fx, losses, model = _replay(gpu, "bf16", fixture=fixture)
     rel = np.abs(losses - fx["mb_loss"]) / np.abs(fx["mb_loss"])
     print("bf16 trajectory: per-micro-batch loss rel err", " ".join(f"{r:.1e}" for r in rel))
     np.testing.assert_allclose(losses, fx["mb_loss"], rtol=5e-3)
