@@ -300,7 +300,7 @@ __device__ __forceinline__ float act_grad(int k, float u) {
     }
     case IRC_ACT_HARDTANH: return (u > -1.f && u < 1.f) ? 1.f : 0.f;
     case IRC_ACT_HARDSIGMOID: return (u > -3.f && u < 3.f) ? 1.f / 6.f : 0.f;
-    case IRC_ACT_HARDSWISH: return u < -3.f ? 0.f : (u <= 3.f ? u / 3.f + 0.5f : 1.f);
+    case IRC_ACT_HARDSWISH: return u <= -3.f ? 0.f : (u < 3.f ? u / 3.f + 0.5f : 1.f);
     case IRC_ACT_TANHSHRINK: {
       const float t = tanhf(u);
       return t * t;

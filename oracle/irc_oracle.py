@@ -452,7 +452,7 @@ def act_grad(name: str, u):
         "Softsign": lambda: 1.0 / (1.0 + np.abs(u)) ** 2,
         "Hardtanh": lambda: ((u > -1) & (u < 1)).astype(u.dtype),
         "Hardsigmoid": lambda: np.where((u > -3) & (u < 3), 1.0 / 6.0, 0.0),
-        "Hardswish": lambda: np.where(u < -3, 0.0, np.where(u <= 3, u / 3.0 + 0.5, 1.0)),
+        "Hardswish": lambda: np.where(u <= -3, 0.0, np.where(u < 3, u / 3.0 + 0.5, 1.0)),
         "Tanhshrink": lambda: t * t,
     }[name]()
 

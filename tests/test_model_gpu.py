@@ -71,7 +71,8 @@ def test_bert_long_512_matches_reference(gpu, mode, atol):
     finally:
         set_precision(old)
     ref = np.concatenate([g["anchor_hs"], g["positive_hs"]])
-    kw = {"rtol": 1e-4} if mode == "fp32" else {}
+    # bf16: the hidden states leave as bf16 (values up to ~5: 2 ulps = 1.6e-2 relative)
+    kw = {"rtol": 1e-4} if mode == "fp32" else {"rtol": 1.6e-2}
     np.testing.assert_allclose(out.float().cpu().numpy(), ref, atol=atol, **kw)
 
 

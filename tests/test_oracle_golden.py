@@ -316,3 +316,22 @@ def test_torch_cpu_baseline_restatement_matches_reference():
     loss = T.nce_loss(torch.from_numpy(n[f"{tag}_q"]), torch.from_numpy(n[f"{tag}_k"]),
                       torch.from_numpy(n[f"{tag}_queue"]), 0.05)
     assert abs(loss.item() - float(n[f"{tag}_loss"])) <= 1e-5 * float(n[f"{tag}_loss"])
+
+
+def test_activation_oracle_matches_torch():
+    """oracle.act_fwd / act_grad (the head activation, model.py:25) against torch's
+    modules and autograd, kinks included."""
+    import torch
+
+    u = np.concatenate([np.random.default_rng(0).standard_normal(2000) * 4,
+                        [-25., -6., -3., -1., 0., 1., 3., 6., 19.9, 20.1, 25.]])
+    for name in ["Identity", "ReLU", "ReLU6", "LeakyReLU", "ELU", "CELU", "SELU", "GELU", "SiLU",
+                 "Mish", "Sigmoid", "Tanh", "Softplus", "Softsign", "Hardtanh", "Hardsigmoid",
+                 "Hardswish", "Tanhshrink"]:
+        ut = torch.tensor(u, requires_grad=True)
+        y = getattr(torch.nn, name)()(ut)
+        y.sum().backward()
+        np.testing.assert_allclose(O.act_fwd(name, u), y.detach().numpy(), rtol=1e-12,
+                                   atol=1e-12, err_msg=name)
+        np.testing.assert_allclose(O.act_grad(name, u), ut.grad.numpy(), rtol=1e-7,
+                                   atol=1e-12, err_msg=name)
