@@ -466,6 +466,13 @@ int irc_corpus_pack(const int* tok, const int* tok_len, int64_t n, int64_t max_t
 int irc_pair_batch(const int* flat, const int64_t* offsets, const int64_t* sel, int64_t rows,
                    int64_t L, int64_t cls_id, int64_t sep_id, int64_t pad_id, int64_t* ids,
                    int64_t* mask, irc_stream_t stream);
+/* Host function (no device work): the uniform pair draw of DocDataset.__getitem__
+ * (src/dataset.py:89-101: np.random.choice(len(doc), 2, replace=False) on numpy's
+ * global legacy RandomState) for n documents at once.  mt_key[624] / *mt_pos are
+ * numpy's MT19937 state (np.random.get_state()), advanced in place exactly as the
+ * n calls would; first / second [n] = doc_start[docs[t]] + the two drawn sentences. */
+int irc_pair_sample(uint32_t* mt_key, int* mt_pos, const int64_t* doc_start,
+                    const int64_t* docs, int64_t n, int64_t* first, int64_t* second);
 
 /* ------------------------------------------------- input pipeline (csrc/wordpiece.hip)
  * BERT WordPiece tokenisation + joint padding on the device: replaces the

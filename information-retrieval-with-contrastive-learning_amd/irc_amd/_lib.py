@@ -29,6 +29,7 @@ SIGNATURES = {
     "irc_scan_topk_workspace": (I64, [I64, I64, I64, I64]),
     "irc_scan_topk": (I32, [P, P, I64, I64, I64, I64, I64, P, I64, P, P, P]),
     "irc_corpus_pack": (I32, [P, P, I64, I64, P, P, P]),
+    "irc_pair_sample": (I32, [P, P, P, P, I64, P, P]),
     "irc_pair_batch": (I32, [P, P, P, I64, I64, I64, I64, I64, P, P, P]),
     "irc_nce_fused_workspace": (I64, [I64, I64, I64, I64, I64]),
     "irc_nce_fused_fwd": (I32, [P, P, I64, I64, I64, F32, I64, I64, P, I64, P, P, P]),

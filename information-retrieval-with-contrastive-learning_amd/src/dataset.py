@@ -173,6 +173,25 @@ class PairSampler:
             raise ValueError(ds.sample_method)
         return int(self.doc_start[idx] + i), int(self.doc_start[idx] + j)
 
+    def pairs_uniform(self, batch):
+        """pair() for a whole batch of documents in the uniform mode: the same draws
+        from numpy's global RandomState (irc_pair_sample restates
+        np.random.choice(n, 2, replace=False) on its MT19937 state and hands the
+        advanced state back), ~0.1 us per pair instead of ~20 us of Python each --
+        at B = 256 the per-call form cost ~5 ms of host time per step."""
+        from irc_amd import _lib
+
+        st = np.random.get_state()
+        key = np.array(st[1], dtype=np.uint32)
+        pos = np.array([st[2]], dtype=np.int32)
+        docs = np.ascontiguousarray(batch, dtype=np.int64)
+        a = np.empty(docs.shape[0], np.int64)
+        b = np.empty(docs.shape[0], np.int64)
+        _lib.call("irc_pair_sample", key.ctypes.data, pos.ctypes.data, self.doc_start.ctypes.data,
+                  docs.ctypes.data, docs.shape[0], a.ctypes.data, b.ctypes.data)
+        np.random.set_state(("MT19937", key, int(pos[0]), st[3], st[4]))
+        return a, b
+
     def __iter__(self):
         # a DataLoader iterator draws its workers' base seed from torch's default
         # generator before the sampler draws its permutation seed: draw it too, so
@@ -182,7 +201,11 @@ class PairSampler:
         for idx in self.sampler:
             batch.append(int(idx))
             if len(batch) == self.bsz:
-                pairs = [self.pair(i) for i in batch]
-                sel = np.array([a for a, _ in pairs] + [b for _, b in pairs], np.int64)
+                if self.dataset.sample_method == "uniform":
+                    a, b = self.pairs_uniform(batch)
+                    sel = np.concatenate([a, b])
+                else:
+                    pairs = [self.pair(i) for i in batch]
+                    sel = np.array([a for a, _ in pairs] + [b for _, b in pairs], np.int64)
                 yield torch.LongTensor(batch).view(-1, 1), sel
                 batch = []

@@ -48,3 +48,28 @@ def test_pair_sampler_replays_dataloader_pairs(tmp_path):
                         [flat[i] for i in sel[B:]]))
     assert len(ps) == len(get_dataloader(args, train=True))
     assert got == ref
+
+
+def test_pairs_uniform_equals_np_random_choice_and_state(tmp_path):
+    """irc_pair_sample (C restatement of np.random.choice(n, 2, replace=False) on the
+    legacy global MT19937) against the per-call numpy draws, over documents of 2 to
+    700 sentences: the same pairs and the same RNG state afterwards, across the
+    624-word regeneration boundary."""
+    args, _ = _args(tmp_path)
+    ps = PairSampler(args)
+    rng = np.random.default_rng(4)
+    lens = np.concatenate([rng.integers(2, 9, 3000), [2, 64, 65, 700, 333, 1024]])
+    ps.doc_start = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=ps.doc_start[1:])
+    docs = rng.integers(0, len(lens), 5000)
+    docs[:6] = np.arange(len(lens) - 6, len(lens))
+    np.random.seed(77)
+    ref = [np.random.choice(int(lens[d]), size=2, replace=False) for d in docs]
+    ref_state = np.random.get_state()
+    np.random.seed(77)
+    a, b = ps.pairs_uniform(docs)
+    st = np.random.get_state()
+    assert np.array_equal(a - ps.doc_start[docs], [r[0] for r in ref])
+    assert np.array_equal(b - ps.doc_start[docs], [r[1] for r in ref])
+    assert np.array_equal(st[1], ref_state[1]) and st[2] == ref_state[2]
+    assert np.random.random() == (np.random.set_state(ref_state), np.random.random())[1]
