@@ -248,13 +248,15 @@ def run_train(args, rank, world, dev, weights="bf16", cfg=None):
     pairs = TRAIN_B * args.steps * world
     achieved = g_flops / g_s / 1e12 if g_s > 0 else None
     loss = float(st.loss_record[-1]) if st.loss_record else None
+    step_tflops = pairs * flops_pair / dt / 1e12
     return model, {
         "pairs_per_s": pairs / dt,
         "ms_per_step": dt * 1e3 / args.steps,
         "loss_last": loss,
         "flops_per_pair": flops_pair,
-        "step_tflops": pairs * flops_pair / dt / 1e12,
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": gpeak,
+        "step_tflops": step_tflops,
+        "roofline": _step_roofline(step_tflops, gpeak, flops_pair, {
+                     "bound": "mfma", "achieved": achieved, "peak": gpeak,
                      "unit": "TFLOP/s", "frac": achieved / gpeak if achieved else None,
                      "traffic": _pmc_traffic(ptag),
                      "traffic_source": _pmc_source(ptag),
@@ -275,7 +277,7 @@ def run_train(args, rank, world, dev, weights="bf16", cfg=None):
                          "achieved": live_flops / live_s / 1e12 if live_s > 0 else None,
                          "note": "timed region itself: BERT GEMMs share the chip with the "
                                  "heads' recurrences on other streams, so event durations "
-                                 "overlap and are summed"}},
+                                 "overlap and are summed"}}),
     }
 
 
@@ -347,7 +349,8 @@ def run_train_bert(args, rank, world, dev):
         "flops_per_pair": flops_pair,
         "step_tflops": step_tflops,
         "step_mfma_frac": step_tflops / BF16_PEAK_TFS,
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS,
+        "roofline": _step_roofline(step_tflops, BF16_PEAK_TFS, flops_pair, {
+                     "bound": "mfma", "achieved": achieved, "peak": BF16_PEAK_TFS,
                      "unit": "TFLOP/s", "frac": achieved / BF16_PEAK_TFS if achieved else None,
                      "traffic": _pmc_traffic("gemm_bf16_bert"),
                      "traffic_source": _pmc_source("gemm_bf16_bert"),
@@ -358,8 +361,22 @@ def run_train_bert(args, rank, world, dev):
                      "alg_flops_per_step": g_flops / args.steps,
                      **g_bytes,
                      "live_overlapped": {
-                         "achieved": live_flops / live_s / 1e12 if live_s > 0 else None}},
+                         "achieved": live_flops / live_s / 1e12 if live_s > 0 else None}}),
     }
+
+
+def _step_roofline(step_tflops, peak, flops_pair, gemm):
+    """The training leg's roofline object: the north star's quantity, the whole
+    encoder + InfoNCE step against the dense MFMA peak (pairs/s x
+    algorithmic FLOPs per pair / peak), with the dominant kernel family -- the GEMM
+    launches, priced on their own HIP-event durations -- as the ``gemm`` sub-field
+    (``traffic``: that family's PMC HBM bytes per launch)."""
+    return {"bound": "mfma", "achieved": step_tflops, "peak": peak, "unit": "TFLOP/s",
+            "frac": step_tflops / peak, "traffic": gemm.get("traffic"),
+            "definition": f"step-level: pairs/s x {flops_pair / 1e9:.2f} GFLOP per pair "
+                          "(algorithmic, SURVEY.md 8d) / dense peak; the GEMM family alone "
+                          "in 'gemm'",
+            "gemm": gemm}
 
 
 def _lstm_flops_per_pair(cfg):
@@ -609,15 +626,18 @@ def _leg_summary(name, d):
     fraction, Q sweep); the full leg goes to the detail file."""
     if name.startswith("train"):
         r = d.get("roofline") or {}
+        gm = r.get("gemm") or {}
         return {"pairs_per_s": _r(d.get("pairs_per_s"), 5), "ms_per_step": _r(d.get("ms_per_step")),
-                "gemm_frac": _r(r.get("frac"), 3), "gemm_ms_per_step": _r(r.get("gemm_ms_per_step")),
-                "traffic_over_alg": _r(r.get("traffic_over_alg"), 3),
-                "step_tflops": _r(d.get("step_tflops"))}
+                "step_frac": _r(r.get("frac"), 3), "step_tflops": _r(d.get("step_tflops")),
+                "gemm_frac": _r(gm.get("frac"), 3), "gemm_ms_per_step": _r(gm.get("gemm_ms_per_step")),
+                "traffic_over_alg": _r(gm.get("traffic_over_alg"), 3)}
     if name == "sparse_tfidf":
         c = d.get("cpu_baseline") or {}
         return {"queries_per_s": _r(d.get("value"), 5), "cpu_queries_per_s": _r(c.get("value"))}
     r, c = d.get("roofline") or {}, d.get("call_level") or {}
+    cb = d.get("cpu_baseline") or {}
     out = {"queries_per_s": _r(d.get("value"), 5), "Q": d.get("queries"),
+           "cpu_queries_per_s": _r(cb.get("value")), "cpu_cores": cb.get("cores"),
            "docs_per_gpu": d.get("docs_per_gpu"), "bound": r.get("bound"),
            "filter_frac": _r(r.get("frac"), 3), "filter_us": _r(r.get("kernel_avg_us")),
            "call_us": _r(c.get("serial_us_per_call")), "call_hbm_frac": _r(c.get("serial_hbm_frac"), 3)}
