@@ -476,13 +476,8 @@ constexpr int ROW_BYTES = BK * 2;  // 128
 // fragment row set used here (row offsets are multiples of 16); the round-2 key r & 7
 // repeats inside every group (rows r, r + 8 / r + 24) and made every fragment read 2-way
 // conflicted: 47-49% of the LDS-array cycles (profiles/r03_lds_y_before.txt).
-// -DIRC_BIG_OLD_SWZ builds the old key for the A/B (same bytes, same MFMAs: bit-identical).
 __device__ __forceinline__ int chunk_key(int r) {
-#ifdef IRC_BIG_OLD_SWZ
-  return r & 7;
-#else
   return (r >> 1) & 7;
-#endif
 }
 
 // rows [0, nrows_tile) of one operand tile: nrows_tile*8 16-byte chunks, NT per pass
@@ -582,74 +577,6 @@ __device__ uint64_t big_stamps[64][5][2];
 // (lane & 15)].  The chunk key (r >> 1) & 7 stays conflict free for the 16x16x32 fragment
 // reads (lane l: row l & 15, chunk 4 s + (l >> 4): each 16-lane group covers 16 distinct
 // 16-byte bank slots).  Ends with every wave past its last LDS read (LDS free).
-#ifdef IRC_BIG_PP
-// Ping-pong form (A/B build): the two row groups (wm = 0 / 1, 4 waves each) run one
-// section apart -- while one group issues its LDS fragment reads (and its share of the
-// next K-tile's DMA), the other runs MFMAs from registers.  Unit u = half K-tile (kt, s2):
-// L(u) = [s2 == 0: this group's passes of K-tile kt + 1's DMA] + the unit's 14 fragment
-// reads; M(u) = its 8 x 2 WNB MFMAs.  Same MFMAs in the same k order per accumulator as
-// the 2-slot loop: bit-identical results.  Buffer rule: the DMA of kt + 1 (into kt - 1's
-// buffer) is issued in L(kt, 0), after the barrier that ends group 1's L(kt - 1, 1), its
-// last reads of kt - 1.  Landing rule: group 0 reads kt + 1 first, in L(kt + 1, 0); group
-// 1 waits vmcnt(0) before the barrier that ends its L(kt, 1) (which is the barrier before
-// that section), group 0 before the one that ends its M(kt, 1).  Group 1 starts one barrier
-// late and skips its last one, so both groups pass the same barrier count.
-template <int WNB>
-__device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t lda,
-                                              const unsigned short* B, int64_t ldb, int m0,
-                                              int n0, int M, int N, int K, char* lds, int wave,
-                                              int lane, f32x4 (&acc4)[8][2 * WNB]) {
-  constexpr int BN = 128 * WNB;
-  constexpr int A_BYTES = BM * ROW_BYTES, STAGE = A_BYTES + BN * ROW_BYTES;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int nk = K / BK;
-  stage<BM>(A, lda, m0, M, 0, lds, wave, lane);
-  stage<BN>(B, ldb, n0, N, 0, lds + A_BYTES, wave, lane);
-  wait_vmcnt<0>();
-  __syncthreads();
-  if (wm == 1) wg_barrier();  // group 1 runs one section behind
-  const int l16 = lane & 15, q4 = lane >> 4;
-  const int key = chunk_key(l16);
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* la = lds + (kt & 1) * STAGE;
-    const char* lb = la + A_BYTES;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      // ---- L section
-      if (s2 == 0 && kt + 1 < nk) {
-        char* nxt = lds + ((kt + 1) & 1) * STAGE;
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln);
-        stage<BN>(B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
-      }
-      const int coff = (((4 * s2 + q4) ^ key) * 16);
-      bf16x8 fa[8], fb[2 * WNB];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 16 + l16) * 128 + coff);
-#pragma unroll
-      for (int j = 0; j < 2 * WNB; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(lb + (wn * 32 * WNB + j * 16 + l16) * 128 + coff);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (wm == 1 && s2 == 1) wait_vmcnt<0>();  // group 0 reads kt + 1 after this barrier
-      wg_barrier();
-      // ---- M section
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < 2 * WNB; ++j)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc4[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      if (wm == 0 && s2 == 1) wait_vmcnt<0>();  // its own kt + 1 DMA, read next section
-      if (!(wm == 1 && kt == nk - 1 && s2 == 1)) wg_barrier();
-    }
-  }
-  // group 0 returns under group 1's last MFMAs: every fragment read of both groups is
-  // done (group 1's last L section ended at group 0's last barrier), LDS is free
-}
-#else
 template <int WNB>
 __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t lda,
                                               const unsigned short* B, int64_t ldb, int m0,
@@ -674,7 +601,6 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
 #endif
     BSTAMP(kt, 0);
     char* nxt = lds + (cur ^ 1) * STAGE;
-#ifndef IRC_BIG_IL
     if (more) {
       // the DMA addresses are re-derived per K-tile (kept live through the loop they
       // would push the 16x16 fragments into spills)
@@ -683,7 +609,6 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
       stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln);
       stage<BN>(B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
     }
-#endif
     BSTAMP(kt, 1);
     const char* la = lds + cur * STAGE;
     const char* lb = la + A_BYTES;
@@ -696,19 +621,6 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
         fa[i] = *reinterpret_cast<const bf16x8*>(la + (wm * 128 + i * 16 + l16) * 128 + coff);
 #pragma unroll
       for (int j = 0; j < 2 * WNB; ++j) {
-#ifdef IRC_BIG_IL
-        // the next K-tile's DMA, one pass per MFMA group (A: 4 passes, B: 2 WNB), so the
-        // LDS-DMA requests queue behind MFMAs instead of stalling the wave in one burst
-        const int gp = s2 * 2 * WNB + j;
-        if (more && gp < 4 + 2 * WNB) {
-          int ln = lane;
-          asm volatile("" : "+v"(ln));
-          if (gp < 4)
-            stage_one<BM>(gp, A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln);
-          else
-            stage_one<BN>(gp - 4, B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
-        }
-#endif
         const bf16x8 fb =
             *reinterpret_cast<const bf16x8*>(lb + (wn * 32 * WNB + j * 16 + l16) * 128 + coff);
 #pragma unroll
@@ -723,7 +635,6 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
     BSTAMP(kt, 4);
   }
 }
-#endif  // IRC_BIG_PP
 }  // namespace big
 
 // IRC_BIG_RING=1 selects the 4-slot ring of gemm_big_kernel (A/B; read on first use;
@@ -865,28 +776,15 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 #else
     const bool more = kt + 1 < nk;
 #endif
-#ifndef IRC_BIG_SPREAD
     if (more) {
       char* nxt = lds + (cur ^ 1) * STAGE;
       big::stage<BM>(A, g.lda, m0, g.M, (kt + 1) * BK, nxt, wave, lane);
       big::stage<BN>(B, g.ldb, n0, g.N, (kt + 1) * BK, nxt + A_BYTES, wave, lane);
     }
-#endif
     const char* la = lds + cur * STAGE;
     const char* lb = la + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < BK / 16; ++kk) {
-#ifdef IRC_BIG_SPREAD  // A/B build: the next K-tile's DMA spread over the 4 k-steps
-      if (more) {
-        char* nxt = lds + (cur ^ 1) * STAGE;
-        constexpr int PA = BM * 8 / NT, PB = BN * 8 / NT;  // 4, 2 * WNB passes
-        const int k1 = (kt + 1) * BK;
-        if (kk == 0) big::stage_part<BM, 0, PA / 2>(A, g.lda, m0, g.M, k1, nxt, wave, lane);
-        if (kk == 1) big::stage_part<BM, PA / 2, PA>(A, g.lda, m0, g.M, k1, nxt, wave, lane);
-        if (kk == 2) big::stage_part<BN, 0, PB / 2>(B, g.ldb, n0, g.N, k1, nxt + A_BYTES, wave, lane);
-        if (kk == 3) big::stage_part<BN, PB / 2, PB>(B, g.ldb, n0, g.N, k1, nxt + A_BYTES, wave, lane);
-      }
-#endif
       const int coff = (((2 * kk + h) ^ swz) * 16);
       bf16x8 fa[4], fb[WNB];
 #pragma unroll
@@ -962,21 +860,6 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-#ifdef IRC_BIG_RPRE  // A/B build: the pass's residual rows loaded before its LDS staging
-      constexpr int CPRR = WCOLS / 8, NRR = 32 * CPRR / 64;
-      u16x8 rpre[NRR];
-      if constexpr (sizeof(TO) == 2 && (EPI == EPI_BIAS_RESID || EPI == EPI_RESID)) {
-#pragma unroll
-        for (int it = 0; it < NRR; ++it) {
-          const int c = it * 64 + lane;
-          const int row = rbase0 + i * 32 + c / CPRR, col = cbase + (c % CPRR) * 8;
-          rpre[it] = (row < g.M && col < g.N)
-                         ? *reinterpret_cast<const u16x8*>(
-                               reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col)
-                         : (u16x8)0;
-        }
-      }
-#endif
       if constexpr (MF16) {
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
@@ -1048,13 +931,8 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
             for (int t = 0; t < 8; ++t)
               v[t] += bf16_to_f32(f32_to_bf16(__builtin_fmaf((bf16_to_f32(rr[t]) - mu) * rs, gg[t], bb[t])));
           } else if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
-#ifdef IRC_BIG_RPRE
-            const u16x8 rr = EPI == EPI_DGELU ? *reinterpret_cast<const u16x8*>(
-                reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col) : rpre[it];
-#else
             const u16x8 rr = *reinterpret_cast<const u16x8*>(
                 reinterpret_cast<const unsigned short*>(R) + (int64_t)row * g.ldr + col);
-#endif
 #pragma unroll
             for (int t = 0; t < 8; ++t)
               v[t] = EPI == EPI_DGELU ? v[t] * gelu_grad_fast(bf16_to_f32(rr[t]))

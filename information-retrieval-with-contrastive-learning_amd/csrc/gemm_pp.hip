@@ -282,9 +282,7 @@ __device__ __forceinline__ void stage_tile(const PArgs& g, const unsigned short*
 // Measured on MI355X (profiles/r03_gemm_j_*): MX qkv / FFN1 (MX out) / FFN2 101 /
 // 184 / 119 us against 110 / 194 / 135; the bf16 forms gain nothing on qkv / FFN2
 // and lose on FFN1 + GELU (237 vs 200 us) and 4096^3 (127 vs 108 us).
-#ifndef IRC_PP_G1_EARLY
 #define IRC_PP_G1_EARLY 1
-#endif
 
 // The ping-pong K loop of one 256x256 output tile over nk K-tiles from kbeg.
 // K-tile kt lives in LDS buffer (kt + par) & 1, the buffers `pitch` bytes apart.
@@ -326,20 +324,15 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
     }
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = (kt + par) & 1;
-      // ---- L section: next tile's DMA (group 0; group 1 with IRC_PP_G1_EARLY = 0),
+      // ---- L section: next tile's DMA (group 0; group 1 too when not G1E),
       // this tile's fragments
 #ifdef IRC_PP_DIAG_NODMA  // diagnostic build: only K-tile 0 is loaded (MFMA + LDS-read rate)
       if (kt + 1 < nk && kt < 0) {
 #else
       if (kt + 1 < nk && (grp == 0 || !G1E)) {
 #endif
-#ifdef IRC_MX_NO_REDERIVE  // A/B build: DMA addresses kept live as in the bf16 loop
-        stage_tile<AK, BK_, false>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch,
-                                   grp, wq, lane);
-#else
         stage_tile<AK, BK_, RD>(g, A, B, m0, n0, kbeg + (kt + 1) * BK, lds + (cur ^ 1) * pitch,
                                 grp, wq, lane);
-#endif
         if constexpr (F8 == 2)
           stage_scales(g, m0, n0, kbeg / BK + kt + 1, lds + MX_SC_OFF + (cur ^ 1) * 2048, grp, wq,
                        lane);
@@ -399,16 +392,9 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
           for (int j = 0; j < 4; ++j) {
             const bf16x8 a2[2] = {fa[i][0], fa[i][1]};
             const bf16x8 b2[2] = {fb[j][0], fb[j][1]};
-#ifdef IRC_MX_NO_OPSEL  // A/B build: bytes extracted by shifts instead of op_sel
-            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                __builtin_bit_cast(v8i32, a2), __builtin_bit_cast(v8i32, b2), acc[i][j], 0, 0, 0,
-                (int)(((i < 4 ? xa.x : xa.y) >> (8 * (i & 3))) & 0xffu), 0,
-                (int)((xb >> (8 * j)) & 0xffu));
-#else  // op_sel picks byte (i & 3) / j of the packed scale registers
             acc[i][j] = mfma_mx_sel(i & 3, j, __builtin_bit_cast(v8i32, a2),
                                     __builtin_bit_cast(v8i32, b2), acc[i][j],
                                     (int)(i < 4 ? xa.x : xa.y), (int)xb);
-#endif
           }
       } else if constexpr (F8) {
 #pragma unroll
@@ -443,14 +429,8 @@ __device__ __forceinline__ void mainloop(const PArgs& g, const unsigned short* A
       // for it after the loop: group 0's last barrier above already follows group
       // 1's last fragment reads, so group 0 starts its epilogue while group 1's last
       // 64 MFMAs run (one barrier fewer for each group keeps the counts matched).
-#ifdef IRC_PP_LAST_BARRIER  // A/B build: both groups meet after the last M section
-      wg_barrier();
-    }
-    if (grp == 0) wg_barrier();
-#else
       if (!(grp == 1 && kt == nk - 1)) wg_barrier();
     }
-#endif
   }
 }
 
@@ -505,58 +485,6 @@ __device__ __forceinline__ void epilogue_vec(const PArgs& g, const f32x4 (&acc)[
           sav[i][e] = (g.sa != nullptr && row < g.M) ? g.sa[row] : 1.f;
         }
     }
-#ifdef IRC_PP_B16_STAGE
-    // bf16 outputs without a residual: stage the rounded values as bf16 (half the LDS bytes;
-    // the neighbour-lane swap pairs two columns of a row into one 4-byte store), then read
-    // whole 16-byte row pieces: the same RNE rounding, bit-identical C
-    constexpr bool B16 = sizeof(TO) == 2 && F8 == 0 && !LN &&
-                         (EPI == EPI_NONE || EPI == EPI_BIAS || EPI == EPI_BIAS_GELU);
-    if constexpr (B16) {
-      constexpr int BP = 72;  // u16 row pitch: rows 4 apart 16 banks apart
-      unsigned short* stb = reinterpret_cast<unsigned short*>(lds) + wave * (32 * BP);
-      unsigned short* C = reinterpret_cast<unsigned short*>(g.C) + batch * g.sC;
-      const int odd = lane & 1;
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            f32x2 v[2];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e >> 1][e & 1] = acc[2 * p + ii][j][e] * alpha + bv[j];
-            if (EPI == EPI_BIAS_GELU) {
-              v[0] = gelu_lite2(v[0]);
-              v[1] = gelu_lite2(v[1]);
-            }
-#pragma unroll
-            for (int e2 = 0; e2 < 2; ++e2) {
-              typedef __bf16 bf16x2_s __attribute__((ext_vector_type(2)));
-              const uint32_t w = __builtin_bit_cast(uint32_t, __builtin_convertvector(v[e2], bf16x2_s));
-              const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false);
-              const uint32_t o2 = odd ? ((x >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (x << 16));
-              const int rl = 16 * ii + 4 * (lane >> 4) + 2 * e2 + odd;
-              *reinterpret_cast<uint32_t*>(&stb[rl * BP + 16 * j + (lane & 14)]) = o2;
-            }
-          }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const int rbase = rbase0 + 32 * p;
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-          const int c = it * 64 + lane;
-          const int rl = c >> 3, c8 = (c & 7) * 8;
-          const int row = rbase + rl, col = cbase + c8;
-          if (row >= g.M || col >= g.N) continue;
-          *reinterpret_cast<u16x8*>(C + (int64_t)row * g.ldc + col) =
-              *reinterpret_cast<const u16x8*>(&stb[rl * BP + c8]);
-        }
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-      return;
-    }
-#endif
 #pragma unroll
     for (int p = 0; p < 4; ++p) {  // 32-row passes
 #pragma unroll
@@ -970,15 +898,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
   // trainable encoder read 3.4-5x their operand bytes from HBM when the slices of a run
   // spread over every XCD, profiles/r04_h_pmc_shapes_bert.txt)
   int bid, batch, split;
-#ifdef IRC_PP_OLD_REMAP  // A/B build: the remap over blockIdx.x alone (rounds 2-3)
-  bid = blockIdx.x;
-  {
-    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-  }
-  batch = blockIdx.y;
-  split = blockIdx.z;
-#else
   {
     const int nz = gridDim.y * gridDim.z;
     const int total = ntiles * nz;
@@ -990,7 +909,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_pp_kernel(PArgs g) {
     split = rest % gridDim.z;
     batch = rest / gridDim.z;
   }
-#endif
   // EPI_SCAN: query tiles fastest, so the blocks of one doc tile run back to back
   // on one XCD and read it from that XCD's L2 (C4: 2048 queries = 8 query tiles)
   int tm, tn;

@@ -106,9 +106,7 @@ __device__ __forceinline__ void sweep(F addr, unsigned epoch, unsigned (&v)[N], 
       }
       return;
     }
-#ifndef IRC_COOP_SWEEP_NOSLEEP
     __builtin_amdgcn_s_sleep(1);
-#endif
   }
 }
 
@@ -622,11 +620,6 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
           for (int i = 0; i < 4; ++i) dh[rb][i] += __uint_as_float(v[mm][rb][i]);
       }
     }
-#ifdef IRC_COOP_DG_LATE
-    // the previous step's dg rows leave after this step's hand-off, so the publish's
-    // vmcnt(0) does not wait for them (diagnostic build)
-    if (s > 0) store_dg(dir == 0 ? t + 1 : t - 1);
-#endif
     __syncthreads();  // all reads of dgl (MFMA) done before it is overwritten
     if (abort_lds) return;
 #pragma unroll
@@ -647,13 +640,8 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
       }
     }
     __syncthreads();  // own dgates complete: next step's A operand, and the dg rows
-#ifndef IRC_COOP_DG_LATE
     store_dg(t);
-#endif
   }
-#ifdef IRC_COOP_DG_LATE
-  store_dg(dir == 0 ? 0 : L - 1);
-#endif
 }
 
 // W_hh [ndir][4H][H] fp32 -> the resident slices of both recurrences (bf16).

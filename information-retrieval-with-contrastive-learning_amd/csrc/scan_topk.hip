@@ -36,12 +36,7 @@
 // wave holds tile it's A fragments in registers (one extra barrier), so NBUF tiles
 // are in flight during the MFMAs and the epilogue instead of NBUF - 1 (0: the
 // round-2 order, the next DMA at the top of each iteration).
-#ifndef IRC_SCAN_EARLY_ISSUE
 #define IRC_SCAN_EARLY_ISSUE 1
-#endif
-#ifndef IRC_SCAN_GENERAL_SELECT
-#define IRC_SCAN_GENERAL_SELECT 0  // A/B builds: 1 = region selects without select_fast
-#endif
 
 namespace irc {
 namespace scan {
@@ -228,11 +223,7 @@ void scan_tile_kernel(
   // LTOP list (descending; 0 = empty slot: real keys are >= 1) and the float
   // prefilter of its last slot
   uint64_t lt0 = 0, lt1 = 0, lt2 = 0, lt3 = 0;
-#ifdef IRC_LTOP_NOCAND  // diagnostic: the LTOP kernel with no candidate ever
-  float ltf = __builtin_huge_valf();
-#else
   float ltf = q < Q ? -__builtin_huge_valf() : __builtin_huge_valf();
-#endif
   const uint64_t qthr = (MODE == KEYS && thr != nullptr && q < Q) ? thr[q] : 0ull;
   const uint32_t qthr_hi = (uint32_t)(qthr >> 32);
   const float qtf = q >= Q ? __builtin_huge_valf()
@@ -334,17 +325,13 @@ void scan_tile_kernel(
       }
       reinterpret_cast<f32x4*>(s1)[0] = o0;
       reinterpret_cast<f32x4*>(s1)[1] = o1;
-#ifndef IRC_SCAN_XCHG_NOWAIT
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the raw barrier does not wait
-#endif
       wg_barrier();
       k0 += reinterpret_cast<const f32x4*>(s2)[0];
       k1 += reinterpret_cast<const f32x4*>(s2)[1];
       const f32x4 keep = (kh & 1) ? k1 : k0;
       reinterpret_cast<f32x4*>(s2)[0] = (kh & 1) ? k0 : k1;
-#ifndef IRC_SCAN_XCHG_NOWAIT
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
       wg_barrier();
       const f32x4 fq = keep + reinterpret_cast<const f32x4*>(s3)[0];
       // the finished quarter kh (rows of registers 4 kh .. 4 kh + 3) in registers 0-3
@@ -1029,7 +1016,7 @@ __device__ __forceinline__ void select_body(Src src, int k, int mode,
   STAMP(mode, 1);
   SEL_STOP(1);
   if constexpr (Src::kRegions) {
-    if (table && staged && !IRC_SCAN_GENERAL_SELECT) {
+    if (table && staged) {
       select_fast<Src, BIGK>(src, q, k, mode, M, rid, roff,
                              reinterpret_cast<uint32_t*>(stage), cand, &s_mm[0][0], s_misc,
                              &s_coll, thr_out, out_score, out_idx, smul);
@@ -2501,9 +2488,6 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
     if ((rc = check_launch("gemm_pp_kernel(scan)"))) return rc;
     const RegionSource s2 = region_source(keys, cnt, p.pp_G, p.pp_qpad, p.pp_cap, 1);
     launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
-#ifdef IRC_SCAN_DOUBLE_SELECT  // diagnostic: the same (idempotent) select again, I-cache warm
-    launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
-#endif
     return check_launch("select_kernel(final)");
   }
   prof_begin(st);
@@ -2513,9 +2497,6 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
   if (rc) return rc;
   const RegionSource s2 = region_source(keys, cnt, p.g_f, p.qpad, p.cap_f, 2 * p.ks);
   launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
-#ifdef IRC_SCAN_DOUBLE_SELECT
-  launch_select(s2, (int)Q, (int)k, SEL_FINAL, nullptr, out_score, out_idx, smul, st);
-#endif
   return check_launch("select_kernel(final)");
 }
 
