@@ -31,6 +31,7 @@ import yaml  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--by-len", action="store_true")
     a = ap.parse_args()
     import e2e_train as E
     import bench
@@ -65,7 +66,7 @@ def main():
         sels.append((idx, sel))
         if len(sels) >= 200:
             break
-    fixed_ids, fixed_mask = corpus.batch(sels[0][1])
+    fixed = list(corpus.batch(sels[0][1]))
     syn_ids, syn_mask = bench.synthetic_batch(512, 64, 1337)
     syn_ids, syn_mask = syn_ids.to(dev), syn_mask.to(dev)
     B = 256
@@ -91,7 +92,7 @@ def main():
 
         def issue(b):
             if kind == "fixed":
-                return model.bert_extract_async(fixed_ids, fixed_mask, B, inputs_ready=True)
+                return model.bert_extract_async(fixed[0], fixed[1], B, inputs_ready=True)
             if kind == "synth":
                 return model.bert_extract_async(syn_ids, syn_mask, B, inputs_ready=True)
             return model.bert_extract_corpus_async(corpus, b[1], B)
@@ -110,6 +111,21 @@ def main():
         model.features_ready(pending)
         return (time.perf_counter() - t0) * 1e3 / n
 
+    if a.by_len:
+        # real corpus batches grouped by their padded L, against synthetic batches of
+        # the same L (token ids uniform, lengths uniform in [10, L]): data vs length
+        by_len = {}
+        for idx, sel in sels:
+            ids, mask = corpus.batch(sel)
+            by_len.setdefault(ids.shape[1], (ids, mask))
+        for L in sorted(by_len):
+            sids, smask = bench.synthetic_batch(512, L, 1337)
+            for name, (i_, m_) in (("real", by_len[L]), ("synth", (sids.to(dev), smask.to(dev)))):
+                fixed[0], fixed[1] = i_, m_
+                ms = run("fixed", a.steps)
+                print(f"L={L:3d} {name:5s} {ms:7.3f} ms/step  {256 / ms * 1e3:8.0f} pairs/s",
+                      flush=True)
+        return
     for rep in range(2):
         for kind in ("loop", "loop+q", "presel", "fixed", "synth"):
             ms = run(kind, a.steps)
