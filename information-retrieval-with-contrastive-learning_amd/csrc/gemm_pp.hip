@@ -1296,12 +1296,18 @@ bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, i
   // both operands K-outer with a small output (split-K slab traffic dominates):
   // the 128x128 kernel's smaller slabs are faster
   if (la == 1 && lb == 1 && ((M + 255) / 256) * ((N + 255) / 256) * batch < 16) return false;
-  // Wave quantisation on 256 CUs: where the 256x384 big-tile kernel fills whole
-  // waves and 256x256 tiles do not (N = 768 / 2304 at M = 32768), it wins.
+  // Wave quantisation on the CUs: the 256x384 big-tile kernel wins where its waves
+  // cost less than the 256x256 tiles' -- one big tile is 1.5 of them (N = 768 / 2304
+  // at M = 512 L: 252 big tiles in one wave against 378 in two at L = 63; a batch's
+  // joint padding rarely lands on L = 64, and requiring whole waves of big tiles sent
+  // every other L to 1.5 waves of 256x256 tiles: 9.29 vs 8.18 ms per C2 step).  Ties
+  // go to the 256x256 kernel (FFN1's N = 3072).
   if (la == 0 && lb == 0 && N % 384 == 0) {
     const int64_t t384 = ((M + 255) / 256) * (N / 384) * batch;
     const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
-    if (t384 % 256 == 0 && t256 % 256 != 0) return false;
+    int64_t ncu = cu_count();
+    if (ncu <= 0) ncu = 256;
+    if (3 * ((t384 + ncu - 1) / ncu) < 2 * ((t256 + ncu - 1) / ncu)) return false;
   }
   if ((uintptr_t)A % 16 || (uintptr_t)B % 16) return false;
   if (lda % 8 || ldb % 8 || sA % 8 || sB % 8) return false;
