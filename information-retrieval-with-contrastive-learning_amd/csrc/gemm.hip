@@ -421,6 +421,99 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restr
   *dst = accumulate ? *dst + v : v;
 }
 
+// Wave-remainder epilogue: C = epi(alpha * sum_s P[s]) over the remainder rows of a GEMM
+// whose full waves ran as their own launch (remainder_split below), P the split-K
+// slabs [S][M][N] fp32, summed in slab order (deterministic).  The epilogues are the
+// big-tile kernel's (bf16 GELU: gelu_lite, fp32: gelu_fast).
+template <typename TO, int EPI>
+__global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict__ P, int S,
+                                                        int M, int N, float alpha,
+                                                        const float* __restrict__ bias,
+                                                        void* R, int64_t ldr, TO* C,
+                                                        int64_t ldc, int accumulate) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t mn = (int64_t)M * N;
+  if (e >= mn) return;
+  const int row = (int)(e / N), col = (int)(e % N);
+  float s = 0.f;
+  for (int k = 0; k < S; ++k) s += P[k * mn + e];
+  float v = s * alpha + (epi_has_bias(EPI) ? bias[col] : 0.f);
+  if (EPI == EPI_BIAS_GELU) v = sizeof(TO) == 2 ? gelu_lite(v) : gelu_fast(v);
+  if (EPI == EPI_BIAS_GELU_SAVE) {
+    TO* pre = static_cast<TO*>(R) + (int64_t)row * ldr + col;
+    if constexpr (sizeof(TO) == 2)
+      *reinterpret_cast<unsigned short*>(pre) = f32_to_bf16(v);
+    else
+      *reinterpret_cast<float*>(pre) = v;
+    v = gelu_fast(v);
+  }
+  if (EPI == EPI_BIAS_RESID || EPI == EPI_RESID || EPI == EPI_DGELU) {
+    float r;
+    if constexpr (sizeof(TO) == 2)
+      r = bf16_to_f32(static_cast<const unsigned short*>(R)[(int64_t)row * ldr + col]);
+    else
+      r = static_cast<const float*>(R)[(int64_t)row * ldr + col];
+    v = EPI == EPI_DGELU ? v * gelu_grad_fast(r) : v + r;
+  }
+  TO* dst = C + (int64_t)row * ldc + col;
+  if constexpr (sizeof(TO) == 2) {
+    *reinterpret_cast<unsigned short*>(dst) = f32_to_bf16(v);
+  } else {
+    float* d = reinterpret_cast<float*>(dst);
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+// Wave remainder of a bf16 GEMM with batch 1 and row-major A (every BERT / LSTM-head
+// linear layer: M = tokens).  Output tiles are 256 rows high, so at M = B L for L just
+// above a multiple of 256 / B (a batch jointly padded to L = 65: 260 tiles of 256 x 384
+// on 256 CUs) the last wave runs a handful of tiles on a nearly idle chip.  Priced in
+// 256x256-tile times per CU (a 256 x 384 tile = 1.5), the plain launch costs
+// ceil(tiles / CUs) waves; the split form runs the rows of the full waves as one
+// launch and the remaining rows as a split-K launch spread over the chip (raw fp32
+// slabs) plus one reduce pass applying the epilogue (~0.5 of a tile time).  Returns
+// the rows of the full-wave launch (0: no split) and the remainder's split count.
+struct RemSplit {
+  int64_t M1 = 0;
+  int splits = 1;
+};
+inline RemSplit remainder_split(int64_t M, int64_t N, int64_t K) {
+  RemSplit best;
+  if (K % 64 != 0 || K < 256 || M < 512) return best;
+  const int64_t ncu = gpp::device_cu_count();
+  const int64_t mt = (M + 255) / 256;
+  double plain = 1e30, split = 1e30;
+  int64_t m1 = 0;
+  for (int wide = 0; wide < 2; ++wide) {
+    if (wide && N % 384 != 0) continue;
+    const int64_t nt = wide ? N / 384 : (N + 255) / 256;
+    const double c = wide ? 1.5 : 1.0;
+    const int64_t tiles = mt * nt;
+    const double p = (double)((tiles + ncu - 1) / ncu) * c;
+    if (p < plain) plain = p;
+    const int64_t full = tiles / ncu;
+    if (full < 1) continue;
+    const int64_t rows = (full * ncu / nt) * 256;  // whole row tiles of the full waves
+    if (rows <= 0 || rows >= M) continue;
+    const double rem_tiles = (double)((M - rows + 255) / 256) * nt;
+    const double sp = (double)full * c + rem_tiles * c / (double)ncu + 0.5;
+    if (sp < split) {
+      split = sp;
+      m1 = rows;
+    }
+  }
+  if (split >= plain) return best;
+  best.M1 = m1;
+  const int64_t tiles2 = ((M - m1 + 255) / 256) * ((N + 255) / 256);
+  int64_t s = ncu / (tiles2 > 0 ? tiles2 : 1);
+  const int64_t smax = K / 128;  // >= 2 K-tiles per slab
+  if (s > smax) s = smax;
+  if (s < 1) s = 1;
+  const int64_t chunk = ((K + s - 1) / s + 63) / 64 * 64;
+  best.splits = (int)((K + chunk - 1) / chunk);
+  return best;
+}
+
 // Split-K count: only when the output tile grid cannot fill the chip and each
 // slice keeps >= 512 of K (bf16) / >= 128 of K (fp32: the exact-fp32 MFMA runs at
 // 1/16 of the bf16 rate, so a 128-deep slice is already 8 K-steps of real work --
@@ -480,17 +573,21 @@ __device__ __forceinline__ int chunk_key(int r) {
   return (r >> 1) & 7;
 }
 
-// rows [0, nrows_tile) of one operand tile: nrows_tile*8 16-byte chunks, NT per pass
+// rows [0, nrows_tile) of one operand tile: nrows_tile*8 16-byte chunks, NT per pass.
+// ls > 0 (the sequence-slot layout of qkv_attn_kernel): tile row t is token
+// min(t & 63, ls - 1) of sequence r0 / 64 + t / 64, sequences of ls rows stored
+// contiguously (r0 a multiple of 64); ls = 0: tile row t is row r0 + t.
 template <int ROWS>
 __device__ __forceinline__ void stage(const unsigned short* __restrict__ X, int64_t ld, int r0,
-                                      int nrows, int k0, char* lds_tile, int wave, int lane) {
+                                      int nrows, int k0, char* lds_tile, int wave, int lane,
+                                      int ls = 0) {
   constexpr int PASSES = ROWS * 8 / NT;
 #pragma unroll
   for (int i = 0; i < PASSES; ++i) {
     const int p = (i * NW + wave) * 64 + lane;  // 16-byte LDS chunk index (lane-linear)
     const int row = p >> 3;
     const int c = (p & 7) ^ chunk_key(row);     // logical k-chunk stored at this slot
-    int gr = r0 + row;
+    int gr = ls == 0 ? r0 + row : ((r0 >> 6) + (row >> 6)) * ls + min(row & 63, ls - 1);
     gr = gr < nrows ? gr : nrows - 1;
     glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
   }
@@ -577,16 +674,17 @@ __device__ uint64_t big_stamps[64][5][2];
 // (lane & 15)].  The chunk key (r >> 1) & 7 stays conflict free for the 16x16x32 fragment
 // reads (lane l: row l & 15, chunk 4 s + (l >> 4): each 16-lane group covers 16 distinct
 // 16-byte bank slots).  Ends with every wave past its last LDS read (LDS free).
+// ls > 0: A rows in the sequence-slot layout of stage() (qkv_attn_kernel at L = ls < 64).
 template <int WNB>
 __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t lda,
                                               const unsigned short* B, int64_t ldb, int m0,
                                               int n0, int M, int N, int K, char* lds, int wave,
-                                              int lane, f32x4 (&acc4)[8][2 * WNB]) {
+                                              int lane, f32x4 (&acc4)[8][2 * WNB], int ls = 0) {
   constexpr int BN = 128 * WNB;
   constexpr int A_BYTES = BM * ROW_BYTES, STAGE = A_BYTES + BN * ROW_BYTES;
   const int wm = wave >> 2, wn = wave & 3;
   const int nk = K / BK;
-  stage<BM>(A, lda, m0, M, 0, lds, wave, lane);
+  stage<BM>(A, lda, m0, M, 0, lds, wave, lane, ls);
   stage<BN>(B, ldb, n0, N, 0, lds + A_BYTES, wave, lane);
   wait_vmcnt<0>();
   __syncthreads();
@@ -606,7 +704,7 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
       // would push the 16x16 fragments into spills)
       int ln = lane;
       asm volatile("" : "+v"(ln));
-      stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln);
+      stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln, ls);
       stage<BN>(B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
     }
     BSTAMP(kt, 1);
@@ -1054,10 +1152,13 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 
 // ---------------------------------------------------------------------------
 // QKV projection + self-attention in one launch: the frozen encoder's BertSelfAttention
-// (modeling_bert, reached from contrastive_module.py:36-41) at L = 64, head dim 64.
+// (modeling_bert, reached from contrastive_module.py:36-41) at L <= 64, head dim 64.
 // The Wqkv rows are permuted so that output tile column block n (384 wide) holds
 // [Q | K | V] of heads 2n and 2n + 1 (64 columns each), and a 256-row tile holds four
-// whole sequences; the QKV activation then never leaves the CU.  Main loop: the big-tile
+// whole sequences, each in a 64-row slot (L < 64, the joint padding of a batch: the
+// slot's rows past L repeat token L - 1, their keys carry the -3e30 past-L bias and
+// their queries are never stored, as in attention_mfma_kernel); the QKV activation
+// then never leaves the CU.  Main loop: the big-tile
 // kernel's 16x16x32 2-slot loop (WNB = 3).  Epilogue, per 128-row half (the waves with
 // wm == half own its accumulators): those 4 waves write bf16(acc + bias) into LDS
 // [128][392] (the same bf16 values the unfused GEMM stores), then all 8 waves run its
@@ -1073,11 +1174,12 @@ struct QaArgs {
   const unsigned short* x;  // [M][K] layer input
   const unsigned short* w;  // [3H][K] head-pair-permuted Wqkv
   const float* bias;        // [3H] permuted bias
-  const int64_t* mask;      // [M / 64][64], nonzero = key visible; null = all visible
+  const int64_t* mask;      // [M / L][L], nonzero = key visible; null = all visible
   unsigned short* ctx;      // [M][H] (row stride ldc)
   int M, K, H;
   int64_t ldx, ldc;
   float scale;
+  int L;                    // sequence length, 1..64 (one 64-row slot per sequence)
 };
 
 __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
@@ -1085,7 +1187,9 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
   __shared__ __attribute__((aligned(1024))) char lds[2 * (BM + BN) * big::ROW_BYTES];
   static_assert(128 * TP * 2 + 8 * 64 * 4 <= 2 * (BM + BN) * big::ROW_BYTES,
                 "staged half and mask biases fit the LDS");
-  const int tiles_m = (g.M + BM - 1) / BM;
+  const int nseq = g.M / g.L;
+  const int ls = g.L == 64 ? 0 : g.L;  // 0: contiguous rows (slots are the sequences)
+  const int tiles_m = (nseq + 3) / 4;
   const int tiles_n = 3 * g.H / BN;
   const int ntiles = tiles_m * tiles_n;
   int bid = blockIdx.x;
@@ -1104,7 +1208,8 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 2 * WNB; ++j) acc4[i][j] = (f32x4)0.0f;
-  big::mainloop_mf16<WNB>(g.x, g.ldx, g.w, g.K, m0, n0, g.M, 3 * g.H, g.K, lds, wave, lane, acc4);
+  big::mainloop_mf16<WNB>(g.x, g.ldx, g.w, g.K, m0, n0, g.M, 3 * g.H, g.K, lds, wave, lane, acc4,
+                          ls);
 
   unsigned short* T = reinterpret_cast<unsigned short*>(lds);    // [128][TP] staged half
   float* mbw = reinterpret_cast<float*>(lds + 128 * TP * 2) + 64 * wave;  // this wave's mask bias
@@ -1154,9 +1259,11 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
     // every wave: queries [32 wm, +32) of (sequence wn >> 1, head 2 tn + (wn & 1)) of
     // this half (the other half's waves hold their packed values meanwhile)
     const int sl = wn >> 1, hh = wn & 1;
-    const int r0 = m0 + 128 * hf + 64 * sl;  // first token of the sequence
-    if (r0 < g.M) {
-      mbw[lane] = (g.mask == nullptr || g.mask[r0 + lane] != 0) ? 0.f : -1e30f;
+    const int seq = 4 * tm + 2 * hf + sl;
+    const int r0 = seq * g.L;  // first token of the sequence
+    if (seq < nseq) {
+      mbw[lane] = lane >= g.L ? -3e30f
+                              : ((g.mask == nullptr || g.mask[r0 + lane] != 0) ? 0.f : -1e30f);
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const unsigned short* Ts = T + 64 * sl * TP;
@@ -1236,7 +1343,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int i = 32 * ib + (e & 3) + 8 * (e >> 2) + 4 * h;
-            out[(int64_t)i * g.ldc + 32 * db + r32] = f32_to_bf16(o[db][e]);
+            if (i < g.L) out[(int64_t)i * g.ldc + 32 * db + r32] = f32_to_bf16(o[db][e]);
           }
       }
     }
@@ -1368,7 +1475,15 @@ extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue,
     const int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch);
     if (sp > s) s = sp;
   }
-  return s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
+  int64_t bytes = s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
+  if (in_dtype == 0 && batch == 1 && pp_enabled()) {  // the wave-remainder split's slabs
+    const gemm::RemSplit r = gemm::remainder_split(M, N, K);
+    if (r.M1 > 0) {
+      const int64_t rb = (int64_t)r.splits * (M - r.M1) * N * (int64_t)sizeof(float);
+      if (rb > bytes) bytes = rb;
+    }
+  }
+  return bytes;
 }
 
 // LayerNorm-fold GEMM of the BERT encoder (include/irc.h irc_gemm_ln): bf16 A [M][K],
@@ -1438,24 +1553,24 @@ extern "C" int irc_gemm_ln(int epilogue, int64_t M, int64_t N, int64_t K, const 
 }
 
 // QKV projection + attention in one launch (include/irc.h irc_qkv_attention; see
-// qkv_attn_kernel): L = 64, head dim 64, H % 128 == 0.
+// qkv_attn_kernel): L <= 64, head dim 64, H % 128 == 0.
 extern "C" int irc_qkv_attention(int64_t M, int64_t H, int64_t heads, int64_t L, const void* x,
                                  int64_t ldx, const void* wqkv_perm, const float* bias_perm,
                                  const int64_t* mask, void* ctx, int64_t ldc,
                                  irc_stream_t stream) {
   using namespace irc::gemm;
-  IRC_REQUIRE(L == 64 && heads * 64 == H && H % 128 == 0,
-              "qkv_attention: needs L = 64, head dim 64 and H %% 128 == 0");
-  IRC_REQUIRE(M > 0 && M % 64 == 0 && M < (1ll << 31), "qkv_attention: M must be a multiple of L");
+  IRC_REQUIRE(L >= 1 && L <= 64 && heads * 64 == H && H % 128 == 0,
+              "qkv_attention: needs L <= 64, head dim 64 and H %% 128 == 0");
+  IRC_REQUIRE(M > 0 && M % L == 0 && M < (1ll << 31), "qkv_attention: M must be a multiple of L");
   IRC_REQUIRE(H % 64 == 0 && ldx % 8 == 0 && ldx >= H && ldc >= H, "qkv_attention: bad strides");
   IRC_REQUIRE((((uintptr_t)x | (uintptr_t)wqkv_perm) % 16) == 0 && ((uintptr_t)ctx % 2) == 0,
               "qkv_attention: operands must be 16-byte aligned");
   IRC_REQUIRE(bias_perm != nullptr, "qkv_attention: bias required");
   QaArgs a{static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(wqkv_perm),
            bias_perm, mask, static_cast<unsigned short*>(ctx), (int)M, (int)H, (int)H, ldx, ldc,
-           0.125f};
+           0.125f, (int)L};
   hipStream_t st = as_stream(stream);
-  const int tiles = (int)((M + big::BM - 1) / big::BM) * (int)(3 * H / 384);
+  const int tiles = (int)((M / L + 3) / 4) * (int)(3 * H / 384);
   prof_begin(st);
   hipLaunchKernelGGL(qkv_attn_kernel, dim3(tiles), dim3(big::NT), 0, st, a);
   // a GEMM with an attention epilogue: its flops and bytes (x, Wqkv, ctx) count as one
@@ -1525,6 +1640,56 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
                gemm_group_m()};
   hipStream_t st = as_stream(stream);
   const int nb = (int)batch;
+  if (in_dtype == 0 && batch == 1 && a_layout == gemm::ROW && pp_enabled() && vec_a && vec_b &&
+      vec_c) {
+    // wave remainder: the full waves' rows, then the rest as split-K + epilogue pass
+    const gemm::RemSplit r = gemm::remainder_split(M, N, K);
+    const int64_t M2 = M - r.M1;
+    const int64_t need = (int64_t)r.splits * M2 * N * (int64_t)sizeof(float);
+    if (r.M1 > 0 && r.splits > 1 && workspace != nullptr && workspace_bytes >= need &&
+        lda % 8 == 0 && ldb % 8 == 0 && (b_layout == gemm::ROW || N % 8 == 0)) {
+      const int es = out_dtype == 0 ? 2 : 4;
+      int rc = irc_gemm(in_dtype, out_dtype, a_layout, b_layout, epilogue, r.M1, N, K, alpha, A,
+                        lda, 0, B, ldb, 0, bias, 0, R, ldr, 0, C, ldc, 0, accumulate, 1, nullptr,
+                        0, stream);
+      if (rc) return rc;
+      const unsigned short* A2 = static_cast<const unsigned short*>(A) + r.M1 * lda;
+      char* C2 = static_cast<char*>(C) + r.M1 * ldc * es;
+      void* R2 = R ? static_cast<char*>(const_cast<void*>(R)) + r.M1 * ldr * es : nullptr;
+      gpp::PArgs pa{A2, static_cast<const unsigned short*>(B), nullptr, nullptr, nullptr,
+                    static_cast<float*>(workspace), (int)M2, (int)N, (int)K,
+                    (int)(((K + r.splits - 1) / r.splits + 63) / 64 * 64), lda, ldb, N, 0, 0, 0,
+                    0, 0, 0, 1.0f, 0, 1};
+      pa.group_m = gemm_group_m();
+      prof_begin(st);
+      gpp::run(1, 0, b_layout, 0, pa, 1, r.splits, st);
+      const dim3 g2((unsigned)((M2 * N + 255) / 256));
+      const float* P = static_cast<const float*>(workspace);
+#define IRC_REMEPI(TO, E)                                                                     \
+  case E:                                                                                     \
+    hipLaunchKernelGGL((gemm::splitk_epi_kernel<TO, E>), g2, dim3(256), 0, st, P, r.splits,   \
+                       (int)M2, (int)N, alpha, bias, R2, ldr, reinterpret_cast<TO*>(C2), ldc, \
+                       accumulate);                                                           \
+    break;
+      if (out_dtype == 0) {
+        switch (epilogue) {
+          IRC_REMEPI(unsigned short, 0) IRC_REMEPI(unsigned short, 1)
+          IRC_REMEPI(unsigned short, 2) IRC_REMEPI(unsigned short, 3)
+          IRC_REMEPI(unsigned short, 4) IRC_REMEPI(unsigned short, 5)
+          IRC_REMEPI(unsigned short, 6)
+        }
+      } else {
+        switch (epilogue) {
+          IRC_REMEPI(float, 0) IRC_REMEPI(float, 1) IRC_REMEPI(float, 2) IRC_REMEPI(float, 3)
+          IRC_REMEPI(float, 4) IRC_REMEPI(float, 5) IRC_REMEPI(float, 6)
+        }
+      }
+#undef IRC_REMEPI
+      prof_end("gemm_bf16", st, 2.0 * M2 * N * K);
+      prof_work("gemm_bf16_bytes", gemm::gemm_alg_bytes(out_dtype, epilogue, accumulate, M2, N, K, 1));
+      return check_launch("gemm remainder");
+    }
+  }
   if (in_dtype == 0 && pp_enabled()) {
     int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch);
     if (sp > 1 && (workspace == nullptr ||

@@ -87,6 +87,8 @@ struct PArgs {
 constexpr int EPI_SCAN = 7;
 
 int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t batch);
+// CUs of the current device (256 when the query fails)
+int device_cu_count();
 bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                int64_t sA, const void* B, int64_t ldb, int64_t sB, int64_t batch, int splits);
 void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, int splits,

@@ -1274,6 +1274,11 @@ static void launch_layout(int la, int lb, int epi, const PArgs& a, dim3 grid, hi
 namespace irc {
 namespace gpp {
 
+int device_cu_count() {
+  const int n = cu_count();
+  return n > 0 ? n : 256;
+}
+
 // Split count: fill (at most) one wave of 256 blocks when the output tile grid
 // alone cannot (fp32 C, no fused epilogue), each K slice >= 1024 deep.
 int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t batch) {

@@ -313,7 +313,8 @@ class BertModel(nn.Module):
 
     def _qkv_attention(self, x, lw, mask, B, L, H, heads):
         """ctx of one layer: one fused launch where it applies, else QKV GEMM + attention."""
-        if self.fused_attention and ops.qkv_attention_supported(L, H, heads):
+        if self.fused_attention and ops.qkv_attention_supported(L, H, heads,
+                                                                ops.QKV_ATTN_MIN_L):
             if "wqkv_p" not in lw:  # permuted once per cast weight set
                 perm = ops.qkv_perm_index(H, lw["wqkv"].device)
                 lw["wqkv_p"] = lw["wqkv"].index_select(0, perm).contiguous()

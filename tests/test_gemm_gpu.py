@@ -471,3 +471,34 @@ def test_pp_persistent_bert_shapes(gpu, b_is_nk):
         ops.gemm_set_persistent(prev)
     for o in outs:
         assert torch.equal(o, ref)
+
+
+@pytest.mark.parametrize("M,N,K,epi,odt,b_is_nk", [
+    (33280, 768, 768, 3, torch.bfloat16, True),    # out-proj at L = 65 (B = 512): 260 big tiles
+    (33280, 768, 3072, 3, torch.bfloat16, True),   # FFN2 at L = 65
+    (33280, 3072, 768, 2, torch.bfloat16, True),   # FFN1 + GELU at L = 65
+    (33280, 2304, 768, 1, torch.bfloat16, True),   # QKV at L = 65
+    (16640, 2048, 768, 1, torch.float32, True),    # LSTM input projection at L = 65 (B = 256)
+    (16640, 2048, 512, 0, torch.float32, False),   # K-outer B operand
+    (33792, 768, 768, 4, torch.float32, True),     # L = 66, residual only, fp32 out
+])
+def test_wave_remainder_split(gpu, M, N, K, epi, odt, b_is_nk):
+    """A GEMM whose last wave of output tiles would run nearly empty (M = B L just above
+    a multiple of the 256-row tiles per wave) runs as the full waves' rows plus a
+    split-K remainder with an epilogue pass (gemm.hip remainder_split); same op as the
+    fp32 reference, tolerances of test_epilogues, rows on both sides of the split."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(M + N + K + epi)
+    a = (torch.randn(M, K, generator=g) * 0.5).bfloat16()
+    b = (torch.randn((N, K) if b_is_nk else (K, N), generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, generator=g) if epi in (1, 2, 3) else None
+    res = torch.randn(M, N, generator=g).to(odt) if epi in (3, 4) else None
+    out = ops.gemm(a.to(gpu), b.to(gpu), b_is_nk=b_is_nk,
+                   bias=None if bias is None else bias.to(gpu), epilogue=epi,
+                   residual=None if res is None else res.to(gpu), out_dtype=odt, alpha=0.5)
+    rows = torch.cat([torch.arange(0, 300), torch.arange(32000, M)])
+    ref = _ref(a[rows], b, False, b_is_nk, bias, epi, None if res is None else res[rows], 0.5)
+    got = out.float().cpu()[rows]
+    rel = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert rel < (1e-2 if odt == torch.bfloat16 else 2e-3), rel

@@ -2,7 +2,8 @@
 form (irc_gemm EPI_BIAS + irc_attention) and a plain PyTorch fp32 reference.
 
 HF BertSelfAttention as the frozen encoder reaches it (contrastive_module.py:36-41 ->
-modeling_bert): softmax(Q K^T / 8 + (1 - mask) * min) V per head, head dim 64, L = 64.
+modeling_bert): softmax(Q K^T / 8 + (1 - mask) * min) V per head, head dim 64, L <= 64
+(one 64-row slot per sequence: the joint padding of a batch lands on any L).
 Where the unfused QKV GEMM runs on the same big-tile main loop (N = 3H = 2304 at
 M = 32768), the fused context must equal the unfused one bit for bit; elsewhere both are
 held to the fp32 reference (bf16 operands: the fused error within 1.5x of the unfused
@@ -59,9 +60,10 @@ def test_perm_index():
     assert p[640:768].tolist() == list(range(1536 + 128, 1536 + 256))
 
 
-@pytest.mark.parametrize("masked", [True, False])
-def test_bit_exact_on_big_tile_shape(gpu, masked):
-    B, L, H, heads = 512, 64, 768, 12
+@pytest.mark.parametrize("masked,L", [(True, 64), (False, 64), (True, 63), (True, 57),
+                                      (False, 61)])
+def test_bit_exact_on_big_tile_shape(gpu, masked, L):
+    B, H, heads = 512, 768, 12
     x, w, b, mask = _inputs(gpu, B, L, H, 5, masked)
     cf = _fused(x, w, b, mask, B, L, H, heads)
     cu = _unfused(x, w, b, mask, B, L, H, heads)
@@ -70,10 +72,13 @@ def test_bit_exact_on_big_tile_shape(gpu, masked):
     assert (cf.float() - ref).norm() / ref.norm() < 1e-2
 
 
-@pytest.mark.parametrize("B,H,heads", [(37, 768, 12), (4, 768, 12), (64, 1024, 16)])
-def test_against_reference(gpu, B, H, heads):
-    """Ragged last tile (B = 37: 2368 rows), a single partial tile, BERT-large width."""
-    L = 64
+@pytest.mark.parametrize("B,H,heads,L", [(37, 768, 12, 64), (4, 768, 12, 64), (64, 1024, 16, 64),
+                                         (37, 768, 12, 40), (5, 768, 12, 1), (64, 1024, 16, 50),
+                                         (300, 768, 12, 48), (9, 768, 12, 17)])
+def test_against_reference(gpu, B, H, heads, L):
+    """Ragged last tile (B = 37: 2368 rows), a single partial tile, BERT-large width;
+    L < 64 (slots with repeated last tokens: B = 37 at L = 40 leaves a 1-sequence last
+    tile, L = 1 a single key)."""
     x, w, b, mask = _inputs(gpu, B, L, H, B + H)
     cf = _fused(x, w, b, mask, B, L, H, heads).float()
     cu = _unfused(x, w, b, mask, B, L, H, heads).float()
@@ -87,17 +92,19 @@ def test_against_reference(gpu, B, H, heads):
 def test_rejects_unsupported(gpu):
     from irc_amd import ops
 
-    x, w, b, mask = _inputs(gpu, 4, 32, 768, 1)
+    x, w, b, mask = _inputs(gpu, 4, 65, 768, 1)
     with pytest.raises(ValueError):
-        _fused(x, w, b, mask, 4, 32, 768, 12)  # L = 32
+        _fused(x, w, b, mask, 4, 65, 768, 12)  # L = 65
     x, w, b, mask = _inputs(gpu, 4, 64, 768, 1)
     with pytest.raises(TypeError):
         ops.qkv_attention(x.float(), w, b, mask, 4, 64, 768, 12)
 
 
-def test_encoder_fused_matches_unfused(gpu):
+@pytest.mark.parametrize("L", [64, 61])
+def test_encoder_fused_matches_unfused(gpu, L):
     """The frozen encoder with the fused launch equals the two-launch encoder bit for bit
-    at B x L = 32768 (every QKV GEMM on the big-tile main loop)."""
+    at B = 512 (every QKV GEMM on the big-tile main loop), at L = 64 and at a joint
+    padding of 61 (slots)."""
     import dataclasses
 
     from irc_amd.bert import BERT_BASE, BertModel
@@ -105,7 +112,7 @@ def test_encoder_fused_matches_unfused(gpu):
     cfg = dataclasses.replace(BERT_BASE, num_hidden_layers=2)
     m = BertModel(cfg, seed=4).to(gpu)
     g = torch.Generator().manual_seed(2)
-    B, L = 512, 64
+    B = 512
     ids = torch.randint(1, cfg.vocab_size, (B, L), generator=g)
     lens = torch.randint(8, L + 1, (B,), generator=g)
     mask = (torch.arange(L)[None, :] < lens[:, None]).to(torch.int64)
