@@ -574,20 +574,21 @@ __device__ __forceinline__ int chunk_key(int r) {
 }
 
 // rows [0, nrows_tile) of one operand tile: nrows_tile*8 16-byte chunks, NT per pass.
-// ls > 0 (the sequence-slot layout of qkv_attn_kernel): tile row t is token
-// min(t & 63, ls - 1) of sequence r0 / 64 + t / 64, sequences of ls rows stored
-// contiguously (r0 a multiple of 64); ls = 0: tile row t is row r0 + t.
+// ls > 0 (the sequence-slot layout of qkv_attn_kernel, slots of 2^sh rows): tile row t
+// is token min(t mod 2^sh, ls - 1) of sequence (r0 + t) >> sh, sequences of ls rows
+// stored contiguously (r0 a multiple of 2^sh); ls = 0: tile row t is row r0 + t.
 template <int ROWS>
 __device__ __forceinline__ void stage(const unsigned short* __restrict__ X, int64_t ld, int r0,
                                       int nrows, int k0, char* lds_tile, int wave, int lane,
-                                      int ls = 0) {
+                                      int ls = 0, int sh = 6) {
   constexpr int PASSES = ROWS * 8 / NT;
 #pragma unroll
   for (int i = 0; i < PASSES; ++i) {
     const int p = (i * NW + wave) * 64 + lane;  // 16-byte LDS chunk index (lane-linear)
     const int row = p >> 3;
     const int c = (p & 7) ^ chunk_key(row);     // logical k-chunk stored at this slot
-    int gr = ls == 0 ? r0 + row : ((r0 >> 6) + (row >> 6)) * ls + min(row & 63, ls - 1);
+    int gr = ls == 0 ? r0 + row
+                     : ((r0 + row) >> sh) * ls + min(row & ((1 << sh) - 1), ls - 1);
     gr = gr < nrows ? gr : nrows - 1;
     glds16(X + (int64_t)gr * ld + k0 + c * 8, lds_tile + (i * NW + wave) * 1024);
   }
@@ -679,12 +680,13 @@ template <int WNB>
 __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t lda,
                                               const unsigned short* B, int64_t ldb, int m0,
                                               int n0, int M, int N, int K, char* lds, int wave,
-                                              int lane, f32x4 (&acc4)[8][2 * WNB], int ls = 0) {
+                                              int lane, f32x4 (&acc4)[8][2 * WNB], int ls = 0,
+                                              int sh = 6) {
   constexpr int BN = 128 * WNB;
   constexpr int A_BYTES = BM * ROW_BYTES, STAGE = A_BYTES + BN * ROW_BYTES;
   const int wm = wave >> 2, wn = wave & 3;
   const int nk = K / BK;
-  stage<BM>(A, lda, m0, M, 0, lds, wave, lane, ls);
+  stage<BM>(A, lda, m0, M, 0, lds, wave, lane, ls, sh);
   stage<BN>(B, ldb, n0, N, 0, lds + A_BYTES, wave, lane);
   wait_vmcnt<0>();
   __syncthreads();
@@ -704,7 +706,7 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
       // would push the 16x16 fragments into spills)
       int ln = lane;
       asm volatile("" : "+v"(ln));
-      stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln, ls);
+      stage<BM>(A, lda, m0, M, (kt + 1) * BK, nxt, wave, ln, ls, sh);
       stage<BN>(B, ldb, n0, N, (kt + 1) * BK, nxt + A_BYTES, wave, ln);
     }
     BSTAMP(kt, 1);
@@ -1152,13 +1154,13 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
 
 // ---------------------------------------------------------------------------
 // QKV projection + self-attention in one launch: the frozen encoder's BertSelfAttention
-// (modeling_bert, reached from contrastive_module.py:36-41) at L <= 64, head dim 64.
+// (modeling_bert, reached from contrastive_module.py:36-41) at L <= 128, head dim 64.
 // The Wqkv rows are permuted so that output tile column block n (384 wide) holds
-// [Q | K | V] of heads 2n and 2n + 1 (64 columns each), and a 256-row tile holds four
-// whole sequences, each in a 64-row slot (L < 64, the joint padding of a batch: the
-// slot's rows past L repeat token L - 1, their keys carry the -3e30 past-L bias and
-// their queries are never stored, as in attention_mfma_kernel); the QKV activation
-// then never leaves the CU.  Main loop: the big-tile
+// [Q | K | V] of heads 2n and 2n + 1 (64 columns each), and a 256-row tile holds whole
+// sequences, each in a slot of SL rows: four of 64 (L <= 64) or two of 128 (L <= 128).
+// At L < SL (the joint padding of a batch) the slot's rows past L repeat token L - 1,
+// their keys carry the -3e30 past-L bias and their queries are never stored, as in
+// attention_mfma_kernel; the QKV activation then never leaves the CU.  Main loop: the big-tile
 // kernel's 16x16x32 2-slot loop (WNB = 3).  Epilogue, per 128-row half (the waves with
 // wm == half own its accumulators): those 4 waves write bf16(acc + bias) into LDS
 // [128][392] (the same bf16 values the unfused GEMM stores), then all 8 waves run its
@@ -1182,14 +1184,18 @@ struct QaArgs {
   int L;                    // sequence length, 1..64 (one 64-row slot per sequence)
 };
 
+template <int SL>
 __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
-  constexpr int WNB = 3, BM = big::BM, BN = 128 * WNB, TP = BN + 8;  // L = 64
+  constexpr int WNB = 3, BM = big::BM, BN = 128 * WNB, TP = BN + 8;
+  constexpr int SPT = BM / SL;         // sequences per tile: 4 (SL = 64) or 2 (SL = 128)
+  constexpr int SH = SL == 64 ? 6 : 7;
+  constexpr int NJM = SL / 32;         // key blocks of 32 per sequence, at most
   __shared__ __attribute__((aligned(1024))) char lds[2 * (BM + BN) * big::ROW_BYTES];
-  static_assert(128 * TP * 2 + 8 * 64 * 4 <= 2 * (BM + BN) * big::ROW_BYTES,
+  static_assert(128 * TP * 2 + 8 * SL * 4 <= 2 * (BM + BN) * big::ROW_BYTES,
                 "staged half and mask biases fit the LDS");
   const int nseq = g.M / g.L;
-  const int ls = g.L == 64 ? 0 : g.L;  // 0: contiguous rows (slots are the sequences)
-  const int tiles_m = (nseq + 3) / 4;
+  const int ls = g.L == SL ? 0 : g.L;  // 0: contiguous rows (slots are the sequences)
+  const int tiles_m = (nseq + SPT - 1) / SPT;
   const int tiles_n = 3 * g.H / BN;
   const int ntiles = tiles_m * tiles_n;
   int bid = blockIdx.x;
@@ -1209,10 +1215,10 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
 #pragma unroll
     for (int j = 0; j < 2 * WNB; ++j) acc4[i][j] = (f32x4)0.0f;
   big::mainloop_mf16<WNB>(g.x, g.ldx, g.w, g.K, m0, n0, g.M, 3 * g.H, g.K, lds, wave, lane, acc4,
-                          ls);
+                          ls, SH);
 
   unsigned short* T = reinterpret_cast<unsigned short*>(lds);    // [128][TP] staged half
-  float* mbw = reinterpret_cast<float*>(lds + 128 * TP * 2) + 64 * wave;  // this wave's mask bias
+  float* mbw = reinterpret_cast<float*>(lds + 128 * TP * 2) + SL * wave;  // this wave's key bias
   // acc + bias -> bf16 pairs (rows e, e + 1 of one column) in registers:
   // 96 VGPRs instead of 192 live while the halves take turns through the LDS
   uint32_t pk[8][2 * WNB][2];
@@ -1235,6 +1241,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
       }
   }
   const int h = lane >> 5, r32 = lane & 31;
+  const int nj = (g.L + 31) / 32;  // key (and query) blocks of 32 of a sequence
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     if (wm == hf) {  // this half's accumulators -> T [128][TP]
@@ -1256,14 +1263,19 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
           }
     }
     __syncthreads();  // the half is staged
-    // every wave: queries [32 wm, +32) of (sequence wn >> 1, head 2 tn + (wn & 1)) of
-    // this half (the other half's waves hold their packed values meanwhile)
-    const int sl = wn >> 1, hh = wn & 1;
-    const int seq = 4 * tm + 2 * hf + sl;
+    // every wave: 32 queries of one (sequence, head) of this half (the other half's
+    // waves hold their packed values meanwhile).  SL = 64: two sequences per half,
+    // wave = (query block wm, sequence wn >> 1, head wn & 1); SL = 128: one sequence,
+    // wave = (query block wave >> 1, head wave & 1)
+    const int sl = SL == 64 ? wn >> 1 : 0, hh = SL == 64 ? wn & 1 : wave & 1;
+    const int ib = SL == 64 ? wm : wave >> 1;
+    const int seq = SPT * tm + (SL == 64 ? 2 * hf + sl : hf);
     const int r0 = seq * g.L;  // first token of the sequence
-    if (seq < nseq) {
-      mbw[lane] = lane >= g.L ? -3e30f
-                              : ((g.mask == nullptr || g.mask[r0 + lane] != 0) ? 0.f : -1e30f);
+    if (seq < nseq && ib < nj) {
+#pragma unroll
+      for (int j = lane; j < SL; j += 64)
+        mbw[j] = j >= g.L ? -3e30f
+                          : ((g.mask == nullptr || g.mask[r0 + j] != 0) ? 0.f : -1e30f);
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const unsigned short* Ts = T + 64 * sl * TP;
@@ -1272,25 +1284,28 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
       const unsigned short* V = Ts + 256 + hh * 64;
       unsigned short* out = g.ctx + (int64_t)r0 * g.ldc + (2 * tn + hh) * 64;
       {
-        const int ib = wm;
         bf16x8 qf[4];
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk)
           qf[kk] = *reinterpret_cast<const bf16x8*>(Q + (32 * ib + r32) * TP + 16 * kk + 8 * h);
-        f32x16 sc[2];
+        // the key blocks jb < nj, in order: attention_mfma_kernel<nj>'s arithmetic
+        f32x16 sc[NJM];
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb) {
+        for (int jb = 0; jb < NJM; ++jb) {
           sc[jb] = (f32x16)0.f;
+          if (jb < nj) {
 #pragma unroll
-          for (int kk = 0; kk < 4; ++kk) {
-            const bf16x8 kf =
-                *reinterpret_cast<const bf16x8*>(Kp + (32 * jb + r32) * TP + 16 * kk + 8 * h);
-            sc[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[jb], 0, 0, 0);
+            for (int kk = 0; kk < 4; ++kk) {
+              const bf16x8 kf =
+                  *reinterpret_cast<const bf16x8*>(Kp + (32 * jb + r32) * TP + 16 * kk + 8 * h);
+              sc[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[jb], 0, 0, 0);
+            }
           }
         }
         float mx = -INFINITY;
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
+        for (int jb = 0; jb < NJM; ++jb) {
+          if (jb >= nj) break;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const f32x4 bias = *reinterpret_cast<const f32x4*>(&mbw[32 * jb + 8 * q + 4 * h]);
@@ -1301,21 +1316,25 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
               mx = fmaxf(mx, v);
             }
           }
+        }
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         float sum = 0.f;
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
+        for (int jb = 0; jb < NJM; ++jb) {
+          if (jb >= nj) break;
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const float p = __expf(sc[jb][e] - mx);
             sc[jb][e] = p;
             sum += p;
           }
+        }
         sum += __shfl_xor(sum, 32, 64);
         const float inv = 1.f / sum;
         f32x16 o[2] = {(f32x16)0.f, (f32x16)0.f};
 #pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
+        for (int jb = 0; jb < NJM; ++jb) {
+          if (jb >= nj) break;
 #pragma unroll
           for (int k2 = 0; k2 < 2; ++k2) {
             bf16x8 pa;
@@ -1337,6 +1356,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
                                                               o[db], 0, 0, 0);
             }
           }
+        }
         // O: col = d (32 db + r32), row = query 32 ib + (e & 3) + 8 (e >> 2) + 4 h
 #pragma unroll
         for (int db = 0; db < 2; ++db)
@@ -1553,14 +1573,14 @@ extern "C" int irc_gemm_ln(int epilogue, int64_t M, int64_t N, int64_t K, const 
 }
 
 // QKV projection + attention in one launch (include/irc.h irc_qkv_attention; see
-// qkv_attn_kernel): L <= 64, head dim 64, H % 128 == 0.
+// qkv_attn_kernel): L <= 128, head dim 64, H % 128 == 0.
 extern "C" int irc_qkv_attention(int64_t M, int64_t H, int64_t heads, int64_t L, const void* x,
                                  int64_t ldx, const void* wqkv_perm, const float* bias_perm,
                                  const int64_t* mask, void* ctx, int64_t ldc,
                                  irc_stream_t stream) {
   using namespace irc::gemm;
-  IRC_REQUIRE(L >= 1 && L <= 64 && heads * 64 == H && H % 128 == 0,
-              "qkv_attention: needs L <= 64, head dim 64 and H %% 128 == 0");
+  IRC_REQUIRE(L >= 1 && L <= 128 && heads * 64 == H && H % 128 == 0,
+              "qkv_attention: needs L <= 128, head dim 64 and H %% 128 == 0");
   IRC_REQUIRE(M > 0 && M % L == 0 && M < (1ll << 31), "qkv_attention: M must be a multiple of L");
   IRC_REQUIRE(H % 64 == 0 && ldx % 8 == 0 && ldx >= H && ldc >= H, "qkv_attention: bad strides");
   IRC_REQUIRE((((uintptr_t)x | (uintptr_t)wqkv_perm) % 16) == 0 && ((uintptr_t)ctx % 2) == 0,
@@ -1570,9 +1590,13 @@ extern "C" int irc_qkv_attention(int64_t M, int64_t H, int64_t heads, int64_t L,
            bias_perm, mask, static_cast<unsigned short*>(ctx), (int)M, (int)H, (int)H, ldx, ldc,
            0.125f, (int)L};
   hipStream_t st = as_stream(stream);
-  const int tiles = (int)((M / L + 3) / 4) * (int)(3 * H / 384);
+  const int spt = L <= 64 ? 4 : 2;  // sequences per 256-row tile (64- or 128-row slots)
+  const int tiles = (int)((M / L + spt - 1) / spt) * (int)(3 * H / 384);
   prof_begin(st);
-  hipLaunchKernelGGL(qkv_attn_kernel, dim3(tiles), dim3(big::NT), 0, st, a);
+  if (L <= 64)
+    hipLaunchKernelGGL(qkv_attn_kernel<64>, dim3(tiles), dim3(big::NT), 0, st, a);
+  else
+    hipLaunchKernelGGL(qkv_attn_kernel<128>, dim3(tiles), dim3(big::NT), 0, st, a);
   // a GEMM with an attention epilogue: its flops and bytes (x, Wqkv, ctx) count as one
   prof_end("gemm_bf16", st, 2.0 * M * 3 * H * H + 4.0 * M * L * H);
   prof_work("gemm_bf16_bytes", 2.0 * (double)M * H + 2.0 * 3 * H * H + 2.0 * (double)M * H);

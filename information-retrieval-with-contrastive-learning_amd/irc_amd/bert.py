@@ -150,8 +150,9 @@ class BertModel(nn.Module):
         self.weight_format = os.environ.get("IRC_ENCODER_WEIGHTS", "bf16")
         # LayerNorm fold of the bf16 encoder (_encode_folded); IRC_LN_FOLD=0 / 1 overrides
         self.ln_fold = os.environ.get("IRC_LN_FOLD", "0") != "0"
-        # QKV projection + attention in one launch where it applies (bf16, L = 64, head
-        # dim 64; irc_qkv_attention); IRC_QKV_ATTN=0 keeps the two-launch form
+        # QKV projection + attention in one launch where it applies (bf16, head dim 64,
+        # L in ops.QKV_ATTN_FUSED_L; irc_qkv_attention); IRC_QKV_ATTN=0 keeps the
+        # two-launch form
         self.fused_attention = os.environ.get("IRC_QKV_ATTN", "1") != "0"
         self.eval()
 
@@ -314,7 +315,7 @@ class BertModel(nn.Module):
     def _qkv_attention(self, x, lw, mask, B, L, H, heads):
         """ctx of one layer: one fused launch where it applies, else QKV GEMM + attention."""
         if self.fused_attention and ops.qkv_attention_supported(L, H, heads,
-                                                                ops.QKV_ATTN_MIN_L):
+                                                                ops.QKV_ATTN_FUSED_L):
             if "wqkv_p" not in lw:  # permuted once per cast weight set
                 perm = ops.qkv_perm_index(H, lw["wqkv"].device)
                 lw["wqkv_p"] = lw["wqkv"].index_select(0, perm).contiguous()

@@ -188,27 +188,27 @@ def qkv_perm_index(H: int, device=None) -> torch.Tensor:
     return (n + part + torch.arange(128).view(1, 1, -1)).reshape(-1).to(device)
 
 
-# Shortest L the frozen encoder sends to the fused kernel: a sequence takes a 64-row
-# slot of the QKV GEMM, so at L < 64 the slot's 64 - L rows are extra QKV work
-# (1 - L / 64 of it), against the separate attention launch and the QKV activation's
-# HBM round trip the fusion saves.
-QKV_ATTN_MIN_L = 48
+# The L the frozen encoder sends to the fused kernel: a sequence takes a 64-row (L <= 64)
+# or 128-row (L <= 128) slot of the QKV GEMM, so below the slot size the slot's extra
+# rows are extra QKV work, against the separate attention launch and the QKV
+# activation's HBM round trip the fusion saves.
+QKV_ATTN_FUSED_L = ((48, 64), (112, 128))
 
 
-def qkv_attention_supported(L: int, H: int, heads: int, min_l: int = 1) -> bool:
-    return min_l <= L <= 64 and heads * 64 == H and H % 128 == 0
+def qkv_attention_supported(L: int, H: int, heads: int, ranges=((1, 128),)) -> bool:
+    return any(lo <= L <= hi for lo, hi in ranges) and heads * 64 == H and H % 128 == 0
 
 
 def qkv_attention(x, wqkv_perm, bias_perm, mask, B, L, H, heads, out=None):
     """irc_qkv_attention: ctx [B*L, H] bf16 = attention(x . Wqkv^T + b) in one launch
     (the QKV activation stays on chip).  wqkv_perm / bias_perm: rows in qkv_perm_index
-    order.  L <= 64: one 64-row slot per sequence.  Same result as gemm(EPI_BIAS) +
-    attention on the big-tile shapes."""
+    order.  One 64-row (L <= 64) or 128-row (L <= 128) slot per sequence.  Same result
+    as gemm(EPI_BIAS) + attention on the big-tile shapes."""
     require_hip(x, wqkv_perm, bias_perm, mask, out)
     if x.dtype != BF16 or wqkv_perm.dtype != BF16 or bias_perm.dtype != F32:
         raise TypeError("qkv_attention: bf16 x / weights, fp32 bias")
     if not qkv_attention_supported(L, H, heads):
-        raise ValueError("qkv_attention: needs L <= 64, head dim 64, H % 128 == 0")
+        raise ValueError("qkv_attention: needs L <= 128, head dim 64, H % 128 == 0")
     if x.shape != (B * L, H) or x.stride(-1) != 1 or tuple(wqkv_perm.shape) != (3 * H, H):
         raise ValueError("qkv_attention: x [B*L, H], Wqkv [3H, H]")
     if mask is not None and (mask.dtype != torch.int64 or not mask.is_contiguous()

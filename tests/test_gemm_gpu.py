@@ -497,7 +497,7 @@ def test_wave_remainder_split(gpu, M, N, K, epi, odt, b_is_nk):
     out = ops.gemm(a.to(gpu), b.to(gpu), b_is_nk=b_is_nk,
                    bias=None if bias is None else bias.to(gpu), epilogue=epi,
                    residual=None if res is None else res.to(gpu), out_dtype=odt, alpha=0.5)
-    rows = torch.cat([torch.arange(0, 300), torch.arange(32000, M)])
+    rows = torch.cat([torch.arange(0, 300), torch.arange(M - 1200, M)])
     ref = _ref(a[rows], b, False, b_is_nk, bias, epi, None if res is None else res[rows], 0.5)
     got = out.float().cpu()[rows]
     rel = (got - ref).abs().max().item() / ref.abs().max().item()

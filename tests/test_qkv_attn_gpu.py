@@ -61,9 +61,13 @@ def test_perm_index():
 
 
 @pytest.mark.parametrize("masked,L", [(True, 64), (False, 64), (True, 63), (True, 57),
-                                      (False, 61)])
+                                      (False, 61), (True, 40), (True, 72), (True, 100),
+                                      (False, 128), (True, 128)])
 def test_bit_exact_on_big_tile_shape(gpu, masked, L):
-    B, H, heads = 512, 768, 12
+    """B x L ~ 32k rows, where the unfused QKV GEMM runs on the big-tile main loop
+    (L <= 64: 64-row slots, four sequences a tile; L in (64, 128]: 128-row slots, two)."""
+    B = {40: 800, 72: 448, 100: 320, 128: 256}.get(L, 512)
+    H, heads = 768, 12
     x, w, b, mask = _inputs(gpu, B, L, H, 5, masked)
     cf = _fused(x, w, b, mask, B, L, H, heads)
     cu = _unfused(x, w, b, mask, B, L, H, heads)
@@ -74,7 +78,9 @@ def test_bit_exact_on_big_tile_shape(gpu, masked, L):
 
 @pytest.mark.parametrize("B,H,heads,L", [(37, 768, 12, 64), (4, 768, 12, 64), (64, 1024, 16, 64),
                                          (37, 768, 12, 40), (5, 768, 12, 1), (64, 1024, 16, 50),
-                                         (300, 768, 12, 48), (9, 768, 12, 17)])
+                                         (300, 768, 12, 48), (9, 768, 12, 17),
+                                         (37, 768, 12, 72), (3, 768, 12, 100),
+                                         (33, 1024, 16, 128), (7, 768, 12, 65)])
 def test_against_reference(gpu, B, H, heads, L):
     """Ragged last tile (B = 37: 2368 rows), a single partial tile, BERT-large width;
     L < 64 (slots with repeated last tokens: B = 37 at L = 40 leaves a 1-sequence last
@@ -92,15 +98,15 @@ def test_against_reference(gpu, B, H, heads, L):
 def test_rejects_unsupported(gpu):
     from irc_amd import ops
 
-    x, w, b, mask = _inputs(gpu, 4, 65, 768, 1)
+    x, w, b, mask = _inputs(gpu, 4, 129, 768, 1)
     with pytest.raises(ValueError):
-        _fused(x, w, b, mask, 4, 65, 768, 12)  # L = 65
+        _fused(x, w, b, mask, 4, 129, 768, 12)  # L = 129
     x, w, b, mask = _inputs(gpu, 4, 64, 768, 1)
     with pytest.raises(TypeError):
         ops.qkv_attention(x.float(), w, b, mask, 4, 64, 768, 12)
 
 
-@pytest.mark.parametrize("L", [64, 61])
+@pytest.mark.parametrize("L", [64, 61, 120])
 def test_encoder_fused_matches_unfused(gpu, L):
     """The frozen encoder with the fused launch equals the two-launch encoder bit for bit
     at B = 512 (every QKV GEMM on the big-tile main loop), at L = 64 and at a joint
@@ -112,7 +118,7 @@ def test_encoder_fused_matches_unfused(gpu, L):
     cfg = dataclasses.replace(BERT_BASE, num_hidden_layers=2)
     m = BertModel(cfg, seed=4).to(gpu)
     g = torch.Generator().manual_seed(2)
-    B = 512
+    B = {120: 256}.get(L, 512)
     ids = torch.randint(1, cfg.vocab_size, (B, L), generator=g)
     lens = torch.randint(8, L + 1, (B,), generator=g)
     mask = (torch.arange(L)[None, :] < lens[:, None]).to(torch.int64)

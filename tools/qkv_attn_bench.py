@@ -1,7 +1,7 @@
 """QKV projection + attention: one fused launch (irc_qkv_attention) against the two-launch
 form (irc_gemm EPI_BIAS + irc_attention) at the frozen encoder's shapes, interleaved.
 
-    python tools/qkv_attn_bench.py [--iters 20] [--h 768]
+    python tools/qkv_attn_bench.py [--iters 20] [--h 768] [--lens 64,57,72,100,128]
 
 Prints us per layer (HIP events on the launch stream) for each form, twice.
 """
@@ -20,11 +20,17 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--h", type=int, default=768)
     ap.add_argument("--b", type=int, default=512)
+    ap.add_argument("--lens", default="64", help="sequence lengths (B = 32768 // L tokens ~ 32k)")
     a = ap.parse_args()
     from irc_amd import ops
 
     dev = torch.device("cuda:0")
-    B, L, H = a.b, 64, a.h
+    for L in (int(v) for v in a.lens.split(",")):
+        run_len(a, ops, dev, L, a.b if a.lens == "64" else max(1, 32768 // L))
+
+
+def run_len(a, ops, dev, L, B):
+    H = a.h
     heads = H // 64
     x = (torch.randn(B * L, H, device=dev) * 0.5).bfloat16()
     w = (torch.randn(3 * H, H, device=dev) * 0.05).bfloat16()
@@ -55,7 +61,8 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / a.iters
-            print(f"H={H} M={B * L} {name:8s} {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s", flush=True)
+            print(f"H={H} L={L} M={B * L} {name:8s} {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s",
+                  flush=True)
 
 
 if __name__ == "__main__":
