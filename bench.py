@@ -262,8 +262,8 @@ def run_train(args, rank, world, dev, weights="bf16", cfg=None):
                      "traffic_source": _pmc_source(ptag),
                      "kernel": ("bf16 GEMM kernels (gemm_big_kernel / gemm_pp_kernel / "
                                 "gemm_kernel, and qkv_attn_kernel: the QKV GEMM with the "
-                                "attention in its epilogue, counted with the attention's "
-                                "flops; all GEMM launches of a single-stream pass of the "
+                                "attention in its epilogue, priced on the QKV GEMM's flops "
+                                "alone; all GEMM launches of a single-stream pass of the "
                                 "same steps)") if weights == "bf16" else
                                ("MX-fp8 GEMM (gemm_pp_kernel F8 = 2: e4m3 codes, E8M0 scales "
                                 "per 32 k applied by v_mfma_scale_f32_16x16x128_f8f6f4) of the "

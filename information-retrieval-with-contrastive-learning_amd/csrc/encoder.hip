@@ -251,9 +251,11 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const unsigned short
 // with R consecutive rows per half-wave: gamma / beta stay in registers across the rows
 // and the next row's loads are issued before this row's statistics.
 // y8 != null: also the MX-fp8 copy, as layernorm_vec_kernel writes it (config C5).
+// Called in place (y == x) by the encoder: x / y are not __restrict__, and the prefetch
+// past the last row re-reads the half-wave's own row (never another half-wave's).
 template <int CPL, int R>
-__global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned short* __restrict__ x,
-                                                            unsigned short* __restrict__ y,
+__global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned short* x,
+                                                            unsigned short* y,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta,
                                                             int64_t rows, float eps,
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned shor
   }
   u16x8 cur[CPL];
   {
-    const unsigned short* xr = x + (row0 < rows ? row0 : 0) * H;
+    const unsigned short* xr = x + (row0 < rows ? row0 : rows - 1) * H;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) cur[i] = *reinterpret_cast<const u16x8*>(xr + (i * 32 + hl) * 8);
   }
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned shor
     const int64_t row = row0 + r;
     u16x8 nxt[CPL];
     if (r + 1 < R) {
-      const int64_t rn = row + 1 < rows ? row + 1 : 0;
+      const int64_t rn = row + 1 < rows ? row + 1 : (row < rows ? row : rows - 1);
 #pragma unroll
       for (int i = 0; i < CPL; ++i)
         nxt[i] = *reinterpret_cast<const u16x8*>(x + rn * H + (i * 32 + hl) * 8);

@@ -49,7 +49,8 @@ def gemm_ln(a, b, bias, *, epilogue, stats=None, gamma=None, beta=None, eps=1e-1
     epilogue EPI_BIAS / EPI_BIAS_GELU: out = LN(a) . W^T + bias' with b = W diag(gamma)
     (the fold: stats of a, colsum of b); EPI_BIAS_RESID: out = a . b^T + bias + LN(residual)
     (stats, gamma, beta of the residual) or + residual.  Returns out, or (out, LnStats)."""
-    require_hip(a, b, bias, residual, out)
+    require_hip(a, b, bias, residual, out, gamma, beta, colsum,
+                stats.t if stats is not None else None)
     for t in (a, b, residual, out):
         if t is not None and (t.dtype != BF16 or t.dim() != 2 or t.stride(-1) != 1):
             raise TypeError("gemm_ln: a, b, residual and out must be 2-D bf16, unit column stride")
@@ -60,6 +61,13 @@ def gemm_ln(a, b, bias, *, epilogue, stats=None, gamma=None, beta=None, eps=1e-1
     N = b.shape[0]
     if b.shape[1] != K:
         raise ValueError(f"gemm_ln inner dims differ: {K} vs {b.shape[1]}")
+    # the kernels read bias / colsum per output column and gamma / beta per statistics
+    # column with 16-byte loads: a short vector would be a device fault
+    for t, n, name in ((bias, N, "bias"), (colsum, N, "colsum"),
+                       (gamma, stats.h if stats is not None else None, "gamma"),
+                       (beta, stats.h if stats is not None else None, "beta")):
+        if t is not None and n is not None and t.numel() != n:
+            raise ValueError(f"gemm_ln: {name} has {t.numel()} elements, needs {n}")
     # the statistics describe a (the fold, epilogues 1 / 2) or the residual (epilogue 3)
     if stats is not None and (stats.t.shape[0] != M or stats.h != (N if residual is not None else K)):
         raise ValueError("gemm_ln: the statistics describe another activation")
