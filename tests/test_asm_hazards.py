@@ -94,3 +94,41 @@ def test_asm_loads_untouched_until_waited(lstm_coop_asm):
         used = set().union(*(_regs(o) for o in ops)) if ops else set()
         assert not (used & pending), f"register of an un-waited asm load touched: {t}"
     assert n > 0, "no asm loads found (the check would be vacuous)"
+
+
+# gfx950 (CDNA3/4 XDL): wait states a VMEM instruction that READS a VGPR written by an
+# MFMA needs after it: 16x16 shapes (8 passes) 11, 32x32 shapes (16 passes) 19.
+def _mfma_wait_states(op):
+    return 19 if "32x32" in op else 11
+
+
+def test_asm_wide_stores_after_mfma_writes(lstm_coop_asm):
+    """The backward's asm stores publish MFMA accumulators: the compiler pads an
+    MFMA-write -> VMEM-read dependency for its own stores, not for one inside inline
+    asm, so the instructions between the last MFMA writing a store's data registers
+    and the store must cover the XDL -> VMEM-read wait states (advisor, round 4)."""
+    ins = lstm_coop_asm
+    n = 0
+    for i, t in enumerate(ins):
+        m = re.match(r"global_store_dwordx4 \S+, (v\[\d+:\d+\]), off sc1", t)
+        if not m:
+            continue
+        n += 1
+        pending = _regs(m.group(1))  # data registers whose last writer is not yet found
+        waits = 0
+        for t2 in reversed(ins[max(0, i - 40):i]):
+            if not pending or re.match(r"s_(cbranch|branch|endpgm|setpc|swappc)", t2):
+                break  # straight-line window only
+            d = re.match(r"(v_mfma\S*)\s+(v\[\d+:\d+\]|v\d+)", t2)
+            if d and _regs(d.group(2)) & pending:
+                need = _mfma_wait_states(d.group(1))
+                assert waits >= need, \
+                    f"asm store of {m.group(1)} {waits} wait states after {t2} (needs {need})"
+                pending -= _regs(d.group(2))
+            else:
+                w = re.match(r"(v_\S+)\s+(v\[\d+:\d+\]|v\d+)", t2)
+                if w:  # a VALU op wrote these last: no XDL dependency for them
+                    pending -= _regs(w.group(2))
+            s = re.match(r"s_nop (\d+)", t2)
+            waits += int(s.group(1)) + 1 if s else 1
+    assert n > 0, "no asm wide stores found (the check would be vacuous)"
