@@ -477,9 +477,17 @@ struct RemSplit {
   int64_t M1 = 0;
   int splits = 1;
 };
+// IRC_GEMM_REMAINDER=0 disables the split (A/B; read once).
+inline bool remainder_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("IRC_GEMM_REMAINDER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 inline RemSplit remainder_split(int64_t M, int64_t N, int64_t K) {
   RemSplit best;
-  if (K % 64 != 0 || K < 256 || M < 512) return best;
+  if (!remainder_enabled() || K % 64 != 0 || K < 256 || M < 512) return best;
   const int64_t ncu = gpp::device_cu_count();
   const int64_t mt = (M + 255) / 256;
   double plain = 1e30, split = 1e30;

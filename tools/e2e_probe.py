@@ -32,6 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--by-len", action="store_true")
+    ap.add_argument("--lens", default="", help="with --by-len: only these padded L")
     a = ap.parse_args()
     import e2e_train as E
     import bench
@@ -118,7 +119,10 @@ def main():
         for idx, sel in sels:
             ids, mask = corpus.batch(sel)
             by_len.setdefault(ids.shape[1], (ids, mask))
+        keep = {int(v) for v in a.lens.split(",") if v}
         for L in sorted(by_len):
+            if keep and L not in keep:
+                continue
             sids, smask = bench.synthetic_batch(512, L, 1337)
             for name, (i_, m_) in (("real", by_len[L]), ("synth", (sids.to(dev), smask.to(dev)))):
                 fixed[0], fixed[1] = i_, m_
