@@ -466,12 +466,15 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict
 
 // Wave remainder of a bf16 GEMM with batch 1 and row-major A (every BERT / LSTM-head
 // linear layer: M = tokens).  Output tiles are 256 rows high, so at M = B L for L just
-// above a multiple of 256 / B (a batch jointly padded to L = 65: 260 tiles of 256 x 384
-// on 256 CUs) the last wave runs a handful of tiles on a nearly idle chip.  Priced in
-// 256x256-tile times per CU (a 256 x 384 tile = 1.5), the plain launch costs
-// ceil(tiles / CUs) waves; the split form runs the rows of the full waves as one
-// launch and the remaining rows as a split-K launch spread over the chip (raw fp32
-// slabs) plus one reduce pass applying the epilogue (~0.5 of a tile time).  Returns
+// above a multiple of 256 / B (a batch jointly padded to L = 65) the last wave runs a
+// handful of tiles on a nearly idle chip.  The split form runs the rows of the full
+// waves as one launch and the remaining rows as a split-K launch spread over the chip
+// (raw fp32 slabs) plus one pass that sums the slabs and applies the epilogue.  Priced
+// in microseconds: a 256 x 256 tile ~0.03 us per unit of K on one CU (a 256 x 384 tile
+// 1.5x), the two extra launches ~25 us together -- so only long-K shapes gain (FFN2 at
+// L = 65: one wave of big tiles + the remainder instead of two waves of 256 x 256;
+// measured on MI355X, the K = 768 shapes lost: the C2 step at L = 65 / 67 took 10.2 /
+// 10.6 ms with the split on every eligible GEMM against 10.0 / 10.1 without).  Returns
 // the rows of the full-wave launch (0: no split) and the remainder's split count.
 struct RemSplit {
   int64_t M1 = 0;
@@ -490,21 +493,22 @@ inline RemSplit remainder_split(int64_t M, int64_t N, int64_t K) {
   if (!remainder_enabled() || K % 64 != 0 || K < 256 || M < 512) return best;
   const int64_t ncu = gpp::device_cu_count();
   const int64_t mt = (M + 255) / 256;
+  const double t256 = 0.03 * (double)K, overhead = 25.0;  // us
   double plain = 1e30, split = 1e30;
   int64_t m1 = 0;
   for (int wide = 0; wide < 2; ++wide) {
     if (wide && N % 384 != 0) continue;
     const int64_t nt = wide ? N / 384 : (N + 255) / 256;
-    const double c = wide ? 1.5 : 1.0;
+    const double tt = wide ? 1.5 * t256 : t256;
     const int64_t tiles = mt * nt;
-    const double p = (double)((tiles + ncu - 1) / ncu) * c;
+    const double p = (double)((tiles + ncu - 1) / ncu) * tt;
     if (p < plain) plain = p;
     const int64_t full = tiles / ncu;
     if (full < 1) continue;
     const int64_t rows = (full * ncu / nt) * 256;  // whole row tiles of the full waves
     if (rows <= 0 || rows >= M) continue;
     const double rem_tiles = (double)((M - rows + 255) / 256) * nt;
-    const double sp = (double)full * c + rem_tiles * c / (double)ncu + 0.5;
+    const double sp = (double)full * tt + rem_tiles * tt / (double)ncu + overhead;
     if (sp < split) {
       split = sp;
       m1 = rows;

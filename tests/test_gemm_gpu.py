@@ -474,13 +474,13 @@ def test_pp_persistent_bert_shapes(gpu, b_is_nk):
 
 
 @pytest.mark.parametrize("M,N,K,epi,odt,b_is_nk", [
-    (33280, 768, 768, 3, torch.bfloat16, True),    # out-proj at L = 65 (B = 512): 260 big tiles
-    (33280, 768, 3072, 3, torch.bfloat16, True),   # FFN2 at L = 65
-    (33280, 3072, 768, 2, torch.bfloat16, True),   # FFN1 + GELU at L = 65
-    (33280, 2304, 768, 1, torch.bfloat16, True),   # QKV at L = 65
-    (16640, 2048, 768, 1, torch.float32, True),    # LSTM input projection at L = 65 (B = 256)
-    (16640, 2048, 512, 0, torch.float32, False),   # K-outer B operand
-    (33792, 768, 768, 4, torch.float32, True),     # L = 66, residual only, fp32 out
+    (33280, 768, 3072, 3, torch.bfloat16, True),   # FFN2 at L = 65 (B = 512): split
+    (34816, 768, 3072, 1, torch.bfloat16, True),   # L = 68, bias only: split
+    (33280, 768, 3072, 4, torch.float32, True),    # residual only, fp32 out: split
+    (33280, 768, 3072, 0, torch.float32, False),   # K-outer B operand: split
+    (33280, 768, 768, 3, torch.bfloat16, True),    # out-proj at L = 65: no split (short K)
+    (33280, 3072, 768, 2, torch.bfloat16, True),   # FFN1 + GELU at L = 65: no split
+    (16640, 2048, 768, 1, torch.float32, True),    # LSTM input projection: no split
 ])
 def test_wave_remainder_split(gpu, M, N, K, epi, odt, b_is_nk):
     """A GEMM whose last wave of output tiles would run nearly empty (M = B L just above
