@@ -144,18 +144,6 @@ int irc_gemm_set_persistent(int mode);
  * results are bit-identical (env IRC_BIG_RING sets the initial value).  Returns the
  * previous setting. */
 int irc_gemm_set_big_ring(int on);
-/* Wave tail of the big-tile bf16 GEMM (batch 1, A [M][K], B [N][K], N % 384 == 0, the
- * caller's workspace from irc_gemm_workspace): where the 256 x 384 output tiles fill
- * whole waves but for a few tiles (M = B L at L = 65: 130 row tiles), those tiles run
- * as split-K pieces inside the same launch and the last piece of each sums the pieces
- * in a fixed order (deterministic; the rows of those tiles are summed in another order
- * than the unsplit GEMM's).  1 = on (the default; env IRC_GEMM_TAIL=0 starts it off),
- * 0 = off.  Returns the previous setting. */
-int irc_gemm_set_tail(int on);
-/* The wave-tail plan irc_gemm takes for a bf16 M x N x K GEMM on the current device:
- * out[0] = rows run as whole tiles (0: no tail form), out[1] = tail tiles, out[2] = K
- * pieces per tail tile, out[3] = K per piece.  For tests and tools. */
-int irc_gemm_tail_plan(int64_t M, int64_t N, int64_t K, int64_t* out);
 /* LayerNorm-fold GEMM of the BERT encoder forward (bf16; HF BertLayer's
  * attention.output / intermediate / output sublayers, contrastive_module.py:39 ->
  * modeling_bert): the encoder keeps each pre-LayerNorm activation h with per-row

@@ -24,9 +24,7 @@
 // in that XCD's L2).
 #include "gemm_pp.h"
 
-#include <algorithm>
 #include <atomic>
-#include <mutex>
 
 namespace irc {
 namespace gemm {
@@ -117,11 +115,6 @@ struct Args {
   float* P;          // split-K partials [batch][split][M][N] (raw sums), or null
   int group_m;       // big-tile kernel: grouped tile order (irc_common.h); 0 = row-major
   LnArgs ln;         // LayerNorm fold (big-tile kernel, bf16 C, vectorised epilogue)
-  // wave tail of the big-tile kernel (TailPlan below; t_np = 0: off): blocks [0, t_np)
-  // are the K pieces of the t_r tiles of rows [t_m1, M), t_s pieces of t_kc each
-  int t_np, t_r, t_m1, t_s, t_kc;
-  float* t_ws;       // [t_r][t_s] piece slabs (register order)
-  uint32_t* t_ctr;   // [t_r] arrival tickets, zero between launches
 };
 
 // bf16 K-outer (COL / KN) slabs are kept k-major in LDS: [BK=32 k][128 rows]
@@ -428,94 +421,6 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restr
   *dst = accumulate ? *dst + v : v;
 }
 
-// Wave tail of a bf16 GEMM on the big-tile kernel (batch 1, A [M][K], B [N][K], N % 384
-// == 0: every BERT linear layer at M = B L).  Output tiles are 256 rows high, so at M
-// just above a whole number of waves (a batch jointly padded to L = 65: 130 row tiles,
-// 260 out-proj tiles on 256 CUs) the last wave runs a handful of tiles on an idle chip,
-// and the 256 x 256 kernel's extra waves are no better.  The tail form runs the rows
-// of the full waves as whole tiles and each remaining tile as S K-pieces in the same
-// launch (blocks [0, np), issued first so they run beside the first wave): a piece
-// writes its fp32 partial tile to a slab, and the last piece of a tile to arrive sums
-// the slabs in piece order and runs the tile's epilogue -- no second launch, no wait.
-// Priced in 256 x 256 tile times (a 256 x 384 tile = 1.5): full waves x 1.5 + the
-// pieces' share, against the 256 x 256 kernel's and the plain big-tile kernel's waves.
-struct TailPlan {
-  int64_t M1 = 0;  // rows of the full waves (0: no tail form)
-  int S = 1, R = 0, kc = 0, np = 0;
-};
-constexpr int64_t TAIL_SLAB = 512 * 8 * 6 * 4;  // floats per piece: 512 threads x 48 f32x4 (WNB = 3)
-constexpr int TAIL_MAX_TILES = 64;                            // tickets per counter slot
-// IRC_GEMM_TAIL=0 disables the tail form (A/B; read once); irc_gemm_set_tail switches
-// it at run time (the tests compare both).
-inline std::atomic<int>& tail_mode() {
-  static std::atomic<int> on{[] {
-    const char* e = getenv("IRC_GEMM_TAIL");
-    return (e && e[0] == '0') ? 0 : 1;
-  }()};
-  return on;
-}
-inline TailPlan tail_plan(int64_t M, int64_t N, int64_t K) {
-  TailPlan p;
-  if (tail_mode().load(std::memory_order_relaxed) == 0) return p;
-  if (N % 384 != 0 || K % 64 != 0 || K < 256 || M < 512) return p;
-  const int64_t ncu = gpp::device_cu_count();
-  if (ncu <= 0) return p;
-  const int64_t mt = (M + 255) / 256, nt = N / 384;
-  const int64_t t384 = mt * nt, t256 = mt * ((N + 255) / 256);
-  const int64_t full = t384 / ncu;
-  if (full < 1 || t384 % ncu == 0) return p;
-  const int64_t mfull = full * ncu / nt;  // row tiles of the whole-tile part
-  if (mfull >= mt) return p;
-  const int64_t R = (mt - mfull) * nt;
-  if (R > TAIL_MAX_TILES) return p;
-  int64_t S = ncu / R;
-  if (S > K / 128) S = K / 128;  // >= 2 K-tiles per piece
-  if (S < 2) return p;
-  const int64_t kc = ((K + S - 1) / S + 63) / 64 * 64;
-  S = (K + kc - 1) / kc;
-  const double cost = 1.5 * (double)full + 1.5 * (double)((R * S + ncu - 1) / ncu) / (double)S;
-  const double plain = std::min((double)((t256 + ncu - 1) / ncu), 1.5 * (double)((t384 + ncu - 1) / ncu));
-  if (cost > plain - 0.1) return p;
-  p.M1 = mfull * 256;
-  p.S = (int)S;
-  p.R = (int)R;
-  p.kc = (int)kc;
-  p.np = (int)((R * S + 7) / 8 * 8);
-  return p;
-}
-inline int64_t tail_bytes(const TailPlan& p) {
-  return p.M1 > 0 ? (int64_t)p.R * p.S * TAIL_SLAB * (int64_t)sizeof(float) : 0;
-}
-// Ticket slots of the tail launches, TAIL_MAX_TILES counters each, handed out in
-// rotation (launches on concurrent streams never share one); zeroed once, and each
-// launch leaves its slot zeroed.  None while a graph is being captured (a replay would
-// keep its slot while the rotation hands it to another launch): the plain form runs.
-constexpr int TAIL_SLOTS = 512;
-inline uint32_t* tail_counter(hipStream_t st) {
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone)
-    return nullptr;
-  static std::mutex mu;
-  static uint32_t* base[64] = {};
-  static std::atomic<uint32_t> next{0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    if (base[dev] == nullptr) {
-      void* q = nullptr;
-      const size_t bytes = (size_t)TAIL_SLOTS * TAIL_MAX_TILES * sizeof(uint32_t);
-      if (hipMalloc(&q, bytes) != hipSuccess) return nullptr;
-      if (hipMemset(q, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-        (void)hipFree(q);
-        return nullptr;
-      }
-      base[dev] = static_cast<uint32_t*>(q);
-    }
-  }
-  return base[dev] + (next.fetch_add(1) % TAIL_SLOTS) * TAIL_MAX_TILES;
-}
-
 // Split-K count: only when the output tile grid cannot fill the chip and each
 // slice keeps >= 512 of K (bf16) / >= 128 of K (fp32: the exact-fp32 MFMA runs at
 // 1/16 of the bf16 rate, so a 128-deep slice is already 8 K-steps of real work --
@@ -785,32 +690,16 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
   constexpr int A_BYTES = BM * big::ROW_BYTES, B_BYTES = BN * big::ROW_BYTES;
   constexpr int STAGE = A_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(1024))) char lds[2 * STAGE];  // [stage][A | B]
-  // wave tail (TailPlan): 16x16x32 2-slot form without the LayerNorm fold
-  constexpr bool TAIL = MF16 && !LN && !RING;
+  const int tiles_m = (g.M + BM - 1) / BM;
   const int tiles_n = (g.N + BN - 1) / BN;
-  int tiles_m = (g.M + BM - 1) / BM;
+  const int ntiles = tiles_m * tiles_n;
   int bid = blockIdx.x;
-  int tm, tn, piece = -1, ptile = 0, kbeg = 0, kcnt = g.K;
-  if (TAIL && g.t_np > 0 && bid < g.t_np) {  // K piece of a tail tile
-    ptile = bid / g.t_s;
-    if (ptile >= g.t_r) return;  // padding of the pieces to whole XCD rounds
-    piece = bid - ptile * g.t_s;
-    tm = g.t_m1 / BM + ptile / tiles_n;
-    tn = ptile % tiles_n;
-    kbeg = piece * g.t_kc;
-    kcnt = min(g.t_kc, g.K - kbeg);
-  } else {
-    if (TAIL && g.t_np > 0) {  // the full waves: rows [0, t_m1)
-      bid -= g.t_np;
-      tiles_m = g.t_m1 / BM;
-    }
-    const int ntiles = tiles_m * tiles_n;
-    {  // XCD-aware bijective remap: blocks sharing an XCD walk consecutive tiles
-      const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
-      bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-    }
-    grouped_tile(bid, tiles_m, tiles_n, g.group_m, tm, tn);
+  {  // XCD-aware bijective remap: blocks sharing an XCD walk consecutive tiles
+    const int q = ntiles / 8, r = ntiles % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
+  int tm, tn;
+  grouped_tile(bid, tiles_m, tiles_n, g.group_m, tm, tn);
   const int batch = blockIdx.y;
   const unsigned short* A = reinterpret_cast<const unsigned short*>(g.A) + batch * g.sA;
   const unsigned short* B = reinterpret_cast<const unsigned short*>(g.B) + batch * g.sB;
@@ -879,48 +768,7 @@ __global__ __launch_bounds__(big::NT, 1) void gemm_big_kernel(Args g) {
     }
     __syncthreads();  // the epilogue's staging rows overlap the ring
   } else if constexpr (MF16) {
-    big::mainloop_mf16<WNB>(A + kbeg, g.lda, B + kbeg, g.ldb, m0, n0, g.M, g.N, kcnt, lds, wave,
-                            lane, acc4);
-    if constexpr (TAIL) {
-      if (piece >= 0) {
-        // raw partial sums -> this piece's slab in register order (coalesced 16-byte
-        // rows of lanes); the last piece of the tile to arrive sums the tile's slabs
-        // in piece order (deterministic) and runs the epilogue.  Agent-scope release /
-        // acquire: the pieces run on different XCDs, whose L2s are not coherent.
-        constexpr int NV = 8 * 2 * WNB;  // f32x4 accumulators per thread
-        f32x4* slabs = reinterpret_cast<f32x4*>(g.t_ws) + (int64_t)ptile * g.t_s * NV * NT;
-        f32x4* mine = slabs + (int64_t)piece * NV * NT + threadIdx.x;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 2 * WNB; ++j) mine[(i * 2 * WNB + j) * NT] = acc4[i][j];
-        int* flag = reinterpret_cast<int*>(lds + 2 * STAGE) - 1;  // past the epilogue's LDS
-        __syncthreads();  // every wave's slab stores complete
-        if (threadIdx.x == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          const uint32_t old =
-              __hip_atomic_fetch_add(g.t_ctr + ptile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int last = old == (uint32_t)(g.t_s - 1);
-          if (last)  // re-armed for the next launch
-            __hip_atomic_store(g.t_ctr + ptile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          *flag = last;
-        }
-        __syncthreads();
-        if (*flag == 0) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        // one accumulator row i at a time over the pieces (a runtime loop): at most
-        // 2 WNB loads in flight on top of the accumulators
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-#pragma unroll
-          for (int j = 0; j < 2 * WNB; ++j) acc4[i][j] = (f32x4)0.0f;
-          const f32x4* p = slabs + i * 2 * WNB * NT + threadIdx.x;
-          for (int s = 0; s < g.t_s; ++s, p += NV * NT)
-#pragma unroll
-            for (int j = 0; j < 2 * WNB; ++j) acc4[i][j] += p[j * NT];
-        }
-      }
-    }
+    big::mainloop_mf16<WNB>(A, g.lda, B, g.ldb, m0, n0, g.M, g.N, g.K, lds, wave, lane, acc4);
   } else {
   const int nk = g.K / BK;
   big::stage<BM>(A, g.lda, m0, g.M, 0, lds, wave, lane);
@@ -1470,27 +1318,6 @@ static int launch_big(const Args& g, int batch, int wnb, hipStream_t st) {
   return check_launch("gemm_big_kernel");
 }
 
-// The tail form of the big-tile kernel (TailPlan; g.t_* set): np piece blocks, then the
-// full waves' tiles.
-template <typename TO>
-static int launch_tail(int epi, const Args& g, hipStream_t st) {
-  static_assert(TAIL_SLAB == (int64_t)big::NT * 8 * 6 * 4, "slab = the WNB = 3 accumulators");
-  const unsigned grid = (unsigned)(g.t_np + (g.t_m1 / big::BM) * (g.N / 384));
-  prof_begin(st);
-  switch (epi) {
-#define IRC_TAILK(E)                                                                         \
-  case E:                                                                                    \
-    hipLaunchKernelGGL((gemm_big_kernel<TO, E, 3, false, true>), dim3(grid), dim3(big::NT), 0, \
-                       st, g);                                                               \
-    break;
-    IRC_TAILK(0) IRC_TAILK(1) IRC_TAILK(2) IRC_TAILK(3) IRC_TAILK(4) IRC_TAILK(5) IRC_TAILK(6)
-#undef IRC_TAILK
-  }
-  prof_end("gemm_bf16", st, 2.0 * g.M * g.N * g.K);
-  prof_work("gemm_bf16_bytes", gemm_alg_bytes(sizeof(TO) == 4, epi, g.accumulate, g.M, g.N, g.K, 1));
-  return check_launch("gemm_big_kernel(tail)");
-}
-
 template <typename TI, typename TO, int LA, int LB, int EPI>
 static int launch(const Args& g0, int batch, int splits, hipStream_t st) {
   if constexpr (sizeof(TI) == 2) {
@@ -1576,8 +1403,6 @@ extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue,
     if (sp > s) s = sp;
   }
   int64_t bytes = s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
-  if (in_dtype == 0 && batch == 1)  // the wave tail's piece slabs
-    bytes = std::max(bytes, gemm::tail_bytes(gemm::tail_plan(M, N, K)));
   return bytes;
 }
 
@@ -1700,25 +1525,6 @@ extern "C" int irc_gemm_set_big_ring(int on) {
   return irc::gemm::big_ring_mode().exchange(on ? 1 : 0);
 }
 
-// Wave-tail form of the big-tile GEMM (1, the default) or off (0); returns the
-// previous setting.
-extern "C" int irc_gemm_set_tail(int on) {
-  return irc::gemm::tail_mode().exchange(on ? 1 : 0);
-}
-
-// The wave-tail plan irc_gemm would use for a bf16 M x N x K GEMM on this device:
-// out[0] = rows of the whole-tile part (0: no tail form), out[1] = tail tiles,
-// out[2] = K pieces per tile, out[3] = K per piece.
-extern "C" int irc_gemm_tail_plan(int64_t M, int64_t N, int64_t K, int64_t* out) {
-  IRC_REQUIRE(out != nullptr, "gemm_tail_plan: out required");
-  const irc::gemm::TailPlan p = irc::gemm::tail_plan(M, N, K);
-  out[0] = p.M1;
-  out[1] = p.R;
-  out[2] = p.S;
-  out[3] = p.kc;
-  return IRC_OK;
-}
-
 // dtype codes: 0 = bf16, 1 = fp32
 extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue,
                         int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
@@ -1759,27 +1565,6 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
                gemm_group_m()};
   hipStream_t st = as_stream(stream);
   const int nb = (int)batch;
-  if (in_dtype == 0 && batch == 1 && a_layout == gemm::ROW && vec_a && vec_b && vec_c) {
-    // wave tail: the full waves as whole tiles, the rest as K pieces in the same launch
-    const gemm::TailPlan tp = gemm::tail_plan(M, N, K);
-    if (tp.M1 > 0 && a_layout == gemm::ROW && b_layout == gemm::ROW && gemm::big_mf16() &&
-        workspace != nullptr && workspace_bytes >= gemm::tail_bytes(tp)) {
-      uint32_t* ctr = gemm::tail_counter(st);
-      if (ctr != nullptr) {
-        gemm::Args gt = g;
-        gt.P = nullptr;
-        gt.t_np = tp.np;
-        gt.t_r = tp.R;
-        gt.t_m1 = (int)tp.M1;
-        gt.t_s = tp.S;
-        gt.t_kc = tp.kc;
-        gt.t_ws = static_cast<float*>(workspace);
-        gt.t_ctr = ctr;
-        return out_dtype == 0 ? gemm::launch_tail<unsigned short>(epilogue, gt, st)
-                              : gemm::launch_tail<float>(epilogue, gt, st);
-      }
-    }
-  }
   if (in_dtype == 0 && pp_enabled()) {
     int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch);
     if (sp > 1 && (workspace == nullptr ||

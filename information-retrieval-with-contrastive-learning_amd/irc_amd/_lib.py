@@ -55,8 +55,6 @@ SIGNATURES = {
     "irc_gemm_workspace": (I64, [I32, I32, I32, I64, I64, I64, I64]),
     "irc_gemm_set_persistent": (I32, [I32]),
     "irc_gemm_set_big_ring": (I32, [I32]),
-    "irc_gemm_set_tail": (I32, [I32]),
-    "irc_gemm_tail_plan": (I32, [I64, I64, I64, P]),
     "irc_gemm_ln": (I32, [I32, I64, I64, I64, P, I64, P, I64, P, P, I64, P, I64, P, I32, P, P, F32,
                           I64, P, P, P, P]),
     "irc_gemm_set_big_mf16": (I32, [I32]),

@@ -35,23 +35,6 @@ def gemm_set_big_ring(on) -> int:
     return int(_lib.load().irc_gemm_set_big_ring(1 if on else 0))
 
 
-def gemm_set_tail(on) -> int:
-    """Wave-tail form of the big-tile bf16 GEMM (irc_gemm_set_tail): True = the last few
-    output tiles of an almost-whole wave count run as split-K pieces in the same launch
-    (the default), False = off.  Returns the previous setting."""
-    return int(_lib.load().irc_gemm_set_tail(1 if on else 0))
-
-
-def gemm_tail_plan(M, N, K):
-    """(rows run as whole tiles, tail tiles, K pieces per tail tile, K per piece) of the
-    wave-tail form for a bf16 M x N x K GEMM on this device (irc_gemm_tail_plan);
-    rows = 0: the plain form runs."""
-    import ctypes
-
-    out = (ctypes.c_int64 * 4)()
-    _lib.call("irc_gemm_tail_plan", int(M), int(N), int(K), ctypes.addressof(out))
-    return tuple(int(v) for v in out)
-
 
 class LnStats:
     """Per-row statistics of a pre-LayerNorm activation: partial (sum, sum of squares)

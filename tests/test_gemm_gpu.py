@@ -471,76 +471,3 @@ def test_pp_persistent_bert_shapes(gpu, b_is_nk):
         ops.gemm_set_persistent(prev)
     for o in outs:
         assert torch.equal(o, ref)
-
-
-@pytest.mark.parametrize("M,N,K,epi,odt", [
-    (33280, 768, 768, 3, torch.bfloat16),    # out-proj + residual at L = 65 (B = 512)
-    (33280, 768, 3072, 3, torch.bfloat16),   # FFN2 + residual at L = 65
-    (33280, 2304, 768, 1, torch.bfloat16),   # QKV at L = 65
-    (33280, 3072, 768, 2, torch.bfloat16),   # FFN1 + GELU at L = 65
-    (34816, 768, 3072, 1, torch.bfloat16),   # bias only at L = 68
-    (33280, 768, 3072, 4, torch.float32),    # residual only, fp32 out
-])
-def test_wave_tail(gpu, M, N, K, epi, odt):
-    """A GEMM whose 256 x 384 output tiles fill whole waves but for a few (M = B L just
-    above a multiple of the rows per wave) runs those tiles as K pieces in the same
-    launch, the last piece of each summing the slabs (gemm.hip TailPlan).  The plan
-    engages; every row against the fp32 reference (tolerances of test_epilogues) and
-    against the tail-off form; two runs bit-identical (fixed summation order); a second
-    input of the same shape right after the first (no stale slab or ticket)."""
-    from irc_amd import ops
-
-    m1, r, s, kc = ops.gemm_tail_plan(M, N, K)
-    assert 0 < m1 < M and r >= 1 and s >= 2 and kc % 64 == 0, (m1, r, s, kc)
-    prev = ops.gemm_set_tail(True)
-    try:
-        for seed in (0, 1):
-            g = torch.Generator().manual_seed(M + N + K + epi + 7 * seed)
-            a = (torch.randn(M, K, generator=g) * 0.5).bfloat16()
-            b = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16()
-            bias = torch.randn(N, generator=g) if epi in (1, 2, 3) else None
-            res = torch.randn(M, N, generator=g).to(odt) if epi in (3, 4) else None
-            args = dict(bias=None if bias is None else bias.to(gpu), epilogue=epi,
-                        residual=None if res is None else res.to(gpu), out_dtype=odt, alpha=0.5)
-            ag, bg = a.to(gpu), b.to(gpu)
-            out = ops.gemm(ag, bg, **args)
-            again = ops.gemm(ag, bg, **args)
-            ops.gemm_set_tail(False)
-            off = ops.gemm(ag, bg, **args)
-            ops.gemm_set_tail(True)
-            torch.cuda.synchronize()
-            assert torch.equal(out, again)
-            rows = torch.cat([torch.arange(0, 300), torch.arange(m1 - 300, M)])
-            ref = _ref(a[rows], b, False, True, bias, epi, None if res is None else res[rows], 0.5)
-            got = out.float().cpu()[rows]
-            rel = (got - ref).abs().max().item() / ref.abs().max().item()
-            assert rel < (1e-2 if odt == torch.bfloat16 else 2e-3), rel
-            d = (out.float() - off.float()).abs().max().item() / off.float().abs().max().item()
-            assert d < (1e-2 if odt == torch.bfloat16 else 1e-5), d
-    finally:
-        ops.gemm_set_tail(prev)
-
-
-def test_wave_tail_concurrent_streams(gpu):
-    """Tail-form launches on two streams at once take separate ticket slots: the
-    results equal the one-stream ones bit for bit."""
-    from irc_amd import ops
-
-    M, N, K = 33280, 768, 768
-    assert ops.gemm_tail_plan(M, N, K)[0] > 0
-    g = torch.Generator().manual_seed(11)
-    xs = [(torch.randn(M, K, generator=g) * 0.5).bfloat16().to(gpu) for _ in range(2)]
-    b = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16().to(gpu)
-    bias = torch.randn(N, generator=g).to(gpu)
-    ref = [ops.gemm(x, b, bias=bias, epilogue=1) for x in xs]
-    torch.cuda.synchronize()
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    outs = []
-    for rep in range(3):
-        for st, x in ((s1, xs[0]), (s2, xs[1])):
-            st.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(st):
-                outs.append(ops.gemm(x, b, bias=bias, epilogue=1))
-    torch.cuda.synchronize()
-    for k, o in enumerate(outs):
-        assert torch.equal(o, ref[k % 2])

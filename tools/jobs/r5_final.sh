@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round 5 closing run on the final code: the whole GPU suite, smoke, bench.py (default
+# line), rocprofv3 kernel-trace summaries of the train and scan parts, HBM traffic of
+# the bench's GEMM family (FETCH_SIZE / WRITE_SIZE passes).
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r5fin
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/ \
+  > $O/pytest_gpu.log 2>&1
+rc=$?
+tail -2 $O/pytest_gpu.log
+[ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/pytest_gpu.log | head; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { tail $O/bench.log; exit 1; }
+tail -1 $O/bench.log | cut -c1-400
+cp gpurun_out/bench_detail.json $O/bench_detail.json 2>/dev/null
+export TMPDIR=/tmp
+cd /tmp || exit 1
+for part in train scan_c2; do
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$part -o run -- \
+    python3 $R/bench.py --part $part --steps 10 --warmup 3 --no-cpu-baseline > $O/prof_$part.log 2>&1 \
+    || { tail $O/prof_$part.log; exit 1; }
+done
+cd $R || exit 1
+python3 tools/prof_summary.py $O/prof_train > $O/train_kernels.txt && head -12 $O/train_kernels.txt
+python3 tools/prof_summary.py $O/prof_scan_c2 > $O/scan_kernels.txt && head -8 $O/scan_kernels.txt
+PMC_PARTS="train scan_c2" timeout -k 10 900 bash tools/pmc_traffic.sh > $O/pmc.log 2>&1 || { tail $O/pmc.log; exit 1; }
+tail -4 $O/pmc.log

@@ -15,3 +15,6 @@ timeout -k 10 400 python -u tools/e2e_probe.py --steps 30 --by-len --lens 62,64,
 grep -E "ms/step" gpurun_out/r5_m_probe.log | grep real
 timeout -k 10 400 python -u tools/e2e_train.py --steps 80 > gpurun_out/r5_m_e2e.log 2>&1 || exit $?
 grep -E "end-to-end" gpurun_out/r5_m_e2e.log
+timeout -k 10 300 python -u tools/step_events.py --steps 30 --L 64 > gpurun_out/r5_m_events64.log 2>&1 || exit $?
+timeout -k 10 300 python -u tools/step_events.py --steps 30 --L 65 > gpurun_out/r5_m_events65.log 2>&1 || exit $?
+grep -A8 "step" gpurun_out/r5_m_events64.log gpurun_out/r5_m_events65.log
