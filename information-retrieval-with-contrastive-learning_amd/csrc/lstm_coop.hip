@@ -5,9 +5,12 @@
 // Why: a single-CU recurrence must stream all of W_hh (512 KB bf16 per
 // direction) through one CU every step; the per-CU L2 path bounds that at
 // ~3.4 us/step.  Here each (group of 32 sequences, direction) is a CLUSTER of
-// P = 4 workgroups, one per CU, each holding a quarter of W_hh resident in LDS
-// (128 KB) for the whole sequence, so the per-step traffic is only the hidden
-// state exchange.
+// P = 4 workgroups, one per CU, each holding a quarter of W_hh (128 KB) resident
+// for the whole sequence -- in VGPRs since round 5 (each wave's MFMA B fragments,
+// 128 VGPRs of its 406 / 360; re-read from LDS every step they set the MFMA phase:
+// forward 287 -> 267 us, backward 357 -> 304 us per layer at C2,
+// profiles/r05_p_coop.txt) -- so the per-step traffic is only the hidden state
+// exchange.  One workgroup per CU by VGPRs (4 waves at > 256 each).
 //
 // Forward: member m owns hidden units [64m, 64m+64) and all four gates of them;
 //   per step gates[32 x 256] = xp_t + h_{t-1}[32 x 256] . W_slice with
@@ -28,7 +31,7 @@
 // are double-buffered by step parity (a member can be at most one step ahead of
 // any other) and zeroed by hipMemsetAsync every call (tag 0 is never an epoch).
 // Co-residency: <= 16 groups per launch (<= 128 workgroups per direction pair,
-// one per CU by LDS), so two concurrent launches (query and key encoders) fit
+// one per CU), so two concurrent launches (query and key encoders) fit
 // the 256 CUs; spins are bounded and set a timeout word instead of hanging.
 #include <cstdlib>
 
@@ -194,20 +197,47 @@ __device__ __forceinline__ Member decode() {
   return Member{rest & 3, (rest >> 2) * 8 + (bx & 7), (int)blockIdx.y};
 }
 
+#ifdef IRC_COOP_STAMPS  // diagnostic build: per-step phase stamps of block 0 (member 0 of
+// cluster 0, direction 0), wave 0 of the forward -- 0 step top, 1 MFMAs issued, 2 first
+// barrier passed, 3 cell update + publish issued, 4 gather complete, 5 gathered h in LDS
+// + saves / hout issued, 6 last barrier passed.  s_memtime (shader clock) and
+// s_memrealtime (100 MHz); read by irc_coop_dbg_stamps (this build only).
+__device__ uint64_t coop_stamps[64][7][2];
+#define CSTAMP(s, i)                                                                       \
+  do {                                                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && (s) < 64) {              \
+      uint64_t c_, r_;                                                                     \
+      asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)"            \
+                   : "=s"(c_), "=s"(r_)::"memory");                                        \
+      *(volatile uint64_t*)&coop_stamps[(s)][(i)][0] = c_;                                 \
+      *(volatile uint64_t*)&coop_stamps[(s)][(i)][1] = r_;                                 \
+    }                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+  } while (0)
+#else
+#define CSTAMP(s, i) \
+  do {               \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------- forward
 // xp [B*L][ndir*4H] fp32 with per-unit interleaved gates (column 4u+g, plus
 // b_ih + b_hh), wpk [ndir][P][NW][4][KKF][64][8] bf16 (forward fragments),
 // hout [B*L][ndir*H] bf16; gsave/csave (may be null) in the member-fragment
-// order read back by lstm_bwd_coop; xch [ndir][ngrp][2][BG][H] bf16, flags
-// [ndir][ngrp][P] (zeroed), tmo [1].
+// order read back by lstm_bwd_coop; xch [ndir][ngrp][2][BG][H] bf16 granules, tmo [1].
+// The member's W slice lives in VGPRs (each wave's 4 gates x 8 k-steps of B fragments,
+// 128 VGPRs), not in LDS: re-reading it from LDS every step (32 KB per wave, 128 KB
+// per CU) set the step's MFMA phase (~1.9 us of a stamped 7.8 us step at 72 cycles
+// per MFMA, profiles/r05_o_coop_stamps_bg32.txt).
 __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     const float* __restrict__ xp, const unsigned short* __restrict__ wpk,
     unsigned short* __restrict__ hout, float* __restrict__ gsave, float* __restrict__ csave,
     unsigned short* __restrict__ hprev, unsigned short* xch, unsigned* flags, unsigned* tmo, int B,
     int L, int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max, int sentinels,
     int wpub) {
-  __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
-  __shared__ __attribute__((aligned(16))) unsigned short hb[BG][HP];
+  constexpr int RB = 2, BGT = BG;  // 16-row blocks per wave, sequences per cluster
+  __shared__ __attribute__((aligned(16))) unsigned short hb[BGT][HP];
   __shared__ int abort_lds;
   const Member mb = decode();
   if (mb.grp >= ngrp_launch) return;  // the whole cluster is absent
@@ -216,19 +246,23 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r16 = lane & 15, q4 = lane >> 4;
-  const int b0 = grp * BG;
+  const int b0 = grp * BGT;
   const int64_t xld = (int64_t)ndir * 4 * H, hld = (int64_t)ndir * H;
 
+  bf16x8 wr[4][KKF];  // this wave's W fragments: gate g, k-step kk
   {  // resident W slice + zero h_{-1}
     const u16x8* src = reinterpret_cast<const u16x8*>(wpk + (int64_t)(dir * P + m) * WSLICE);
-    u16x8* dst = reinterpret_cast<u16x8*>(wl);
-    for (int i = threadIdx.x; i < WSLICE / 8; i += NTH) dst[i] = src[i];
-    for (int i = threadIdx.x; i < BG * HP; i += NTH) (&hb[0][0])[i] = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int kk = 0; kk < KKF; ++kk)
+        wr[g][kk] = *reinterpret_cast<const bf16x8*>(&src[((w * 4 + g) * KKF + kk) * 64 + lane]);
+    for (int i = threadIdx.x; i < BGT * HP; i += NTH) (&hb[0][0])[i] = 0;
     if (threadIdx.x == 0) abort_lds = 0;
   }
   if (hprev) {  // h_{-1} = 0: the first step's row of hprev (own slice)
     const int t0 = dir == 0 ? 0 : L - 1;
-    for (int p = threadIdx.x; p < BG * UPW / 8; p += NTH) {
+    for (int p = threadIdx.x; p < BGT * UPW / 8; p += NTH) {
       const int row = p / (UPW / 8), col = m * UPW + (p % (UPW / 8)) * 8;
       if (b0 + row < B)
         *reinterpret_cast<u16x8*>(hprev + (((int64_t)dir * B + b0 + row) * L + t0) * H + col) =
@@ -236,14 +270,14 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
     }
   }
   const int u = m * UPW + w * UPV + r16;  // this lane's hidden unit
-  float c[2][4];
+  float c[RB][4];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) c[rb][i] = 0.f;
-  auto load_xp = [&](int t, f32x4 (&dst)[2][4]) {
+  auto load_xp = [&](int t, f32x4 (&dst)[RB][4]) {
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         int b = b0 + rb * 16 + 4 * q4 + i;
@@ -252,45 +286,45 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
                                                      (int64_t)dir * 4 * H + 4 * u);
       }
   };
-  f32x4 xr[2][4];
+  f32x4 xr[RB][4];
   load_xp(dir == 0 ? 0 : L - 1, xr);
-  // granules [2 parity][BG][H/2]: {epoch, two bf16 of units 2c, 2c+1}
+  // granules [2 parity][BGT][H/2]: {epoch, two bf16 of units 2c, 2c+1}
   unsigned long long* X =
-      reinterpret_cast<unsigned long long*>(xch) + (int64_t)(dir * ngrp_total + grp) * 2 * BG * (H / 2);
+      reinterpret_cast<unsigned long long*>(xch) + (int64_t)(dir * ngrp_total + grp) * 2 * BGT * (H / 2);
   (void)flags;
   __syncthreads();
 
   for (int s = 0; s < L; ++s) {
+    CSTAMP(s, 0);
     const int t = dir == 0 ? s : L - 1 - s;
-    f32x4 acc[2][4];
+    f32x4 acc[RB][4];
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[rb][g][i] = xr[rb][i][g];
     if (s + 1 < L) load_xp(dir == 0 ? t + 1 : t - 1, xr);
     if (s > 0) {
-#pragma unroll 2
-      for (int kk = 0; kk < KKF; ++kk) {
-        bf16x8 a[2];
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
+      for (int kk = 0; kk < KKF; ++kk) {
+        bf16x8 a[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
           a[rb] = *reinterpret_cast<const bf16x8*>(&hb[rb * 16 + r16][kk * 32 + 8 * q4]);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(
-              &wl[(((w * 4 + g) * KKF + kk) * 64 + lane) * 8]);
+        for (int g = 0; g < 4; ++g)
 #pragma unroll
-          for (int rb = 0; rb < 2; ++rb)
-            acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw, acc[rb][g], 0, 0, 0);
-        }
+          for (int rb = 0; rb < RB; ++rb)
+            acc[rb][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], wr[g][kk], acc[rb][g], 0, 0, 0);
       }
     }
+    CSTAMP(s, 1);
     __syncthreads();  // every read of h_{t-1} done
-    f32x4 gv[2][4], cv[2];
+    CSTAMP(s, 2);
+    f32x4 gv[RB][4], cv[RB];
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float ig = sigm(acc[rb][0][i]);
@@ -304,72 +338,77 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         cv[rb][i] = cn;
       }
     if (wpub) {
-      // per-wave publish: this wave's 16 units x 32 rows go out as soon as the wave
-      // has written them (LDS ops of one wave complete in order: no barrier), as 2
-      // granule pairs per lane, and its hout / hprev rows as one 16-byte store per lane
-      const int row = lane >> 1, col = m * UPW + w * UPV + 8 * (lane & 1);
+      // per-wave publish: this wave's 16 units x BGT rows go out as soon as the wave
+      // has written them (LDS ops of one wave complete in order: no barrier), as RB
+      // granule pairs per lane, and its hout / hprev rows as 16-byte stores per lane
       if (s + 1 < L) {
-        unsigned long long* Xp = X + (s & 1) * BG * (H / 2);
+        unsigned long long* Xp = X + (s & 1) * BGT * (H / 2);
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < RB; ++k) {
           const int idx = k * 64 + lane, pr = idx >> 2, pc = m * UPW + w * UPV + 4 * (idx & 3);
           const uint2 hv = *reinterpret_cast<const uint2*>(&hb[pr][pc]);
           st_sc1_pair(Xp + pr * (H / 2) + pc / 2, granule((unsigned)(s + 1), hv.x),
                       granule((unsigned)(s + 1), hv.y));
         }
       }
-      if (b0 + row < B) {
-        const u16x8 hv = *reinterpret_cast<const u16x8*>(&hb[row][col]);
-        *reinterpret_cast<u16x8*>(hout + ((int64_t)(b0 + row) * L + t) * hld + dir * H + col) = hv;
-        const int tn = dir == 0 ? t + 1 : t - 1;
-        if (hprev && tn >= 0 && tn < L)
-          *reinterpret_cast<u16x8*>(hprev + (((int64_t)dir * B + b0 + row) * L + tn) * H + col) =
-              hv;
+#pragma unroll
+      for (int h2 = 0; h2 < RB / 2; ++h2) {
+        const int row = 32 * h2 + (lane >> 1), col = m * UPW + w * UPV + 8 * (lane & 1);
+        if (b0 + row < B) {
+          const u16x8 hv = *reinterpret_cast<const u16x8*>(&hb[row][col]);
+          *reinterpret_cast<u16x8*>(hout + ((int64_t)(b0 + row) * L + t) * hld + dir * H + col) = hv;
+          const int tn = dir == 0 ? t + 1 : t - 1;
+          if (hprev && tn >= 0 && tn < L)
+            *reinterpret_cast<u16x8*>(hprev + (((int64_t)dir * B + b0 + row) * L + tn) * H + col) =
+                hv;
+        }
       }
     } else {
       __syncthreads();  // own slice of h_t complete in LDS
     }
+    CSTAMP(s, 3);
     if (s + 1 < L) {
-      // publish the own 32 x 64 slice as 1024 granules (2 pairs per thread) ...
+      // publish the own BGT x 64 slice as granules (2 per store) ...
       const unsigned ep = (unsigned)(s + 1);
-      unsigned long long* Xp = X + (s & 1) * BG * (H / 2);
+      unsigned long long* Xp = X + (s & 1) * BGT * (H / 2);
 #pragma unroll
-      for (int k = 0; k < BG * UPW / 4 / NTH; ++k) {
+      for (int k = 0; k < BGT * UPW / 4 / NTH; ++k) {
         if (wpub) break;
         const int p = k * NTH + threadIdx.x;
         const int row = p / (UPW / 4), c2 = m * (UPW / 2) + (p % (UPW / 4)) * 2;
         const uint2 hv = *reinterpret_cast<const uint2*>(&hb[row][2 * c2]);
         st_sc1_pair(Xp + row * (H / 2) + c2, granule(ep, hv.x), granule(ep, hv.y));
       }
-      // ... and gather the other three (12 granules per thread)
+      // ... and gather the other three
       if (sentinels) {  // sentinel: each producer's first granule (own slot: already ours)
         const unsigned long long* sent[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) sent[q] = Xp + q * (UPW / 2);
         poll_sentinels(sent, ep, tmo, &abort_lds, spin_max);
       }
-      constexpr int NG = 3 * BG * UPW / 2 / NTH;
+      constexpr int NG = 3 * BGT * UPW / 2 / NTH;
       unsigned v[NG];
       auto addr = [&](int k) {
         const int idx = k * NTH + threadIdx.x;
-        const int mm = (m + 1 + idx / (BG * UPW / 2)) & 3, loc = idx % (BG * UPW / 2);
+        const int mm = (m + 1 + idx / (BGT * UPW / 2)) & 3, loc = idx % (BGT * UPW / 2);
         return Xp + (loc / (UPW / 2)) * (H / 2) + mm * (UPW / 2) + loc % (UPW / 2);
       };
       sweep<NG>(addr, ep, v, tmo, &abort_lds, spin_max);
+      CSTAMP(s, 4);
 #pragma unroll
       for (int k = 0; k < NG; ++k) {
         const int idx = k * NTH + threadIdx.x;
-        const int mm = (m + 1 + idx / (BG * UPW / 2)) & 3, loc = idx % (BG * UPW / 2);
+        const int mm = (m + 1 + idx / (BGT * UPW / 2)) & 3, loc = idx % (BGT * UPW / 2);
         *reinterpret_cast<unsigned*>(&hb[loc / (UPW / 2)][2 * (mm * (UPW / 2) + loc % (UPW / 2))]) =
             v[k];
       }
     }
-    // saves + h_t rows (own slice) after the hand-off: they drain under the next MFMAs
+    // saves + h_t rows (own slice) after the hand-off: they drain under the next MFMAs.
     if (gsave) {
       float* gs = gsave + ((int64_t)(dir * ngrp_total + grp) * L + t) * GSTEP;
       float* cs = csave + ((int64_t)(dir * ngrp_total + grp) * L + t) * CSTEP;
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
+      for (int rb = 0; rb < RB; ++rb) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           *reinterpret_cast<f32x4*>(gs + ((((m * NW + w) * 2 + rb) * 4 + i) * 64 + lane) * 4) =
@@ -377,7 +416,7 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
         *reinterpret_cast<f32x4*>(cs + (((m * NW + w) * 2 + rb) * 64 + lane) * 4) = cv[rb];
       }
     }
-    for (int p = threadIdx.x; p < BG * UPW / 8 && !wpub; p += NTH) {  // h_t -> hout (own slice)
+    for (int p = threadIdx.x; p < BGT * UPW / 8 && !wpub; p += NTH) {  // h_t -> hout (own slice)
       const int row = p / (UPW / 8), col = m * UPW + (p % (UPW / 8)) * 8;
       if (b0 + row < B) {
         const u16x8 hv = *reinterpret_cast<const u16x8*>(&hb[row][col]);
@@ -389,7 +428,9 @@ __global__ __launch_bounds__(NTH, 1) void lstm_fwd_coop(
               hv;
       }
     }
+    CSTAMP(s, 5);
     __syncthreads();  // h_t complete for the next step (and the abort word)
+    CSTAMP(s, 6);
     if (abort_lds) return;
   }
 }
@@ -408,7 +449,6 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
     const float* __restrict__ gsave, const float* __restrict__ csave,
     unsigned short* __restrict__ dg, float* xch, unsigned* flags, unsigned* tmo, int B, int L,
     int ndir, int grp0, int ngrp_launch, int ngrp_total, unsigned spin_max, int tagged) {
-  __shared__ __attribute__((aligned(16))) unsigned short wl[WSLICE];  // 128 KB
   __shared__ __attribute__((aligned(16))) unsigned short dgl[BG][HP];  // own dgates, k = g*64+lu
   __shared__ int abort_lds;
   const Member mb = decode();
@@ -420,10 +460,14 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
   const int r16 = lane & 15, q4 = lane >> 4;
   const int b0 = grp * BG;
   const int64_t hld = (int64_t)ndir * H, gld = (int64_t)ndir * 4 * H;
+  bf16x8 wr[4][KKB];  // this wave's W^T fragments (VGPRs, as the forward's): block cb, k-step kk
   {
     const u16x8* src = reinterpret_cast<const u16x8*>(wtpk + (int64_t)(dir * P + m) * WSLICE);
-    u16x8* dst = reinterpret_cast<u16x8*>(wl);
-    for (int i = threadIdx.x; i < WSLICE / 8; i += NTH) dst[i] = src[i];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int kk = 0; kk < KKB; ++kk)
+        wr[cb][kk] = *reinterpret_cast<const bf16x8*>(&src[((w * 4 + cb) * KKB + kk) * 64 + lane]);
     if (threadIdx.x == 0) abort_lds = 0;
   }
   // cell ownership as in the forward: lane -> unit u (own), rows rb*16 + 4*q4 + i
@@ -485,20 +529,17 @@ __global__ __launch_bounds__(NTH, 1) void lstm_bwd_coop(
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) acc[rb][cb] = (f32x4)0.f;
-#pragma unroll 2
+#pragma unroll
       for (int kk = 0; kk < KKB; ++kk) {
         bf16x8 a[2];
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
           a[rb] = *reinterpret_cast<const bf16x8*>(&dgl[rb * 16 + r16][kk * 32 + 8 * q4]);
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(
-              &wl[(((w * 4 + cb) * KKB + kk) * 64 + lane) * 8]);
+        for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb)
-            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], bw, acc[rb][cb], 0, 0, 0);
-        }
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], wr[cb][kk], acc[rb][cb], 0, 0, 0);
       }
       const unsigned ep = (unsigned)s;
       if (tagged == 1) {
@@ -737,7 +778,7 @@ static unsigned coop_spin_max() {
 
 // Clusters per launch such that every workgroup of the q- and k-encoder launches
 // (which may run concurrently on two streams) is co-resident: one workgroup per
-// CU (128 KB LDS each), so 2 * groups * P * ndir <= CUs.  The CU count comes
+// CU (by VGPRs), so 2 * groups * P * ndir <= CUs.  The CU count comes
 // from the device, not a constant; on MI355X (256 CUs, ndir 2) this is 16.
 static int coop_groups_per_launch(int64_t ndir) {
   int dev = 0, cus = 0;
@@ -835,3 +876,11 @@ extern "C" int irc_lstm_coop_fault(const void* sync, int64_t B, int64_t ndir, vo
                      static_cast<unsigned*>(fault));
   return check_launch("lstm_coop_fault");
 }
+
+#ifdef IRC_COOP_STAMPS
+extern "C" int irc_coop_dbg_stamps(uint64_t* out /* [64][7][2] */) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(irc::lstmc::coop_stamps),
+                             sizeof(irc::lstmc::coop_stamps)) == hipSuccess ? 0 : -1;
+}
+#endif
