@@ -9,7 +9,8 @@
 // for the whole sequence -- in VGPRs since round 5 (each wave's MFMA B fragments,
 // 128 VGPRs of its 406 / 360; re-read from LDS every step they set the MFMA phase:
 // forward 287 -> 267 us, backward 357 -> 304 us per layer at C2,
-// profiles/r05_p_coop.txt) -- so the per-step traffic is only the hidden state
+// profiles/r05_p_coop.txt; with the v_rcp_f32 gates below 221 / 291 us,
+// profiles/r05_q_coop.txt) -- so the per-step traffic is only the hidden state
 // exchange.  One workgroup per CU by VGPRs (4 waves at > 256 each).
 //
 // Forward: member m owns hidden units [64m, 64m+64) and all four gates of them;
@@ -59,8 +60,13 @@ constexpr int NFLAG = P * NW;                // backward flag words per (dir, gr
 typedef __attribute__((address_space(1))) unsigned int gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
-__device__ __forceinline__ float tanh_f(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
+// v_rcp_f32 (1 ulp) instead of the correctly rounded division (~12 instructions with its
+// scale / fixup and denormal-mode switches): 40 of them per lane per step were most of
+// the recurrence's cell update (profiles/r05_p_coop_stamps.txt)
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_f(float x) {
+  return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f;
+}
 
 __device__ __forceinline__ void st_sc1(void* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -29,8 +29,13 @@ constexpr int BG = 32;   // sequences per workgroup (M of the MFMA)
 constexpr int NW = 8;    // waves per workgroup (2 per SIMD)
 constexpr int NTH = NW * 64;
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
-__device__ __forceinline__ float tanh_f(float x) { return 2.f / (1.f + __expf(-2.f * x)) - 1.f; }
+// v_rcp_f32 (1 ulp) instead of the correctly rounded division (~12 instructions with its
+// scale / fixup and denormal-mode switches): 40 of them per lane per step were most of
+// the recurrence's cell update (profiles/r05_p_coop_stamps.txt)
+__device__ __forceinline__ float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_f(float x) {
+  return 2.f * __builtin_amdgcn_rcpf(1.f + __expf(-2.f * x)) - 1.f;
+}
 
 template <int H>
 struct Geo {
