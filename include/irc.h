@@ -157,7 +157,11 @@ int irc_gemm_set_big_ring(int on);
  *     R = h, ln_stats, ln_gamma, ln_beta (bf16-rounded, as irc_layernorm writes it) when
  *     ln_gamma != NULL, else R itself.
  * stats_out (optional): the partials of C's bf16 values, *stats_nt_out pairs per row.
- * A [M][K], B [N][K], C / R [M][N]-strided bf16; K % 64 == 0, N % 8 == 0, 16-byte rows. */
+ * A [M][K], B [N][K], C / R [M][N]-strided bf16; K % 64 == 0, N % 8 == 0, 16-byte rows.
+ * Not bit-reproducible: each tile's row partials are summed with LDS float atomics in
+ * arrival order, so stats_out (and the LayerNorm that later reads it) can differ in the
+ * last bits from run to run.  The default encoder path (separate LayerNorm kernels,
+ * IRC_LN_FOLD unset) does not use it and is deterministic. */
 int irc_gemm_ln(int epilogue, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                 const void* B, int64_t ldb, const float* bias, const void* R, int64_t ldr,
                 void* C, int64_t ldc, const float* ln_stats, int ln_nt, const float* ln_gamma,

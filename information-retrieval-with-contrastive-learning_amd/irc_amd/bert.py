@@ -148,7 +148,9 @@ class BertModel(nn.Module):
         # "bf16" (default) or "fp8": MX-fp8 weights and inputs (e4m3 with one E8M0 scale
         # per 32 consecutive values) for every nn.Linear of the frozen encoder (config C5)
         self.weight_format = os.environ.get("IRC_ENCODER_WEIGHTS", "bf16")
-        # LayerNorm fold of the bf16 encoder (_encode_folded); IRC_LN_FOLD=0 / 1 overrides
+        # LayerNorm fold of the bf16 encoder (_encode_folded); IRC_LN_FOLD=0 / 1 overrides.
+        # Off by default: measured no faster, and not bit-reproducible (irc_gemm_ln sums
+        # its row statistics with LDS float atomics, include/irc.h)
         self.ln_fold = os.environ.get("IRC_LN_FOLD", "0") != "0"
         # QKV projection + attention in one launch where it applies (bf16, head dim 64,
         # L in ops.QKV_ATTN_FUSED_L; irc_qkv_attention); IRC_QKV_ATTN=0 keeps the
