@@ -7,3 +7,4 @@ timeout -k 10 300 python -u tools/host_time.py --steps 30 > gpurun_out/r5_s_host
 grep -E "alone|wall" gpurun_out/r5_s_host_time.log
 timeout -k 10 300 python -u tools/lstm_coop_repro.py --n 4 > gpurun_out/r5_s_repro.log 2>&1 || exit $?
 tail -6 gpurun_out/r5_s_repro.log
+bash tools/jobs/r5_t.sh
