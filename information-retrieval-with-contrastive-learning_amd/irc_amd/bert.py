@@ -156,6 +156,12 @@ class BertModel(nn.Module):
         # L in ops.QKV_ATTN_FUSED_L; irc_qkv_attention); IRC_QKV_ATTN=0 keeps the
         # two-launch form
         self.fused_attention = os.environ.get("IRC_QKV_ATTN", "1") != "0"
+        # A batch whose B * L rows sit just above a multiple of 32768 (128 row tiles of 256:
+        # whole waves of every BERT GEMM on 256 CUs; a C2 batch of 512 sequences padded to
+        # L = 65) runs as two chunks of whole sequences -- the rows of the whole waves, and
+        # the few left over on a side stream beside them -- instead of one launch per GEMM
+        # whose last wave is nearly empty (IRC_BERT_SPLIT=0: off)
+        self.split_tail = os.environ.get("IRC_BERT_SPLIT", "1") != "0"
         self.eval()
 
     # HF _init_weights: normal(0, 0.02) for Linear/Embedding, padding row 0, LN (1, 0)
@@ -314,14 +320,22 @@ class BertModel(nn.Module):
             prev = lw
         return ops.layernorm(h2, prev["ln2_g"], prev["ln2_b"], eps, out=h2)
 
+    def _fused_applies(self, L):
+        c = self.config
+        return self.fused_attention and ops.qkv_attention_supported(
+            L, c.hidden_size, c.num_attention_heads, ops.QKV_ATTN_FUSED_L)
+
+    @staticmethod
+    def _permute_qkv(lw):
+        if "wqkv_p" not in lw:  # permuted once per cast weight set
+            perm = ops.qkv_perm_index(lw["wqkv"].shape[1], lw["wqkv"].device)
+            lw["wqkv_p"] = lw["wqkv"].index_select(0, perm).contiguous()
+            lw["bqkv_p"] = lw["bqkv"].index_select(0, perm).contiguous()
+
     def _qkv_attention(self, x, lw, mask, B, L, H, heads):
         """ctx of one layer: one fused launch where it applies, else QKV GEMM + attention."""
-        if self.fused_attention and ops.qkv_attention_supported(L, H, heads,
-                                                                ops.QKV_ATTN_FUSED_L):
-            if "wqkv_p" not in lw:  # permuted once per cast weight set
-                perm = ops.qkv_perm_index(H, lw["wqkv"].device)
-                lw["wqkv_p"] = lw["wqkv"].index_select(0, perm).contiguous()
-                lw["bqkv_p"] = lw["bqkv"].index_select(0, perm).contiguous()
+        if self._fused_applies(L):
+            self._permute_qkv(lw)
             return ops.qkv_attention(x, lw["wqkv_p"], lw["bqkv_p"], mask, B, L, H, heads)
         qkv = ops.gemm(x, lw["wqkv"], bias=lw["bqkv"], epilogue=ops.EPI_BIAS)
         return ops.attention(qkv, mask, B, L, H, heads)
@@ -337,13 +351,65 @@ class BertModel(nn.Module):
             raise ValueError(f"sequence length {L} > max_position_embeddings")
         H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
         w = self._weights()
-        if self._fp8_mode():
-            return self._encode_fp8(ids, mask, w).view(B, L, H)
         if self.ln_fold and compute_dtype() == torch.bfloat16:
             return self._encode_folded(ids, mask, w).view(B, L, H)
+        n1 = self._split_point(B, L) if ids.is_cuda else 0
+        if n1:
+            return self._encode_split(ids, mask, w, n1).view(B, L, H)
+        return self._encode_rows(ids, mask, w).view(B, L, H)
+
+    # rows of one set of whole waves of every BERT GEMM (128 row tiles of 256)
+    SPLIT_ROWS = 32768
+
+    def _split_point(self, B: int, L: int) -> int:
+        """Sequences of the whole-wave chunk, or 0 (no split): only when the rows past
+        the last multiple of SPLIT_ROWS are a small remainder (<= 1/4 of it)."""
+        if not self.split_tail or self.ln_fold:
+            return 0
+        M, R = B * L, self.SPLIT_ROWS
+        full = M // R * R
+        if full == 0 or M - full > R // 4 or M == full:
+            return 0
+        n1 = full // L
+        return n1 if 0 < n1 < B else 0
+
+    def _encode_split(self, ids, mask, w, n1):
+        """encode() as two chunks of whole sequences (every op is per row except the
+        attention, which is per sequence): rows [0, n1 L) on the calling stream, the
+        rest on a side stream beside them, both writing their slice of one output."""
+        from ._torch import side_stream
+
+        B, L = ids.shape
+        H = self.config.hidden_size
+        dev = ids.device
+        dt = torch.bfloat16 if compute_dtype() == torch.bfloat16 else torch.float32
+        out = torch.empty((B * L, H), dtype=dt, device=dev)
+        if dt == torch.bfloat16 and not self._fp8_mode() and self._fused_applies(L):
+            for lw in w["layers"]:  # created on this stream, before the side stream waits
+                self._permute_qkv(lw)
+        cur = torch.cuda.current_stream(dev)
+        side = side_stream(dev, "bert_tail")
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self._encode_rows(ids[n1:], mask[n1:], w, out=out[n1 * L:])
+        for t in (ids, mask, out):
+            t.record_stream(side)
+        self._encode_rows(ids[:n1], mask[:n1], w, out=out[:n1 * L])
+        cur.wait_stream(side)
+        return out
+
+    def _encode_rows(self, ids, mask, w, out=None):
+        """The encoder over whole sequences ids [B, L] -> [B L, H]; the last LayerNorm
+        writes into `out` when given."""
+        c = self.config
+        B, L = ids.shape
+        H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
+        if self._fp8_mode():
+            return self._encode_fp8(ids, mask, w, out=out)
         x = ops.embed_ln(ids, w["word"], w["pos"], w["type0"], w["ln_g"], w["ln_b"], eps)
         bf16 = compute_dtype() == torch.bfloat16
-        for lw in w["layers"]:
+        nl = len(w["layers"])
+        for li, lw in enumerate(w["layers"]):
             if bf16:
                 ctx = self._qkv_attention(x, lw, mask, B, L, H, heads)
             else:
@@ -353,10 +419,11 @@ class BertModel(nn.Module):
             a = ops.layernorm(a, lw["ln1_g"], lw["ln1_b"], eps, out=a)
             i = ops.gemm(a, lw["w1"], bias=lw["b1"], epilogue=ops.EPI_BIAS_GELU)
             x = ops.gemm(i, lw["w2"], bias=lw["b2"], residual=a, epilogue=ops.EPI_BIAS_RESID)
-            x = ops.layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, out=x)
-        return x.view(B, L, H)
+            last = li + 1 == nl and out is not None
+            x = ops.layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, out=out if last else x)
+        return x
 
-    def _encode_fp8(self, ids, mask, w):
+    def _encode_fp8(self, ids, mask, w, out=None):
         """encode() with every nn.Linear on MX-fp8 (irc_gemm_mx, config C5): e4m3
         operands with one power-of-two scale per 32 k of a row, applied inside the
         MFMA.  Each GEMM input arrives already quantised from its producer -- the
@@ -381,7 +448,7 @@ class BertModel(nn.Module):
             if li + 1 < nl:
                 x, x8 = ops.layernorm_mx(x, lw["ln2_g"], lw["ln2_b"], eps, out=x)
             else:
-                x = ops.layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, out=x)
+                x = ops.layernorm(x, lw["ln2_g"], lw["ln2_b"], eps, out=out if out is not None else x)
         return x
 
     def forward(self, input_ids=None, attention_mask=None, **kw):
