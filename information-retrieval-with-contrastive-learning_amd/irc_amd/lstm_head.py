@@ -77,6 +77,39 @@ def _layout(specs):
     return offs, total
 
 
+
+def _cu_count(dev) -> int:
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+# Rows of the input projection past its last whole wave (256 x 256 output tiles on all CUs)
+# run beside it on a side stream instead of as a nearly empty last wave of the same launch
+# (B L = 256 x 65 = 16640 rows: 2 waves of 520 tiles + 8; IRC_HEAD_SPLIT=0: off)
+_HEAD_SPLIT = os.environ.get("IRC_HEAD_SPLIT", "1") != "0"
+
+
+def _gemm_rows_split(x, w, b):
+    """xp = x . w^T + b (fp32 out) -- as one GEMM, or, when M sits just above a whole
+    number of waves, as the whole-wave rows here plus the rest on a side stream."""
+    M, N = x.shape[0], w.shape[0]
+    ct = (N + 255) // 256
+    ncu = _cu_count(x.device) if (_HEAD_SPLIT and x.is_cuda) else 0
+    rpw = 256 * (ncu // ct) if ct and ncu % ct == 0 else 0  # rows per wave of tiles
+    full = M // rpw * rpw if rpw else 0
+    if full == 0 or M == full or M - full > rpw // 4:
+        return ops.gemm(x, w, bias=b, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
+    out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    cur = torch.cuda.current_stream(x.device)
+    side = side_stream(x.device, "head_tail")
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        ops.gemm(x[full:], w, bias=b, epilogue=ops.EPI_BIAS, out=out[full:])
+    for t in (x, w, b, out):
+        t.record_stream(side)
+    ops.gemm(x[:full], w, bias=b, epilogue=ops.EPI_BIAS, out=out[:full])
+    cur.wait_stream(side)
+    return out
+
 class LSTMHead(nn.Module):
     """Drop-in for the reference ``LSTM`` module (same config keys and names)."""
 
@@ -211,7 +244,7 @@ class LSTMHead(nn.Module):
             # MFMA recurrence: packed W_ih columns so xp is read as per-unit float4s
             wih, bih, bhh, whh = self._layer_fp32(l)
             wp, bp, w, wT = ops.lstm_pack(wih, bih, bhh, whh, H, nd, whh_packs=kind != "coop")
-            xp = ops.gemm(x, wp, bias=bp, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
+            xp = _gemm_rows_split(x, wp, bp)
             if kind == "coop":
                 wf, wb = ops.lstm_coop_pack(whh, H, nd)
                 hout, gsave, csave, hprev, sync = ops.lstm_fwd_coop(xp, wf, B, L, H, nd,

@@ -1,4 +1,4 @@
-"""The frozen encoder's split form (irc_amd.bert.BertModel._encode_split): a batch whose
+"""Whole-wave splits.  The frozen encoder's split form (irc_amd.bert.BertModel._encode_split): a batch whose
 B L rows sit just above a multiple of 32768 (whole waves of every BERT GEMM) runs as
 the whole-wave chunk of sequences plus the rest on a side stream.  Every op is per row
 except the attention, which is per sequence, so each chunk must equal encoding its
@@ -40,3 +40,24 @@ def test_split_encode(gpu, B, L):
     y0 = m.encode(ids, mask)
     err = (y.float() - y0.float()).abs().max().item()
     assert err <= 3e-2 * y0.float().abs().max().item(), err
+
+
+def test_head_input_projection_split(gpu):
+    """The LSTM head's input projection at B L = 256 x 65 rows (irc_amd.lstm_head.
+    _gemm_rows_split): the whole-wave rows on the calling stream equal the one-launch
+    GEMM bit for bit (same 256 x 256 tiles), the 256 tail rows on the side stream agree
+    within fp32 reassociation (a smaller launch takes another kernel)."""
+    from irc_amd import lstm_head, ops
+
+    g = torch.Generator().manual_seed(3)
+    M, K, N = 256 * 65, 768, 2048
+    x = (torch.randn(M, K, generator=g) * 0.5).bfloat16().to(gpu)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16().to(gpu)
+    b = torch.randn(N, generator=g).to(gpu)
+    ref = ops.gemm(x, w, bias=b, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
+    got = lstm_head._gemm_rows_split(x, w, b)
+    torch.cuda.synchronize()
+    full = M // 8192 * 8192
+    assert full == 16384
+    assert torch.equal(got[:full], ref[:full])
+    assert torch.allclose(got[full:], ref[full:], rtol=1e-5, atol=1e-5)
