@@ -1306,13 +1306,20 @@ bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, i
   // at M = 512 L: 252 big tiles in one wave against 378 in two at L = 63; a batch's
   // joint padding rarely lands on L = 64, and requiring whole waves of big tiles sent
   // every other L to 1.5 waves of 256x256 tiles: 9.29 vs 8.18 ms per C2 step).  Ties
-  // go to the 256x256 kernel (FFN1's N = 3072).
+  // go to the big-tile kernel too (FFN1 + GELU, N = 3072: 4 waves of 256x384 against 6 of
+  // 256x256): alone the two are within a few us either way from box to box, but in the
+  // overlapped C2 step the big tiles gain 4%: 30.9-31.0k vs 29.6-29.7k pairs/s, three
+  // interleaved pairs (profiles/r05_y_ties_ab.txt, r05_w_ffn1_pp_vs_big.txt).
   if (la == 0 && lb == 0 && N % 384 == 0) {
     const int64_t t384 = ((M + 255) / 256) * (N / 384) * batch;
     const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
     int64_t ncu = cu_count();
     if (ncu <= 0) ncu = 256;
+#ifdef IRC_PP_TIES_PP  // diagnostic build: ties to the 256x256 kernel (the round-4 rule)
     if (3 * ((t384 + ncu - 1) / ncu) < 2 * ((t256 + ncu - 1) / ncu)) return false;
+#else
+    if (3 * ((t384 + ncu - 1) / ncu) <= 2 * ((t256 + ncu - 1) / ncu)) return false;
+#endif
   }
   if ((uintptr_t)A % 16 || (uintptr_t)B % 16) return false;
   if (lda % 8 || ldb % 8 || sA % 8 || sB % 8) return false;
