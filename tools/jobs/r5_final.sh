@@ -4,7 +4,7 @@
 # the bench's GEMM family (FETCH_SIZE / WRITE_SIZE passes).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r5fin
+O=$R/gpurun_out/${R5FIN:-r5fin}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/ \
@@ -29,3 +29,5 @@ python3 tools/prof_summary.py $O/prof_train > $O/train_kernels.txt && head -12 $
 python3 tools/prof_summary.py $O/prof_scan_c2 > $O/scan_kernels.txt && head -8 $O/scan_kernels.txt
 PMC_PARTS="train scan_c2" timeout -k 10 900 bash tools/pmc_traffic.sh > $O/pmc.log 2>&1 || { tail $O/pmc.log; exit 1; }
 tail -4 $O/pmc.log
+timeout -k 10 400 python -u tools/e2e_train.py --steps 80 > $O/e2e.log 2>&1 || { tail $O/e2e.log; exit 1; }
+grep -E "end-to-end" $O/e2e.log
