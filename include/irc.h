@@ -130,6 +130,19 @@ int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilog
  * gradients, K = B*L); passing a smaller/NULL workspace disables it. */
 int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M, int64_t N,
                            int64_t K, int64_t batch);
+/* irc_gemm / irc_gemm_workspace with a cap on the split-K launch: at most max_blocks
+ * 256 x 256-tile blocks (0 = the default, 256 = one wave on the chip).  A smaller cap
+ * gives fewer, longer splits: slower alone, but a GEMM that runs beside other work
+ * (the LSTM weight gradients on their side stream) takes fewer CUs from it.  Pass the
+ * same max_blocks to both calls; results stay deterministic for a given cap. */
+int irc_gemm_ex(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue, int64_t M,
+                int64_t N, int64_t K, float alpha, const void* A, int64_t lda, int64_t strideA,
+                const void* B, int64_t ldb, int64_t strideB, const float* bias, int64_t strideBias,
+                const void* R, int64_t ldr, int64_t strideR, void* C, int64_t ldc, int64_t strideC,
+                int accumulate, int64_t batch, void* workspace, int64_t workspace_bytes,
+                int64_t max_blocks, irc_stream_t stream);
+int64_t irc_gemm_workspace_ex(int in_dtype, int out_dtype, int epilogue, int64_t M, int64_t N,
+                              int64_t K, int64_t batch, int64_t max_blocks);
 /* Persistent tile loop of the 256x256 bf16 GEMM, for launches of more output tiles
  * than CUs (batch 1, no split-K, aligned C): mode 0 = one workgroup per tile (the
  * default); 1 = each workgroup takes tiles from a tile counter and DMAs the next

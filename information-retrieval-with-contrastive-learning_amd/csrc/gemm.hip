@@ -426,12 +426,14 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restr
 // 1/16 of the bf16 rate, so a 128-deep slice is already 8 K-steps of real work --
 // the InfoNCE / scaling-layer GEMMs of the heads' step ran on 2-4 workgroups for
 // 50-100 us each before).  Restricted to fp32 C with no fused epilogue.
+// budget: the largest number of split-K blocks, in 256 x 256-tile units (two 128 x 128
+// blocks each); 256 = one wave on MI355X.
 inline int split_count(int TIbytes, int out_f32, int epi, int64_t M, int64_t N, int64_t K,
-                       int64_t batch) {
+                       int64_t batch, int64_t budget = 256) {
   if (!out_f32 || !(epi == EPI_NONE || (epi == EPI_BIAS && TIbytes == 4))) return 1;
   const int64_t tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * batch;
   const int bk = TIbytes == 2 ? TT<unsigned short>::BK : TT<float>::BK;
-  int64_t s = (512 + tiles - 1) / tiles;
+  int64_t s = (2 * budget + tiles - 1) / tiles;
   const int64_t smax = K / (TIbytes == 2 ? 512 : 128);
   if (s > smax) s = smax;
   if (s > (TIbytes == 2 ? 32 : 64)) s = TIbytes == 2 ? 32 : 64;
@@ -1395,15 +1397,23 @@ static bool pp_enabled() {
   return on;
 }
 
-extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M,
-                                      int64_t N, int64_t K, int64_t batch) {
-  int s = gemm::split_count(in_dtype == 0 ? 2 : 4, out_dtype == 1, epilogue, M, N, K, batch);
+static inline int64_t split_budget(int64_t max_blocks) { return max_blocks > 0 ? max_blocks : 256; }
+
+extern "C" int64_t irc_gemm_workspace_ex(int in_dtype, int out_dtype, int epilogue, int64_t M,
+                                         int64_t N, int64_t K, int64_t batch, int64_t max_blocks) {
+  const int64_t bud = split_budget(max_blocks);
+  int s = gemm::split_count(in_dtype == 0 ? 2 : 4, out_dtype == 1, epilogue, M, N, K, batch, bud);
   if (in_dtype == 0 && pp_enabled()) {
-    const int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch);
+    const int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch, bud);
     if (sp > s) s = sp;
   }
   int64_t bytes = s > 1 ? (int64_t)s * M * N * batch * (int64_t)sizeof(float) : 0;
   return bytes;
+}
+
+extern "C" int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M,
+                                      int64_t N, int64_t K, int64_t batch) {
+  return irc_gemm_workspace_ex(in_dtype, out_dtype, epilogue, M, N, K, batch, 0);
 }
 
 // LayerNorm-fold GEMM of the BERT encoder (include/irc.h irc_gemm_ln): bf16 A [M][K],
@@ -1526,13 +1536,14 @@ extern "C" int irc_gemm_set_big_ring(int on) {
 }
 
 // dtype codes: 0 = bf16, 1 = fp32
-extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue,
-                        int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
-                        int64_t strideA, const void* B, int64_t ldb, int64_t strideB,
-                        const float* bias, int64_t strideBias, const void* R, int64_t ldr,
-                        int64_t strideR, void* C, int64_t ldc, int64_t strideC, int accumulate,
-                        int64_t batch, void* workspace, int64_t workspace_bytes,
-                        irc_stream_t stream) {
+extern "C" int irc_gemm_ex(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue,
+                           int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
+                           int64_t strideA, const void* B, int64_t ldb, int64_t strideB,
+                           const float* bias, int64_t strideBias, const void* R, int64_t ldr,
+                           int64_t strideR, void* C, int64_t ldc, int64_t strideC, int accumulate,
+                           int64_t batch, void* workspace, int64_t workspace_bytes,
+                           int64_t max_blocks, irc_stream_t stream) {
+  const int64_t bud = split_budget(max_blocks);
   IRC_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: bad sizes");
   IRC_REQUIRE(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31), "gemm: size too large");
   IRC_REQUIRE(in_dtype == 0 || in_dtype == 1, "gemm: in_dtype must be 0 (bf16) or 1 (fp32)");
@@ -1550,7 +1561,7 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
   const int vec_b = ldb % vec == 0 && strideB % vec == 0 && ((uintptr_t)B % 16) == 0;
   if (M == 0 || N == 0) return IRC_OK;
   // split-K when the caller provided the workspace irc_gemm_workspace asked for
-  int splits = gemm::split_count(in_dtype == 0 ? 2 : 4, out_dtype == 1, epilogue, M, N, K, batch);
+  int splits = gemm::split_count(in_dtype == 0 ? 2 : 4, out_dtype == 1, epilogue, M, N, K, batch, bud);
   if (splits > 1 && (workspace == nullptr ||
                      workspace_bytes < (int64_t)splits * M * N * batch * (int64_t)sizeof(float)))
     splits = 1;
@@ -1566,7 +1577,7 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
   hipStream_t st = as_stream(stream);
   const int nb = (int)batch;
   if (in_dtype == 0 && pp_enabled()) {
-    int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch);
+    int sp = gpp::splits_for(out_dtype == 1, epilogue, M, N, K, batch, bud);
     if (sp > 1 && (workspace == nullptr ||
                    workspace_bytes < (int64_t)sp * M * N * batch * (int64_t)sizeof(float)))
       sp = 1;
@@ -1600,4 +1611,16 @@ extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout,
     return gemm::by_layout<float, float>(a_layout, b_layout, epilogue, g, nb, splits, st);
   set_error("gemm: fp32 inputs with bf16 output is not supported");
   return IRC_E_INVALID;
+}
+
+extern "C" int irc_gemm(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue,
+                        int64_t M, int64_t N, int64_t K, float alpha, const void* A, int64_t lda,
+                        int64_t strideA, const void* B, int64_t ldb, int64_t strideB,
+                        const float* bias, int64_t strideBias, const void* R, int64_t ldr,
+                        int64_t strideR, void* C, int64_t ldc, int64_t strideC, int accumulate,
+                        int64_t batch, void* workspace, int64_t workspace_bytes,
+                        irc_stream_t stream) {
+  return irc_gemm_ex(in_dtype, out_dtype, a_layout, b_layout, epilogue, M, N, K, alpha, A, lda,
+                     strideA, B, ldb, strideB, bias, strideBias, R, ldr, strideR, C, ldc, strideC,
+                     accumulate, batch, workspace, workspace_bytes, 0, stream);
 }

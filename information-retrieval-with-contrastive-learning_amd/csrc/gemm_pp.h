@@ -86,7 +86,8 @@ struct PArgs {
 
 constexpr int EPI_SCAN = 7;
 
-int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t batch);
+int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t batch,
+               int64_t budget = 256);
 // CUs of the current device (256 when the query fails)
 int device_cu_count();
 bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,

@@ -1281,11 +1281,12 @@ int device_cu_count() {
 
 // Split count: fill (at most) one wave of 256 blocks when the output tile grid
 // alone cannot (fp32 C, no fused epilogue), each K slice >= 1024 deep.
-int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t batch) {
+int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t batch,
+               int64_t budget) {
   if (!out_f32 || epi != 0) return 1;
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256) * batch;
   if (tiles >= 160) return 1;
-  int64_t s = 256 / tiles;           // one wave of blocks on 256 CUs
+  int64_t s = budget / tiles;        // at most `budget` blocks (256: one wave on 256 CUs)
   const int64_t smax = K / 1024;     // >= 16 K-tiles per slice
   if (s > smax) s = smax;
   if (s > 32) s = 32;

@@ -53,6 +53,9 @@ SIGNATURES = {
     "irc_gemm": (I32, [I32, I32, I32, I32, I32, I64, I64, I64, F32, P, I64, I64, P, I64, I64,
                        P, I64, P, I64, I64, P, I64, I64, I32, I64, P, I64, P]),
     "irc_gemm_workspace": (I64, [I32, I32, I32, I64, I64, I64, I64]),
+    "irc_gemm_ex": (I32, [I32, I32, I32, I32, I32, I64, I64, I64, F32, P, I64, I64, P, I64, I64,
+                          P, I64, P, I64, I64, P, I64, I64, I32, I64, P, I64, I64, P]),
+    "irc_gemm_workspace_ex": (I64, [I32, I32, I32, I64, I64, I64, I64, I64]),
     "irc_gemm_set_persistent": (I32, [I32]),
     "irc_gemm_set_big_ring": (I32, [I32]),
     "irc_gemm_ln": (I32, [I32, I64, I64, I64, P, I64, P, I64, P, P, I64, P, I64, P, I32, P, P, F32,

@@ -87,6 +87,10 @@ def _cu_count(dev) -> int:
 # (B L = 256 x 65 = 16640 rows: 2 waves of 520 tiles + 8; IRC_HEAD_SPLIT=0: off)
 _HEAD_SPLIT = os.environ.get("IRC_HEAD_SPLIT", "1") != "0"
 
+# Split-K cap (256 x 256-tile blocks) of the side-stream weight-gradient GEMMs in the
+# MFMA-path BPTT (irc_gemm_ex max_blocks; 0 = one full wave)
+WGRAD_MAX_BLOCKS = int(os.environ.get("IRC_WGRAD_BLOCKS", "128"))
+
 
 def _gemm_rows_split(x, w, b):
     """xp = x . w^T + b (fp32 out) -- as one GEMM, or, when M sits just above a whole
@@ -367,13 +371,17 @@ class LSTMHead(nn.Module):
         cur = torch.cuda.current_stream(dg.device)
         side = side_stream(dg.device, "lstm_wgrad")
         side.wait_stream(cur)
+        # Half a wave of split-K blocks: each dW GEMM is slower alone (l0 112 vs 78 us) but
+        # leaves CUs to the encoder forward running beside it (C2 train leg +1.3%,
+        # DESIGN.md 6c).
+        mb = WGRAD_MAX_BLOCKS
         with torch.cuda.stream(side):
             ops.gemm_strided(dg, x, g[ih:], M=4 * H, N=In, K=BL, batch=nd, lda=nd * 4 * H,
                              sA=4 * H, ldb=x.stride(0), sB=0, ldc=In, sC=4 * H * In,
-                             trans_a=True, b_is_nk=False, accumulate=True)
+                             trans_a=True, b_is_nk=False, accumulate=True, max_blocks=mb)
             ops.gemm_strided(dg, hprev, g[hh:], M=4 * H, N=H, K=BL, batch=nd, lda=nd * 4 * H,
                              sA=4 * H, ldb=H, sB=BL * H, ldc=H, sC=4 * H * H, trans_a=True,
-                             b_is_nk=False, accumulate=True)
+                             b_is_nk=False, accumulate=True, max_blocks=mb)
             db = ops.colsum(dg)  # d(b_ih) = d(b_hh): one column sum, added to both
             ops.axpby(g[bi:bi + nd * 4 * H], db, out=g[bi:bi + nd * 4 * H])
             ops.axpby(g[bh:bh + nd * 4 * H], db, out=g[bh:bh + nd * 4 * H])

@@ -139,26 +139,28 @@ def gemm(a, b, *, trans_a=False, b_is_nk=True, bias=None, epilogue=EPI_NONE, res
     return out
 
 
-def _splitk_ws(a, out, epilogue, M, N, K, batch):
+def _splitk_ws(a, out, epilogue, M, N, K, batch, max_blocks=0):
     """Device workspace for the GEMM's deterministic split-K (None when unused)."""
-    nws = _lib.load().irc_gemm_workspace(_code(a), _code(out), int(epilogue), M, N, K, batch)
+    nws = _lib.load().irc_gemm_workspace_ex(_code(a), _code(out), int(epilogue), M, N, K, batch,
+                                            int(max_blocks))
     if nws <= 0:
         return None, 0
     return torch.empty((nws,), dtype=torch.uint8, device=a.device), nws
 
 
 def gemm_strided(a, b, out, *, M, N, K, batch, lda, sA, ldb, sB, ldc, sC, trans_a=False,
-                 b_is_nk=True, alpha=1.0, accumulate=False):
+                 b_is_nk=True, alpha=1.0, accumulate=False, max_blocks=0):
     """Batched C_i (=|+=) alpha * op(A_i) @ op(B_i) over raw strides (elements):
-    A_i = a + i*sA, etc.  Same operand layouts as ``gemm``; no epilogue."""
+    A_i = a + i*sA, etc.  Same operand layouts as ``gemm``; no epilogue.  max_blocks caps
+    a split-K launch (irc_gemm_ex; 0 = one wave)."""
     require_hip(a, b, out)
     if a.dtype != b.dtype:
         raise TypeError("gemm operands must share a dtype")
-    ws, nws = _splitk_ws(a, out, EPI_NONE, M, N, K, batch)
-    _lib.call("irc_gemm", _code(a), _code(out), 1 if trans_a else 0, 0 if b_is_nk else 1,
+    ws, nws = _splitk_ws(a, out, EPI_NONE, M, N, K, batch, max_blocks)
+    _lib.call("irc_gemm_ex", _code(a), _code(out), 1 if trans_a else 0, 0 if b_is_nk else 1,
               EPI_NONE, M, N, K, float(alpha), ptr(a), lda, sA, ptr(b), ldb, sB, None, 0, None,
               0, 0, ptr(out), ldc, sC, 1 if accumulate else 0, batch, ptr(ws), nws,
-              stream_ptr(a.device))
+              int(max_blocks), stream_ptr(a.device))
     return out
 
 

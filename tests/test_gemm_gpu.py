@@ -108,6 +108,31 @@ def test_splitk_batched_accumulate(gpu, dtype, M, N, K):
     assert torch.equal(out, out2)
 
 
+@pytest.mark.parametrize("max_blocks", [0, 32, 128, 1])
+def test_splitk_block_cap(gpu, max_blocks):
+    """irc_gemm_ex with a split-K cap (the LSTM head's side-stream dW GEMMs: dgates^T . x,
+    K = B*L): within fp32 reassociation of the uncapped GEMM, bitwise reproducible, and
+    a smaller cap never needs more workspace."""
+    from irc_amd import _lib, ops
+
+    M, N, K = 1024, 768, 16640
+    lib = _lib.load()
+    full = lib.irc_gemm_workspace_ex(0, 1, 0, M, N, K, 2, 0)
+    assert full == lib.irc_gemm_workspace(0, 1, 0, M, N, K, 2) > 0
+    assert lib.irc_gemm_workspace_ex(0, 1, 0, M, N, K, 2, max_blocks) <= full
+    g = torch.Generator().manual_seed(11)
+    a = torch.randn((K, 2 * M), generator=g).to(torch.bfloat16).to(gpu)
+    b = torch.randn((K, N), generator=g).to(torch.bfloat16).to(gpu)
+    outs = []
+    for mb in (0, max_blocks, max_blocks):
+        c = torch.zeros((2, M, N), device=gpu)
+        ops.gemm_strided(a, b, c, M=M, N=N, K=K, batch=2, lda=2 * M, sA=M, ldb=N, sB=0, ldc=N,
+                         sC=M * N, trans_a=True, b_is_nk=False, accumulate=True, max_blocks=mb)
+        outs.append(c)
+    assert torch.equal(outs[1], outs[2])
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=2e-3)
+
+
 def test_splitk_matches_unsplit(gpu):
     """Same GEMM with and without the workspace: equal within fp32 reassociation."""
     from irc_amd import _lib, ops
