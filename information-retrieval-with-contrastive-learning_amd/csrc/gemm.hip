@@ -1397,7 +1397,12 @@ static bool pp_enabled() {
   return on;
 }
 
-static inline int64_t split_budget(int64_t max_blocks) { return max_blocks > 0 ? max_blocks : 256; }
+#ifndef IRC_SPLIT_BLOCKS_DEFAULT  // diagnostic builds: another default split-K cap
+#define IRC_SPLIT_BLOCKS_DEFAULT 256
+#endif
+static inline int64_t split_budget(int64_t max_blocks) {
+  return max_blocks > 0 ? max_blocks : IRC_SPLIT_BLOCKS_DEFAULT;
+}
 
 extern "C" int64_t irc_gemm_workspace_ex(int in_dtype, int out_dtype, int epilogue, int64_t M,
                                          int64_t N, int64_t K, int64_t batch, int64_t max_blocks) {
