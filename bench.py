@@ -56,7 +56,8 @@ C4_Q, C4_D, C5_Q = 2048, 1024, 2048
 # than the 256 MiB Infinity Cache, so its Q sweep is HBM-honest), 1024 queries
 C3_N_PER_GPU, C3_Q = 250_000, 1024
 PP_MIN_Q = 192  # irc_scan_topk's filter runs on the ping-pong GEMM kernel from this Q
-SCAN_DEPTH = 2  # query batches in flight in the retrieval legs (search_many)
+SCAN_DEPTH = 3  # query batches in flight in the retrieval legs (search_many; 2 -> 3: C2 +13%,
+# profiles/r05_zd_scan_depth.txt)
 
 
 def _cpu_model():

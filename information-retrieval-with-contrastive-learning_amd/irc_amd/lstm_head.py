@@ -87,9 +87,11 @@ def _cu_count(dev) -> int:
 # (B L = 256 x 65 = 16640 rows: 2 waves of 520 tiles + 8; IRC_HEAD_SPLIT=0: off)
 _HEAD_SPLIT = os.environ.get("IRC_HEAD_SPLIT", "1") != "0"
 
-# Split-K cap (256 x 256-tile blocks) of the side-stream weight-gradient GEMMs in the
-# MFMA-path BPTT (irc_gemm_ex max_blocks; 0 = one full wave)
-WGRAD_MAX_BLOCKS = int(os.environ.get("IRC_WGRAD_BLOCKS", "128"))
+# Split-K cap (256 x 256-tile blocks) of the MFMA-path BPTT's GEMMs: the weight gradients on
+# their side stream and dX (irc_gemm_ex max_blocks; 0 = one full wave).  They run beside the
+# encoder forward, whose GEMMs set the step: half a wave of blocks is slower alone but leaves
+# it CUs (profiles/r05_zc_split_cap_ab.txt; a cap of 64 measured slower)
+SPLIT_MAX_BLOCKS = int(os.environ.get("IRC_HEAD_SPLIT_BLOCKS", "128"))
 
 
 def _gemm_rows_split(x, w, b):
@@ -367,14 +369,13 @@ class LSTMHead(nn.Module):
         # dx is the critical path (next layer's recurrence); the weight/bias
         # gradients go to a side stream and overlap that recurrence, which only
         # occupies B/32 * ndir CUs.  Joined in backward_compute.
-        dx = ops.gemm(dg, wih_c, out_dtype=torch.float32) if l > 0 else None
+        mb = SPLIT_MAX_BLOCKS
+        dx = ops.gemm(dg, wih_c, out_dtype=torch.float32, max_blocks=mb) if l > 0 else None
         cur = torch.cuda.current_stream(dg.device)
         side = side_stream(dg.device, "lstm_wgrad")
         side.wait_stream(cur)
-        # Half a wave of split-K blocks: each dW GEMM is slower alone (l0 112 vs 78 us) but
-        # leaves CUs to the encoder forward running beside it (C2 train leg +1.3%,
-        # DESIGN.md 6c).
-        mb = WGRAD_MAX_BLOCKS
+        # Half a wave of split-K blocks (SPLIT_MAX_BLOCKS): each dW GEMM is slower alone
+        # (l0 112 vs 78 us) but leaves CUs to the encoder forward beside it.
         with torch.cuda.stream(side):
             ops.gemm_strided(dg, x, g[ih:], M=4 * H, N=In, K=BL, batch=nd, lda=nd * 4 * H,
                              sA=4 * H, ldb=x.stride(0), sB=0, ldc=In, sC=4 * H * In,

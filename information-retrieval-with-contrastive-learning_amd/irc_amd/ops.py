@@ -105,12 +105,13 @@ def gemm_set_persistent(mode) -> int:
 
 
 def gemm(a, b, *, trans_a=False, b_is_nk=True, bias=None, epilogue=EPI_NONE, residual=None,
-         alpha=1.0, out=None, out_dtype=None, accumulate=False):
+         alpha=1.0, out=None, out_dtype=None, accumulate=False, max_blocks=0):
     """out[M, N] = alpha * op(a) @ op(b) (+ bias) (-> gelu) (+ residual).
 
     a: [M, K] (or [K, M] with trans_a); b: [N, K] when b_is_nk (nn.Linear weight
     layout, i.e. a @ b.T) else [K, N].  Inputs bf16 or fp32 (same dtype);
-    fp32 inputs run the exact fp32 MFMA.  2-D only (see gemm_strided).
+    fp32 inputs run the exact fp32 MFMA.  2-D only (see gemm_strided).  max_blocks
+    caps a split-K launch (irc_gemm_ex; 0 = one wave).
     """
     require_hip(a, b, bias, residual, out)
     if a.dtype != b.dtype:
@@ -130,12 +131,12 @@ def gemm(a, b, *, trans_a=False, b_is_nk=True, bias=None, epilogue=EPI_NONE, res
         raise TypeError("bias must be fp32")
     if residual is not None and residual.dtype != out.dtype:
         raise TypeError("residual dtype must match the output")
-    ws, nws = _splitk_ws(a, out, epilogue, M, N, K, 1)
-    _lib.call("irc_gemm", _code(a), _code(out), 1 if trans_a else 0, 0 if b_is_nk else 1,
+    ws, nws = _splitk_ws(a, out, epilogue, M, N, K, 1, max_blocks)
+    _lib.call("irc_gemm_ex", _code(a), _code(out), 1 if trans_a else 0, 0 if b_is_nk else 1,
               int(epilogue), M, N, K, float(alpha), ptr(a), a.stride(0), 0, ptr(b), b.stride(0),
               0, ptr(bias), 0, ptr(residual), residual.stride(0) if residual is not None else 0, 0,
               ptr(out), out.stride(0), 0, 1 if accumulate else 0, 1, ptr(ws), nws,
-              stream_ptr(a.device))
+              int(max_blocks), stream_ptr(a.device))
     return out
 
 

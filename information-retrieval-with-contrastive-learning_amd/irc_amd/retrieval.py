@@ -272,16 +272,18 @@ class ShardedDenseIndex:
         dist.all_gather(ii, i.contiguous(), group=self.group)
         return self._merge(torch.stack(ss), torch.stack(ii), k)
 
-    def search_many(self, batches, k: int, depth: int = 2, equal_counts: bool = False,
-                    graphs: bool | None = None):
+    def search_many(self, batches, k: int, depth: int = 3, equal_counts: bool = False,
+                    graphs: bool = False):
         """search() over a sequence of query batches with up to ``depth`` batches
         in flight on as many HIP streams (each with its own scan workspace): one
         batch's latency-bound selects overlap the next batch's HBM-bound filter.
-        ``graphs`` (default: single process and every batch of one shape): each
-        stream replays a HIP graph of the whole local search captured once, so the
-        host issues a copy, a replay and two result copies per batch instead of
-        the call's individual launches.  Results are identical to calling
-        search() per batch; returned in order, usable on the current stream."""
+        ``graphs`` (single process, every batch of one shape): each stream replays a
+        HIP graph of the whole local search captured once, so the host issues a copy,
+        a replay and two result copies per batch instead of the call's individual
+        launches -- measured slower than direct launches at C2 (Q = 256: 86.4 vs 81.1
+        us a batch at depth 2, 76.0 vs 71.9 at depth 3; depth 4 slower again,
+        profiles/r05_zd_scan_depth.txt).  Results are identical to calling search()
+        per batch; returned in order, usable on the current stream."""
         import torch.distributed as dist
 
         batches = list(batches)
@@ -290,8 +292,6 @@ class ShardedDenseIndex:
         streams = _search_streams(dev, depth)
         single = self.group is None or not dist.is_initialized() or \
             dist.get_world_size(self.group) == 1
-        if graphs is None:
-            graphs = single and len({tuple(b.shape) for b in batches}) <= 1
         if graphs and not single:
             raise ValueError("graphed search_many needs a single-process index")
         slots = self._graph_slots(batches[0], k, depth, streams) if (graphs and batches) else None

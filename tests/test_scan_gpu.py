@@ -281,18 +281,19 @@ def test_clustered_corpus_rescan_properties(gpu, Q, D, fp8):
 
 
 def test_search_many_equals_serial_search(gpu):
-    """Pipelined batches (search_many, 2 streams, own workspaces) return exactly
+    """Pipelined batches (search_many, 2 / 3 streams, own workspaces) return exactly
     what serial search() calls return."""
     from irc_amd import retrieval
 
     rng = np.random.default_rng(8)
     d = _dev(_grid(rng, (30000, 256), 3), gpu)
     index = retrieval.ShardedDenseIndex(d)
-    batches = [_dev(_grid(rng, (q, 256), 3), gpu) for q in (256, 1, 300, 64, 256)]
-    many = index.search_many(batches, 50, depth=2)
-    for q, (s, i) in zip(batches, many):
-        s0, i0 = index.search(q, 50)
-        assert torch.equal(s, s0) and torch.equal(i, i0)
+    batches = [_dev(_grid(rng, (q, 256), 3), gpu) for q in (256, 1, 300, 64, 256, 256, 17)]
+    for depth in (2, 3):
+        many = index.search_many(batches, 50, depth=depth)
+        for q, (s, i) in zip(batches, many):
+            s0, i0 = index.search(q, 50)
+            assert torch.equal(s, s0) and torch.equal(i, i0)
 
 
 def test_graphed_search_many_equals_serial_search(gpu):
