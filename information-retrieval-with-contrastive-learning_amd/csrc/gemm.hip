@@ -1594,7 +1594,7 @@ extern "C" int irc_gemm_ex(int in_dtype, int out_dtype, int a_layout, int b_layo
                     accumulate, vec_c};
       pa.group_m = gemm_group_m();
       prof_begin(st);
-      gpp::run(out_dtype == 1, a_layout, b_layout, epilogue, pa, batch, sp, st);
+      gpp::run(out_dtype == 1, a_layout, b_layout, epilogue, pa, batch, sp, st, max_blocks);
       if (sp > 1) {
         const int64_t n = M * N * batch;
         hipLaunchKernelGGL(gemm::splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256),

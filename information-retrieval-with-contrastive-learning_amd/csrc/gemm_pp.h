@@ -92,8 +92,10 @@ int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t ba
 int device_cu_count();
 bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                int64_t sA, const void* B, int64_t ldb, int64_t sB, int64_t batch, int splits);
+// max_grid > 0: at most that many workgroups -- a launch of more tiles runs as a static
+// persistent tile loop over a grid of max_grid (same per-tile arithmetic: bit-identical)
 void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, int splits,
-         hipStream_t st);
+         hipStream_t st, int64_t max_grid = 0);
 // scan filter: A = queries [M=Q][K=D], B = docs [N][D] (row stride ldb), EPI_SCAN;
 // fp8: e4m3 operands, K / lda / ldb in 2-byte units (D/2)
 void run_scan(const PArgs& a, hipStream_t st, bool fp8 = false);

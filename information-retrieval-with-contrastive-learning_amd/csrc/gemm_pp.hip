@@ -1345,22 +1345,33 @@ static void launch_pers(int epi, const PArgs& a, unsigned grid, uint32_t* ctr, h
 }
 
 void run(int out_f32, int la, int lb, int epi, const PArgs& a, int64_t batch, int splits,
-         hipStream_t st) {
+         hipStream_t st, int64_t max_grid) {
   const int64_t tiles = ((int64_t)(a.M + 255) / 256) * ((a.N + 255) / 256);
-  // persistent form: one launch-wide pass over more tiles than CUs, A K-major
-  if (splits == 1 && batch == 1 && a.vec_c && la == 0 && pers_enabled()) {
-    const int ncu = cu_count();
-    uint32_t* ctr = (ncu > 0 && tiles > ncu) ? pers_counter(st) : nullptr;
-    if (ctr != nullptr) {
-      if (out_f32) {
-        if (lb == 0) launch_pers<true, true, float>(epi, a, (unsigned)ncu, ctr, st);
-        else launch_pers<true, false, float>(epi, a, (unsigned)ncu, ctr, st);
-      } else {
-        if (lb == 0) launch_pers<true, true, unsigned short>(epi, a, (unsigned)ncu, ctr, st);
-        else launch_pers<true, false, unsigned short>(epi, a, (unsigned)ncu, ctr, st);
-      }
-      return;
+  // persistent form: one launch-wide pass over more tiles than CUs (or than the caller's
+  // grid cap), A K-major
+  const bool pers_ok = splits == 1 && batch == 1 && a.vec_c && la == 0;
+  const int ncu = pers_ok ? cu_count() : 0;
+  int64_t pgrid = 0;
+  uint32_t* ctr = nullptr;
+  if (pers_ok && max_grid > 0 && tiles > max_grid && (ncu <= 0 || max_grid < ncu)) {
+    // the caller's cap: static waves of max_grid tiles (the dynamic mode takes its
+    // counter slot as usual; without one, the static form needs none)
+    pgrid = max_grid;
+    if (pers_mode().load(std::memory_order_relaxed) == 1) ctr = pers_counter(st);
+    if (pers_mode().load(std::memory_order_relaxed) == 1 && ctr == nullptr) pgrid = 0;
+  } else if (pers_ok && pers_enabled() && ncu > 0 && tiles > ncu) {
+    ctr = pers_counter(st);
+    pgrid = ctr != nullptr ? ncu : 0;
+  }
+  if (pgrid > 0) {
+    if (out_f32) {
+      if (lb == 0) launch_pers<true, true, float>(epi, a, (unsigned)pgrid, ctr, st);
+      else launch_pers<true, false, float>(epi, a, (unsigned)pgrid, ctr, st);
+    } else {
+      if (lb == 0) launch_pers<true, true, unsigned short>(epi, a, (unsigned)pgrid, ctr, st);
+      else launch_pers<true, false, unsigned short>(epi, a, (unsigned)pgrid, ctr, st);
     }
+    return;
   }
   const dim3 grid((unsigned)tiles, (unsigned)batch, (unsigned)splits);
   if (splits > 1)  // raw fp32 slabs, no epilogue (reduced afterwards)

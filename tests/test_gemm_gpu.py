@@ -133,6 +133,26 @@ def test_splitk_block_cap(gpu, max_blocks):
     torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=2e-3)
 
 
+@pytest.mark.parametrize("max_blocks", [128, 100, 7])
+@pytest.mark.parametrize("M,N,K,epi,od", [(16640, 2048, 768, 1, torch.float32),
+                                          (4000, 1536, 512, 2, torch.bfloat16),
+                                          (3000, 1000, 256, 0, torch.float32)])
+def test_grid_cap_bit_identical(gpu, max_blocks, M, N, K, epi, od):
+    """irc_gemm_ex max_blocks on a launch of more 256 x 256 tiles than the cap (the LSTM
+    head's input projection): a static persistent tile loop over max_blocks workgroups,
+    bit-identical to one workgroup per tile."""
+    from irc_amd import ops
+
+    g = torch.Generator().manual_seed(M + N)
+    a = torch.randn((M, K), generator=g).to(torch.bfloat16).to(gpu)
+    w = torch.randn((N, K), generator=g).to(torch.bfloat16).to(gpu)
+    bias = torch.randn(N, generator=g).to(gpu)
+    kw = dict(bias=bias if epi else None, epilogue=epi, out_dtype=od)
+    ref = ops.gemm(a, w, **kw)
+    capped = ops.gemm(a, w, max_blocks=max_blocks, **kw)
+    assert torch.equal(ref, capped)
+
+
 def test_splitk_matches_unsplit(gpu):
     """Same GEMM with and without the workspace: equal within fp32 reassociation."""
     from irc_amd import _lib, ops
