@@ -134,7 +134,10 @@ int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M,
  * 256 x 256-tile blocks (0 = the default, 256 = one wave on the chip).  A smaller cap
  * gives fewer, longer splits: slower alone, but a GEMM that runs beside other work
  * (the LSTM weight gradients on their side stream) takes fewer CUs from it.  Pass the
- * same max_blocks to both calls; results stay deterministic for a given cap. */
+ * same max_blocks to both calls; results stay deterministic for a given cap.  An
+ * unsplit 256 x 256-tile launch of more tiles than max_blocks (batch 1, A [M][K]) runs
+ * as a static persistent tile loop over max_blocks workgroups: bit-identical to the
+ * uncapped launch. */
 int irc_gemm_ex(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue, int64_t M,
                 int64_t N, int64_t K, float alpha, const void* A, int64_t lda, int64_t strideA,
                 const void* B, int64_t ldb, int64_t strideB, const float* bias, int64_t strideBias,
