@@ -4,7 +4,7 @@
 # the bench's GEMM family (FETCH_SIZE / WRITE_SIZE passes).
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/${R5FIN:-r5fin2}
+O=$R/gpurun_out/${R5FIN:-r5fin3}
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/ \
