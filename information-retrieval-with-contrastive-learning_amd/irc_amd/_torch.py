@@ -34,7 +34,7 @@ _side: dict = {}
 # Streams created with the high priority: none by default.  The frozen encoder's feature
 # prefetch at high priority gained the C2 step 0.6-1.1% in round 4 (profiles/r04_q_priority_ab.txt)
 # and now costs it 0.5-1%; once such a stream exists in the process the pipelined retrieval
-# (search_many) runs slower too -- C2 3.58M -> 2.1M queries/s, serial calls unchanged
+# (search_many) runs slower too -- C2 3.58M -> 2.1M queries/s (round 4: serial calls unchanged)
 # (profiles/r05_zh_priority_ab.txt, r04_t_priority_retrieval.txt); the heads' streams at high
 # priority measured 3% slower.  IRC_HIGH_PRIORITY_STREAMS: comma-separated tags (A/B runs).
 HIGH_PRIORITY_TAGS: tuple = tuple(
