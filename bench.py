@@ -55,6 +55,14 @@ C4_Q, C4_D, C5_Q = 2048, 1024, 2048
 # C3 retrieval leg: 1M docs over 4 GPUs = 250k x 768 bf16 per GPU (384 MB: larger
 # than the 256 MiB Infinity Cache, so its Q sweep is HBM-honest), 1024 queries
 C3_N_PER_GPU, C3_Q = 250_000, 1024
+# Strong scaling (the north star's ">= 6x at 8 GPUs on a 5M-doc sharded
+# corpus"): a FIXED corpus split N_total / world per rank, the same global query batch at
+# every world size.  (name, docs in total, dtype, global queries, dim)
+STRONG_LEGS = (("retrieval_strong_c3", 1_000_000, "bf16", C3_Q, SCAN_D),
+               ("retrieval_strong_c4", 5_000_000, "bf16", C4_Q, C4_D),
+               ("retrieval_strong_c5", 5_000_000, "fp8", C5_Q, SCAN_D))
+STRONG_CHUNKS = 8  # the corpus is drawn in n_total / 8 chunks, each from its own seed, so
+# the docs (and the top-k) are the same at 1, 2, 4 and 8 ranks
 PP_MIN_Q = 192  # irc_scan_topk's filter runs on the ping-pong GEMM kernel from this Q
 SCAN_DEPTH = 3  # query batches in flight in the retrieval legs (search_many; 2 -> 3: C2 +13%,
 # profiles/r05_zd_scan_depth.txt)
@@ -518,6 +526,102 @@ def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16", nq=
     }
 
 
+def strong_shard(n_total, dim, rank, world, dev):
+    """This rank's rows [lo, hi) of the fixed corpus (unit-norm Gaussian, bf16): drawn
+    chunk by chunk (STRONG_CHUNKS seeds), so every world size sees the same documents."""
+    from irc_amd.retrieval import shard_bounds
+
+    lo, hi = shard_bounds(n_total, world, rank)
+    chunk = -(-n_total // STRONG_CHUNKS)
+    parts = []
+    for c in range(lo // chunk, (hi - 1) // chunk + 1):
+        c0, c1 = c * chunk, min(n_total, (c + 1) * chunk)
+        g = torch.Generator(device=dev).manual_seed(4049 + c)
+        x = torch.nn.functional.normalize(torch.randn(c1 - c0, dim, generator=g, device=dev))
+        parts.append(x[max(lo, c0) - c0:min(hi, c1) - c0].bfloat16())
+        del x
+    return (parts[0] if len(parts) == 1 else torch.cat(parts)), lo
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def run_scan_strong(args, rank, world, dev, n_total, dtype, nq, dim, k=SCAN_K, make_index=None,
+                    reps=None):
+    """Strong scaling of the sharded scan: the fixed corpus of n_total
+    docs split n_total / world per rank (ShardedDenseIndex), the same nq global queries
+    per batch (each rank contributes nq / world and receives the global top-k of all
+    nq).  Reports global queries/s (serial calls and `SCAN_DEPTH` batches in flight),
+    the ranks and backend the collectives ran on, and the three steps of one search
+    timed apart -- query all-gather, local scan, per-shard list all-gather + merge --
+    each max over ranks.  make_index(rank, world, dev) -> index lets the CPU tests
+    drive the same orchestration with a host-side double of the local scan."""
+    if make_index is None:
+        from irc_amd import retrieval
+
+        def make_index(rank, world, dev):
+            shard, lo = strong_shard(n_total, dim, rank, world, dev)
+            group = dist.group.WORLD if world > 1 else None
+            return retrieval.ShardedDenseIndex(shard, doc_offset=lo, group=group, dtype=dtype)
+    index = make_index(rank, world, dev)
+    gq = torch.Generator().manual_seed(7)
+    allq = torch.nn.functional.normalize(torch.randn(nq, dim, generator=gq)).bfloat16()
+    myq = allq[rank * nq // world:(rank + 1) * nq // world].to(dev)
+    equal = nq % world == 0
+    reps = reps or max(args.steps, 10)
+
+    def timed(fn, n):
+        if world > 1:
+            dist.barrier()
+        _sync(dev)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        _sync(dev)
+        return _max_over_ranks(time.perf_counter() - t0, dev, world) / n
+
+    search = lambda: index.search(myq, k, equal_counts=equal)  # noqa: E731
+    for _ in range(max(args.warmup, 2)):
+        res = search()
+    _sync(dev)
+    t_call = timed(search, reps)
+    if dev.type == "cuda":
+        index.search_many([myq] * 4, k, depth=SCAN_DEPTH, equal_counts=equal)
+        t_pipe = timed(lambda: index.search_many([myq] * reps, k, depth=SCAN_DEPTH,
+                                                 equal_counts=equal), 1) / reps
+    else:
+        t_pipe = t_call
+    sharded = index._sharded()
+    gathered = index._gather_queries(myq, equal) if sharded else myq
+    s, i = index._local_topk(gathered, k)
+    phases = {"query_allgather_us": timed(lambda: index._gather_queries(myq, equal), reps) * 1e6
+              if sharded else 0.0,
+              "local_scan_us": timed(lambda: index._local_topk(gathered, k), reps) * 1e6,
+              "list_allgather_merge_us": timed(lambda: index._exchange_merge(s, i, k), reps) * 1e6
+              if sharded else 0.0}
+    local = index.docs.shape[0]
+    counts = torch.tensor([local], dtype=torch.int64, device=dev)
+    lo_hi = [counts.clone() for _ in range(world)]
+    if world > 1:
+        dist.all_gather(lo_hi, counts)
+    per_rank = [int(c.item()) for c in lo_hi]
+    return {
+        "value": nq / t_pipe, "unit": "queries/s", "scaling": "strong",
+        "serial_queries_per_s": nq / t_call, "serial_us_per_call": t_call * 1e6,
+        "pipelined_us_per_batch": t_pipe * 1e6, "batches_in_flight": SCAN_DEPTH,
+        "phases": phases,
+        "ranks": world, "backend": dist.get_backend() if world > 1 else None,
+        "docs_total": n_total, "docs_per_rank": per_rank, "queries": nq,
+        "queries_per_rank": nq // world, "dim": dim, "k": k, "dtype": dtype,
+        "query_doc_pairs_per_s": nq * n_total / t_pipe,
+        "result_shape": list(res[1].shape),
+        "workload": (f"fixed {n_total}-doc corpus (D={dim}, {dtype}) split {n_total} / {world} "
+                     f"per rank, {nq} global queries per batch, top-{k}; global queries/s"),
+    }
+
+
 def scan_q_sweep(index, dev, dim=SCAN_D, qs=(1, 16, 64, 256), reps=20):
     """Local scan filter at several query-batch sizes (SURVEY.md 8d grades the HBM
     fraction at Q in {1, 16, 64, 256}): kernel HIP-event time and algorithmic bytes
@@ -603,19 +707,29 @@ def run_sparse(args, dev, cpu_baseline):
     return out
 
 
-def cpu_baseline_scan(budget_s):
+def cpu_baseline_scan(budget_s, n=SCAN_N_PER_GPU, nq=SCAN_Q, dim=SCAN_D, max_q=SCAN_Q,
+                      leg="C2"):
+    """The reference's CPU arithmetic for one retrieval leg's shard (fp32 q @ d.T and an
+    exact top-k, src/evaluation.py:110-112 / tfidf_doc_ranker.py:60-75), on the host's
+    torch threads.  Bounded sample: at most max_q of the leg's nq queries per pass over
+    the whole shard, repeated for budget_s; queries/s is per query, so it compares with
+    the GPU leg's rate directly.  fp8 legs are timed on the same shapes in fp32 (the
+    reference has no fp8 path)."""
     from oracle import torch_cpu_step
 
     g = torch.Generator().manual_seed(2024)
-    d = torch.nn.functional.normalize(torch.randn(SCAN_N_PER_GPU, SCAN_D, generator=g))
+    d = torch.nn.functional.normalize(torch.randn(n, dim, generator=g))
     gq = torch.Generator().manual_seed(7)
-    q = torch.nn.functional.normalize(torch.randn(SCAN_Q, SCAN_D, generator=gq))
+    qn = min(nq, max_q)
+    q = torch.nn.functional.normalize(torch.randn(qn, dim, generator=gq))
     v, reps = torch_cpu_step.scan_baseline(q.bfloat16().float(), d.bfloat16().float(), SCAN_K,
                                            budget_s)
+    del d
     return {"value": v, "unit": "queries/s", "cores": torch.get_num_threads(), "kind": "port",
             "cpu_model": _cpu_model(),
-            "sample": f"{reps} x full C2 batch (Q={SCAN_Q}, N={SCAN_N_PER_GPU}, D={SCAN_D}, "
-                      f"k={SCAN_K}): torch CPU fp32 matmul over 64k-doc chunks + topk merge"}
+            "sample": f"{reps} x {qn} of the {leg} batch's {nq} queries over the full shard "
+                      f"(N={n}, D={dim}, k={SCAN_K}): torch CPU fp32 matmul over 64k-doc chunks "
+                      "+ topk merge"}
 
 
 def _r(x, n=4):
@@ -632,6 +746,13 @@ def _leg_summary(name, d):
                 "step_frac": _r(r.get("frac"), 3), "step_tflops": _r(d.get("step_tflops")),
                 "gemm_frac": _r(gm.get("frac"), 3), "gemm_ms_per_step": _r(gm.get("gemm_ms_per_step")),
                 "traffic_over_alg": _r(gm.get("traffic_over_alg"), 3)}
+    if name.startswith("retrieval_strong"):
+        ph = d.get("phases") or {}
+        return {"queries_per_s": _r(d.get("value"), 5), "scaling": "strong",
+                "docs_total": d.get("docs_total"), "docs_per_rank": d.get("docs_per_rank"),
+                "ranks": d.get("ranks"), "Q": d.get("queries"), "dtype": d.get("dtype"),
+                "call_us": _r(d.get("serial_us_per_call")),
+                "phases_us": {k.replace("_us", ""): _r(v) for k, v in ph.items()}}
     if name == "sparse_tfidf":
         c = d.get("cpu_baseline") or {}
         return {"queries_per_s": _r(d.get("value"), 5), "cpu_queries_per_s": _r(c.get("value"))}
@@ -649,8 +770,9 @@ def _leg_summary(name, d):
 
 
 # summary order: the training legs last (nearest the end of the output)
-LEGS = ("sparse_tfidf", "retrieval_fp8", "retrieval_c4", "retrieval_c3", "retrieval",
-        "train_bert", "train_c4", "train_fp8", "train")
+LEGS = ("sparse_tfidf", "retrieval_strong_c3", "retrieval_strong_c4", "retrieval_strong_c5",
+        "retrieval_fp8", "retrieval_c4", "retrieval_c3", "retrieval", "train_bert", "train_c4",
+        "train_fp8", "train")
 
 
 def _compact(line):
@@ -704,7 +826,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--part", default="all",
                     choices=["all", "train", "train_fp8", "train_c4", "scan", "scan_c2",
-                             "scan_c3", "bert"])
+                             "scan_c3", "bert", "strong"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -751,12 +873,25 @@ def main():
                            sweep=False)
         torch.cuda.empty_cache()
         scan_fp8 = run_scan(args, rank, world, dev, FP8_N_PER_GPU, "fp8", C5_Q, SCAN_D)
+    strong = {}
+    if args.part in ("all", "strong"):
+        for name, n_total, sdt, snq, sdim in STRONG_LEGS:
+            torch.cuda.empty_cache()
+            strong[name] = run_scan_strong(args, rank, world, dev, n_total, sdt, snq, sdim)
+        torch.cuda.empty_cache()
     cpu_t = cpu_s = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if train is not None:
             cpu_t = cpu_baseline_train(model, args.cpu_steps)
         if scan is not None:
             cpu_s = cpu_baseline_scan(args.cpu_budget)
+        # the other retrieval legs, each beside its own CPU figure (shorter budgets)
+        for leg, n, nq, dim, name in ((scan_c3, C3_N_PER_GPU, C3_Q, SCAN_D, "C3"),
+                                      (scan_c4, FP8_N_PER_GPU, C4_Q, C4_D, "C4"),
+                                      (scan_fp8, FP8_N_PER_GPU, C5_Q, SCAN_D, "C5")):
+            if leg is not None:
+                leg["cpu_baseline"] = cpu_baseline_scan(args.cpu_budget / 2, n, nq, dim,
+                                                        max_q=128, leg=name)
     if scan is not None:
         scan["cpu_baseline"] = cpu_s
     sparse_leg = None
@@ -779,6 +914,11 @@ def main():
         elif bert is not None:
             head = {"value": bert["pairs_per_s"], "unit": "pairs/s",
                     "ms_per_step": bert["ms_per_step"], "roofline": bert["roofline"],
+                    "cpu_baseline": None}
+        elif scan is None and scan_c3 is None:
+            leg = strong["retrieval_strong_c4"]
+            head = {"value": leg["value"], "unit": "queries/s",
+                    "ms_per_step": leg["pipelined_us_per_batch"] / 1e3, "roofline": None,
                     "cpu_baseline": None}
         elif scan is None:
             head = {"value": scan_c3["value"], "unit": "queries/s",
@@ -832,6 +972,7 @@ def main():
             line["retrieval_c4"] = scan_c4
         if sparse_leg is not None:
             line["sparse_tfidf"] = sparse_leg
+        line.update(strong)
         if scan_fp8 is not None:
             scan_fp8["workload"] = (f"C5 retrieval shard: {FP8_N_PER_GPU} e4m3 docs/GPU "
                                     f"(5M over 8 GPUs), {C5_Q} queries, top-{SCAN_K}")

@@ -47,7 +47,10 @@ int irc_abi_version(void);
  * row, must stay < 2^32).  Outputs out_score [Q, k] fp32 and out_idx [Q, k]
  * int64, sorted; slots beyond min(k, N) are (-inf, -1).  D % 64 == 0,
  * 1 <= k <= 1024.  Exact: the result is the top-k of the fp32 scores the MFMA
- * produced, never an approximation (sample threshold + exact radix select).
+ * produced, never an approximation (sample threshold + exact radix select).  A
+ * shard larger than one pass of the GEMM filter's plan (Q >= 192: over 1M docs, or
+ * a survivor workspace over IRC_SCAN_PP_MAX_GB) is scanned in equal doc chunks
+ * whose top-k lists are merged in the same launch sequence; same result.
  */
 int64_t irc_scan_topk_workspace(int64_t Q, int64_t N, int64_t D, int64_t k);
 int irc_scan_topk(const void* queries, const void* docs, int64_t Q, int64_t N, int64_t D,
@@ -134,10 +137,11 @@ int64_t irc_gemm_workspace(int in_dtype, int out_dtype, int epilogue, int64_t M,
  * 256 x 256-tile blocks (0 = the default, 256 = one wave on the chip).  A smaller cap
  * gives fewer, longer splits: slower alone, but a GEMM that runs beside other work
  * (the LSTM weight gradients on their side stream) takes fewer CUs from it.  Pass the
- * same max_blocks to both calls; results stay deterministic for a given cap.  An
- * unsplit 256 x 256-tile launch of more tiles than max_blocks (batch 1, A [M][K]) runs
- * as a static persistent tile loop over max_blocks workgroups: bit-identical to the
- * uncapped launch. */
+ * same max_blocks to both calls; results stay deterministic for a given cap.  The cap
+ * never limits an unsplit launch.  A negative max_blocks is a grid cap instead (no
+ * split-K cap): an unsplit 256 x 256-tile launch of more tiles than -max_blocks (batch 1,
+ * A [M][K]) runs as a static persistent tile loop over -max_blocks workgroups,
+ * bit-identical to the uncapped launch. */
 int irc_gemm_ex(int in_dtype, int out_dtype, int a_layout, int b_layout, int epilogue, int64_t M,
                 int64_t N, int64_t K, float alpha, const void* A, int64_t lda, int64_t strideA,
                 const void* B, int64_t ldb, int64_t strideB, const float* bias, int64_t strideBias,

@@ -251,14 +251,15 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const unsigned short
 // with R consecutive rows per half-wave: gamma / beta stay in registers across the rows
 // and the next row's loads are issued before this row's statistics.
 // y8 != null: also the MX-fp8 copy, as layernorm_vec_kernel writes it (config C5).
-// Called in place (y == x) by the encoder.  x / y stay __restrict__ on purpose (without
-// it the compiler serialises the next row's prefetch behind this row's stores: +0.25 ms
-// per C2 step): every element is read by the lane that writes it, before it writes it,
-// and a half-wave's rows are its own -- the prefetch past the last row re-reads the
-// half-wave's own row, whose value is then discarded, never another half-wave's.
+// Called in place (y == x) by the encoder, so x and y are NOT __restrict__ (aliasing them
+// legally): every element is read by the lane that writes it, before it writes it, and a
+// half-wave's rows are its own -- the prefetch past the last row re-reads the half-wave's
+// own row, whose value is then discarded, never another half-wave's.  The gfx950 code is
+// instruction-for-instruction the same as with __restrict__ (hipcc, ROCm 7.2: the next
+// row's loads are issued ahead of this row's stores in program order either way).
 template <int CPL, int R>
-__global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned short* __restrict__ x,
-                                                            unsigned short* __restrict__ y,
+__global__ __launch_bounds__(256) void layernorm_rows_kernel(const unsigned short* x,
+                                                            unsigned short* y,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta,
                                                             int64_t rows, float eps,

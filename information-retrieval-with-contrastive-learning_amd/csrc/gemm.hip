@@ -1400,9 +1400,12 @@ static bool pp_enabled() {
 #ifndef IRC_SPLIT_BLOCKS_DEFAULT  // diagnostic builds: another default split-K cap
 #define IRC_SPLIT_BLOCKS_DEFAULT 256
 #endif
+// max_blocks > 0: the split-K budget; < 0: a grid cap of -max_blocks workgroups on an
+// unsplit launch (the split-K budget stays the default); 0: neither.
 static inline int64_t split_budget(int64_t max_blocks) {
   return max_blocks > 0 ? max_blocks : IRC_SPLIT_BLOCKS_DEFAULT;
 }
+static inline int64_t grid_cap(int64_t max_blocks) { return max_blocks < 0 ? -max_blocks : 0; }
 
 extern "C" int64_t irc_gemm_workspace_ex(int in_dtype, int out_dtype, int epilogue, int64_t M,
                                          int64_t N, int64_t K, int64_t batch, int64_t max_blocks) {
@@ -1594,7 +1597,7 @@ extern "C" int irc_gemm_ex(int in_dtype, int out_dtype, int a_layout, int b_layo
                     accumulate, vec_c};
       pa.group_m = gemm_group_m();
       prof_begin(st);
-      gpp::run(out_dtype == 1, a_layout, b_layout, epilogue, pa, batch, sp, st, max_blocks);
+      gpp::run(out_dtype == 1, a_layout, b_layout, epilogue, pa, batch, sp, st, grid_cap(max_blocks));
       if (sp > 1) {
         const int64_t n = M * N * batch;
         hipLaunchKernelGGL(gemm::splitk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256),

@@ -2349,6 +2349,71 @@ static bool supported_d(int64_t D) {
 static void launch_select(const RegionSource& src, int Q, int k, int mode, uint64_t* thr,
                           float* out_score, int64_t* out_idx, float smul, hipStream_t st);
 
+// Shards too large for the GEMM filter's plan (its survivor workspace, 2 KB per (256-doc
+// tile, query), over pp_max_bytes, or more tiles than the select's region table) are
+// scanned as doc chunks that fit it, and the chunks' exact top-k lists merged by the same
+// (score desc, index asc) rule -- the result is identical to one pass.  Without this a
+// 5M-doc shard at Q = 2048 (config C4 on one GPU) would fall back to the stationary-query
+// kernel, which re-reads the corpus once per 128 queries.  Returns N (no chunking) or the
+// chunk size (a multiple of 256; the chunks are equal but for the last).
+static int64_t chunk_docs(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
+  if (Q < pp_min_q() || N < 256 || !(eb == 2 || D % 128 == 0)) return N;
+  const int64_t qpad = (Q + 255) / 256 * 256;
+  int64_t tiles = (int64_t)(pp_max_bytes() / ((size_t)qpad * 256 * 8));
+  if (tiles > SEL_MAXR) tiles = SEL_MAXR;
+  if (tiles < 1) return N;
+  const int64_t ntiles = (N + 255) / 256;
+  if (ntiles <= tiles) return N;
+  const int64_t nch = (ntiles + tiles - 1) / tiles;
+  return (ntiles + nch - 1) / nch * 256;  // balanced chunks of whole 256-doc tiles
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Workspace of a chunked scan: the per-chunk lists [nch][Q][k] (fp32 scores, int64 ids)
+// ahead of one chunk's own plan.
+static size_t workspace_bytes_for(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
+  const int64_t nc = chunk_docs(Q, N, D, k, eb);
+  if (nc >= N) return make_plan(Q, N, D, k, eb).bytes;
+  const int64_t nch = (N + nc - 1) / nc;
+  return align256((size_t)nch * Q * k * 12) + make_plan(Q, nc, D, k, eb).bytes;
+}
+
+static int scan_topk_impl(int eb, float smul, const void* queries, const void* docs, int64_t Q,
+                          int64_t N, int64_t D, int64_t k, int64_t doc_offset, void* workspace,
+                          int64_t workspace_bytes, float* out_score, int64_t* out_idx,
+                          hipStream_t st);
+
+static int scan_topk_chunked(int eb, float smul, const void* queries, const void* docs, int64_t Q,
+                             int64_t N, int64_t D, int64_t k, int64_t doc_offset, int64_t nc,
+                             void* workspace, int64_t workspace_bytes, float* out_score,
+                             int64_t* out_idx, hipStream_t st) {
+  const int64_t nch = (N + nc - 1) / nc;
+  const size_t lists = align256((size_t)nch * Q * k * 12);
+  IRC_REQUIRE(workspace != nullptr && workspace_bytes >= (int64_t)workspace_bytes_for(Q, N, D, k, eb),
+              "scan_topk: workspace %lld < required %lld bytes", (long long)workspace_bytes,
+              (long long)workspace_bytes_for(Q, N, D, k, eb));
+  char* ws = static_cast<char*>(workspace);
+  float* cs = reinterpret_cast<float*>(ws);
+  int64_t* ci = reinterpret_cast<int64_t*>(ws + (size_t)nch * Q * k * 4);
+  for (int64_t c = 0; c < nch; ++c) {
+    const int64_t c0 = c * nc, n = (N - c0 < nc) ? N - c0 : nc;
+    const int rc = scan_topk_impl(eb, smul, queries, static_cast<const char*>(docs) + c0 * D * eb,
+                                  Q, n, D, k, doc_offset + c0, ws + lists,
+                                  workspace_bytes - (int64_t)lists, cs + c * Q * k, ci + c * Q * k,
+                                  st);
+    if (rc) return rc;
+  }
+  ListSource src{cs, ci, (int)nch, (int)Q, (int)k};
+  if (k > 512)
+    hipLaunchKernelGGL((select_kernel_bigk<ListSource>), dim3(Q), dim3(SEL_NT), 0, st, src, (int)k,
+                       (int)SEL_FINAL, nullptr, out_score, out_idx, 1.0f);
+  else
+    hipLaunchKernelGGL((select_kernel<ListSource>), dim3(Q), dim3(SEL_NT), 0, st, src, (int)k,
+                       (int)SEL_FINAL, nullptr, out_score, out_idx, 1.0f);
+  return check_launch("select_kernel(chunk merge)");
+}
+
 // The scan for both element widths (eb = 2: bf16, 1: e4m3; smul scales the
 // returned scores, 1 for bf16).
 static int scan_topk_impl(int eb, float smul, const void* queries, const void* docs, int64_t Q,
@@ -2373,6 +2438,10 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
                        (int)SEL_FINAL, nullptr, out_score, out_idx, 1.0f);
     return check_launch("select_kernel(empty)");
   }
+  const int64_t nc = chunk_docs(Q, N, D, k, eb);
+  if (nc < N)
+    return scan_topk_chunked(eb, smul, queries, docs, Q, N, D, k, doc_offset, nc, workspace,
+                             workspace_bytes, out_score, out_idx, st);
   const Plan p = make_plan(Q, N, D, k, eb);
   IRC_REQUIRE(workspace != nullptr && workspace_bytes >= (int64_t)p.bytes,
               "scan_topk: workspace %lld < required %lld bytes", (long long)workspace_bytes,
@@ -2552,12 +2621,12 @@ extern "C" int irc_scan_set_ppl_min_q(int q) { return ppl_min_q_ref().exchange(q
 
 extern "C" int64_t irc_scan_topk_workspace(int64_t Q, int64_t N, int64_t D, int64_t k) {
   if (Q <= 0 || N <= 0 || k <= 0) return 256;
-  return (int64_t)make_plan(Q, N, D, k, 2).bytes;
+  return (int64_t)workspace_bytes_for(Q, N, D, k, 2);
 }
 
 extern "C" int64_t irc_scan_topk_fp8_workspace(int64_t Q, int64_t N, int64_t D, int64_t k) {
   if (Q <= 0 || N <= 0 || k <= 0) return 256;
-  return (int64_t)make_plan(Q, N, D, k, 1).bytes;
+  return (int64_t)workspace_bytes_for(Q, N, D, k, 1);
 }
 
 extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, int64_t N,

@@ -351,7 +351,8 @@ class BertModel(nn.Module):
             raise ValueError(f"sequence length {L} > max_position_embeddings")
         H, heads, eps = c.hidden_size, c.num_attention_heads, c.layer_norm_eps
         w = self._weights()
-        if self.ln_fold and compute_dtype() == torch.bfloat16:
+        # the fold runs on bf16 weights: MX-fp8 weights (C5) keep the unfolded encoder
+        if self.ln_fold and compute_dtype() == torch.bfloat16 and not self._fp8_mode():
             return self._encode_folded(ids, mask, w).view(B, L, H)
         n1 = self._split_point(B, L) if ids.is_cuda else 0
         if n1:
@@ -364,7 +365,7 @@ class BertModel(nn.Module):
     def _split_point(self, B: int, L: int) -> int:
         """Sequences of the whole-wave chunk, or 0 (no split): only when the rows past
         the last multiple of SPLIT_ROWS are a small remainder (<= 1/4 of it)."""
-        if not self.split_tail or self.ln_fold:
+        if not self.split_tail or (self.ln_fold and not self._fp8_mode()):
             return 0
         M, R = B * L, self.SPLIT_ROWS
         full = M // R * R

@@ -93,10 +93,6 @@ _HEAD_SPLIT = os.environ.get("IRC_HEAD_SPLIT", "1") != "0"
 # it CUs (profiles/r05_zc_split_cap_ab.txt; a cap of 64 measured slower)
 SPLIT_MAX_BLOCKS = int(os.environ.get("IRC_HEAD_SPLIT_BLOCKS", "128"))
 
-# Grid cap of the input projection (a static persistent tile loop over at most this many
-# workgroups, irc_gemm_ex max_blocks; 0 = one workgroup per tile)
-PROJ_MAX_BLOCKS = int(os.environ.get("IRC_HEAD_PROJ_BLOCKS", "0"))
-
 
 def _gemm_rows_split(x, w, b):
     """xp = x . w^T + b (fp32 out) -- as one GEMM, or, when M sits just above a whole
@@ -106,10 +102,8 @@ def _gemm_rows_split(x, w, b):
     ncu = _cu_count(x.device) if (_HEAD_SPLIT and x.is_cuda) else 0
     rpw = 256 * (ncu // ct) if ct and ncu % ct == 0 else 0  # rows per wave of tiles
     full = M // rpw * rpw if rpw else 0
-    mb = PROJ_MAX_BLOCKS
     if full == 0 or M == full or M - full > rpw // 4:
-        return ops.gemm(x, w, bias=b, epilogue=ops.EPI_BIAS, out_dtype=torch.float32,
-                        max_blocks=mb)
+        return ops.gemm(x, w, bias=b, epilogue=ops.EPI_BIAS, out_dtype=torch.float32)
     out = torch.empty((M, N), dtype=torch.float32, device=x.device)
     cur = torch.cuda.current_stream(x.device)
     side = side_stream(x.device, "head_tail")
@@ -118,7 +112,7 @@ def _gemm_rows_split(x, w, b):
         ops.gemm(x[full:], w, bias=b, epilogue=ops.EPI_BIAS, out=out[full:])
     for t in (x, w, b, out):
         t.record_stream(side)
-    ops.gemm(x[:full], w, bias=b, epilogue=ops.EPI_BIAS, out=out[:full], max_blocks=mb)
+    ops.gemm(x[:full], w, bias=b, epilogue=ops.EPI_BIAS, out=out[:full])
     cur.wait_stream(side)
     return out
 

@@ -111,7 +111,8 @@ def gemm(a, b, *, trans_a=False, b_is_nk=True, bias=None, epilogue=EPI_NONE, res
     a: [M, K] (or [K, M] with trans_a); b: [N, K] when b_is_nk (nn.Linear weight
     layout, i.e. a @ b.T) else [K, N].  Inputs bf16 or fp32 (same dtype);
     fp32 inputs run the exact fp32 MFMA.  2-D only (see gemm_strided).  max_blocks
-    caps a split-K launch (irc_gemm_ex; 0 = one wave).
+    caps a split-K launch (irc_gemm_ex; 0 = one wave); a negative value caps the grid of an
+    unsplit launch at -max_blocks workgroups instead (a static persistent tile loop).
     """
     require_hip(a, b, bias, residual, out)
     if a.dtype != b.dtype:

@@ -164,7 +164,10 @@ class FusedSGD(_LiveLR):
             ops.fault_gate(coef, *faults)
         self.last_norm = coef
         shadow = self.head.shadow_buffer() if hasattr(self.head, "shadow_buffer") else None
-        ops.sgd_step(self.head.flat.detach(), g, buf, coef, self.lr, self.momentum,
+        # unclipped and ungated (FusedAdam's rule): the kernel reads no coefficient, so a
+        # non-finite norm cannot reach the update through inf / inf
+        use = coef if (max_norm is not None or faults) else None
+        ops.sgd_step(self.head.flat.detach(), g, buf, use, self.lr, self.momentum,
                      self.weight_decay, not self.started, shadow)
         # a gated first step leaves the zero buffer unwritten: the next step's
         # mom * 0 + d is then exactly torch's first-step d, so no host check is needed

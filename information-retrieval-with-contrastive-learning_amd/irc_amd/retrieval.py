@@ -240,12 +240,25 @@ class ShardedDenseIndex:
         """Global top-k of the gathered queries.  ``equal_counts``: every rank
         passes the same number of queries, so the ragged-count exchange (a host
         sync) is skipped and the whole search stays stream-ordered."""
+        if not self._sharded():
+            return self._local_topk(queries, k, ws_tag)
+        allq = self._gather_queries(queries, equal_counts)  # (1)
+        s, i = self._local_topk(allq, k, ws_tag)  # (2)
+        return self._exchange_merge(s, i, k)  # (3)
+
+    # The three steps of a sharded search, separately callable (bench.py times each).
+    def _sharded(self):
         import torch.distributed as dist
 
-        if self.group is None or not dist.is_initialized() or dist.get_world_size(self.group) == 1:
-            return self._local_topk(queries, k, ws_tag)
+        return not (self.group is None or not dist.is_initialized() or
+                    dist.get_world_size(self.group) == 1)
+
+    def _gather_queries(self, queries, equal_counts=False):
+        """(1) every rank's query slice, all-gathered in rank order (ragged: the counts
+        are exchanged first, a host sync that ``equal_counts`` skips)."""
+        import torch.distributed as dist
+
         world = dist.get_world_size(self.group)
-        # (1) all-gather query embeddings (ragged: exchange counts first)
         if equal_counts:
             counts = [queries.shape[0]] * world
         else:
@@ -262,10 +275,14 @@ class ShardedDenseIndex:
             qpad[: queries.shape[0]] = queries
         gathered = [torch.empty_like(qpad) for _ in range(world)]
         dist.all_gather(gathered, qpad, group=self.group)
-        allq = torch.cat([g[:c] for g, c in zip(gathered, counts)], dim=0)
-        # (2) local exact top-k over this shard (global indices)
-        s, i = self._local_topk(allq, k, ws_tag)
-        # (3) exchange per-shard lists and merge (every rank gets the result)
+        return torch.cat([g[:c] for g, c in zip(gathered, counts)], dim=0)
+
+    def _exchange_merge(self, s, i, k):
+        """(3) every shard's exact top-k lists (global doc ids) all-gathered and merged
+        by the (score desc, index asc) rule: every rank gets the global result."""
+        import torch.distributed as dist
+
+        world = dist.get_world_size(self.group)
         ss = [torch.empty_like(s) for _ in range(world)]
         ii = [torch.empty_like(i) for _ in range(world)]
         dist.all_gather(ss, s.contiguous(), group=self.group)

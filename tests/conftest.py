@@ -18,6 +18,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU tests")
 
 
+def bf16_ulps(got, ref, floor):
+    """Largest |got - ref| in bf16 ulps of the reference value: the ulp taken at
+    max(|ref|, floor) (bf16 keeps 8 significant bits: ulp(x) = 2^(floor(log2 x) - 7)).
+    The floor is the scale of the quantity (e.g. 1 for LayerNorm outputs): near zero a
+    bf16 result carries the rounding of the O(floor) values it was computed from, not
+    ulps of its own tiny magnitude.  Used for every bf16-output bound: an absolute bound
+    on bf16 outputs is either loose at small values or fails at large ones."""
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    ulp = np.exp2(np.floor(np.log2(np.maximum(np.abs(ref), floor))) - 7)
+    return float(np.max(np.abs(got - ref) / ulp))
+
+
 def load_golden(name):
     with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
         return {k: z[k] for k in z.files}

@@ -138,8 +138,8 @@ def test_splitk_block_cap(gpu, max_blocks):
                                           (4000, 1536, 512, 2, torch.bfloat16),
                                           (3000, 1000, 256, 0, torch.float32)])
 def test_grid_cap_bit_identical(gpu, max_blocks, M, N, K, epi, od):
-    """irc_gemm_ex max_blocks on a launch of more 256 x 256 tiles than the cap (the LSTM
-    head's input projection): a static persistent tile loop over max_blocks workgroups,
+    """irc_gemm_ex with a negative max_blocks (a grid cap) on a launch of more 256 x 256
+    tiles than the cap: a static persistent tile loop over -max_blocks workgroups,
     bit-identical to one workgroup per tile."""
     from irc_amd import ops
 
@@ -149,7 +149,7 @@ def test_grid_cap_bit_identical(gpu, max_blocks, M, N, K, epi, od):
     bias = torch.randn(N, generator=g).to(gpu)
     kw = dict(bias=bias if epi else None, epilogue=epi, out_dtype=od)
     ref = ops.gemm(a, w, **kw)
-    capped = ops.gemm(a, w, max_blocks=max_blocks, **kw)
+    capped = ops.gemm(a, w, max_blocks=-max_blocks, **kw)
     assert torch.equal(ref, capped)
 
 

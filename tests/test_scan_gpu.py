@@ -420,3 +420,37 @@ def test_single_pass_gemm_filter_equals_sampled_pipeline(gpu, Q, fp8):
         finally:
             retrieval.set_single_pass_min_q(prev)
         assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][0], outs[1][0])
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_shard_beyond_one_pass_is_chunked_exact(gpu, dtype):
+    """A shard of more 256-doc tiles than the GEMM filter's select handles in one pass
+    (4096 tiles = 1,048,576 docs) at Q >= 192: scanned as two doc chunks plus a merge
+    (scan_topk.hip chunk_docs).  Integer grid with many ties across the chunk boundary:
+    bit-exact against the oracle (the first queries) and, for every query, against the
+    same queries below the GEMM-filter threshold (Q = 191: one unchunked pass)."""
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(41)
+    N, D, k = (1 << 20) + 3000, 128, 100
+    d = _grid(rng, (N, D), lim=3 if dtype == "bf16" else 2)
+    q = _grid(rng, (192, D), lim=3 if dtype == "bf16" else 2)
+    if dtype == "fp8":
+        d8, q8 = O.quantize_e4m3(d * 16), O.quantize_e4m3(q * 16)
+        run = lambda qq: retrieval.scan_topk_fp8(_dev(qq, gpu), _dev(d8, gpu), k, 5,  # noqa
+                                                 1.0 / 256)
+        qsrc = q8
+    else:
+        run = lambda qq: retrieval.scan_topk(_dev(qq, gpu), _dev(d, gpu), k, 5)  # noqa: E731
+        qsrc = q
+    s, i = (t.cpu().numpy() for t in run(qsrc))
+    s1, i1 = (t.cpu().numpy() for t in run(qsrc[:191]))
+    np.testing.assert_array_equal(i[:191], i1)
+    np.testing.assert_array_equal(s[:191], s1)
+    if dtype == "fp8":
+        ri, rs = O.scan_topk_fp8(q8[:6], d8, k, 5, 1.0 / 256)
+    else:
+        ri, rs = O.scan_topk(q[:6], d, k, 5)
+    np.testing.assert_array_equal(i[:6], ri)
+    np.testing.assert_array_equal(s[:6], rs)
+    assert (i[:, 1:] != i[:, :-1]).all()
