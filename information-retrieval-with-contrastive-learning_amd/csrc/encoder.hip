@@ -795,34 +795,19 @@ extern "C" int irc_layernorm(int dtype, const void* x, void* y, const float* gam
   const bool al = ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0 &&
                   ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0;
   if (dtype == 0 && al && (H == 768 || H == 1024 || H == 512)) {
-    const dim3 g8((unsigned)((rows + 7) / 8));
     hipStream_t st = as_stream(stream);
     prof_begin(st);
-    // IRC_LN_ROWS=1 selects the one-row-per-half-wave kernel (A/B, read once; bit-identical):
-    // 4 rows per half-wave measured 15.9 vs 17.7 us over [32768, 768] (6.35 vs 5.70 TB/s,
-    // profiles/r04_w_ln_rows.txt)
-    static const int nr = [] {
-      const char* e = getenv("IRC_LN_ROWS");
-      return (e && e[0] == '1') ? 1 : 4;
-    }();
+    // 4 rows per half-wave: 15.9 vs 17.7 us over [32768, 768] for the one-row
+    // layernorm_vec_kernel (6.35 vs 5.70 TB/s, bit-identical; profiles/r04_w_ln_rows.txt)
     const dim3 g32((unsigned)((rows + 31) / 32));
-    if (nr == 4 && H == 768)
+    if (H == 768)
       hipLaunchKernelGGL((enc::layernorm_rows_kernel<3, 4>), g32, dim3(256), 0, st,
                          (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
-    else if (nr == 4 && H == 1024)
+    else if (H == 1024)
       hipLaunchKernelGGL((enc::layernorm_rows_kernel<4, 4>), g32, dim3(256), 0, st,
                          (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
-    else if (nr == 4)
-      hipLaunchKernelGGL((enc::layernorm_rows_kernel<2, 4>), g32, dim3(256), 0, st,
-                         (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
-    else if (H == 768)
-      hipLaunchKernelGGL((enc::layernorm_vec_kernel<3>), g8, dim3(256), 0, st,
-                         (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
-    else if (H == 1024)
-      hipLaunchKernelGGL((enc::layernorm_vec_kernel<4>), g8, dim3(256), 0, st,
-                         (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
     else
-      hipLaunchKernelGGL((enc::layernorm_vec_kernel<2>), g8, dim3(256), 0, st,
+      hipLaunchKernelGGL((enc::layernorm_rows_kernel<2, 4>), g32, dim3(256), 0, st,
                          (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps);
     prof_end("layernorm", st, (double)rows * H * 4.0);
     return check_launch("layernorm_vec_kernel");
@@ -854,26 +839,9 @@ extern "C" int irc_layernorm_mx(const void* x, void* y, const float* gamma, cons
   prof_begin(st);
   auto* yy8 = static_cast<unsigned char*>(y8);
   auto* yys = static_cast<unsigned char*>(ys);
-  // the 4-rows kernel only on request (IRC_LN_MX_ROWS=4): with the MX outputs it measured
-  // no faster (C5 step 29.2k / 29.2k vs 29.3k / 29.3k pairs/s, profiles/r04_y_ln_mx_rows.txt)
-  static const bool rows4 = [] {
-    const char* e = getenv("IRC_LN_MX_ROWS");
-    return e && e[0] == '4';
-  }();
-  const dim3 g32((unsigned)((rows + 31) / 32));
-  if (rows4 && H == 768)
-    hipLaunchKernelGGL((enc::layernorm_rows_kernel<3, 4>), g32, dim3(256), 0, st,
-                       (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
-                       yys, mpad);
-  else if (rows4 && H == 1024)
-    hipLaunchKernelGGL((enc::layernorm_rows_kernel<4, 4>), g32, dim3(256), 0, st,
-                       (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
-                       yys, mpad);
-  else if (rows4)
-    hipLaunchKernelGGL((enc::layernorm_rows_kernel<2, 4>), g32, dim3(256), 0, st,
-                       (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
-                       yys, mpad);
-  else if (H == 768)
+  // one row per half-wave: the 4-rows kernel with the MX outputs measured no faster
+  // (C5 step 29.2k / 29.2k vs 29.3k / 29.3k pairs/s, profiles/r04_y_ln_mx_rows.txt)
+  if (H == 768)
     hipLaunchKernelGGL((enc::layernorm_vec_kernel<3>), g8, dim3(256), 0, st,
                        (const unsigned short*)x, (unsigned short*)y, gamma, beta, rows, eps, yy8,
                        yys, mpad);

@@ -646,28 +646,21 @@ __device__ __forceinline__ void mainloop_mf16(const unsigned short* A, int64_t l
 }
 }  // namespace big
 
-// IRC_BIG_RING=1 selects the 4-slot ring of gemm_big_kernel (A/B; read on first use;
-// default off: within noise of the 2-slot loop on every BERT shape and 1.4% slower on
-// the C2 step, profiles/r03_ring_r_*); irc_gemm_set_big_ring switches it at run time
-// (the tests compare both bit for bit).
+// The 4-slot ring of gemm_big_kernel: off (within noise of the 2-slot loop on every BERT
+// shape and 1.4% slower on the C2 step, profiles/r03_ring_r_*); irc_gemm_set_big_ring
+// switches it at run time (the tests compare both bit for bit).
 inline std::atomic<int>& big_ring_mode() {
-  static std::atomic<int> on{[] {
-    const char* e = getenv("IRC_BIG_RING");
-    return (e && e[0] == '1') ? 1 : 0;
-  }()};
+  static std::atomic<int> on{0};
   return on;
 }
 inline bool big_ring() { return big_ring_mode().load(std::memory_order_relaxed) != 0; }
 
-// The 16x16x32 MFMA form of gemm_big_kernel is the default (IRC_BIG_MF16=0 selects the
-// 32x32x16 form; read on first use; irc_gemm_set_big_mf16 switches it at run time).
-// Measured on MI355X, interleaved (profiles/r04_f_*): out-proj 48.6 / 48.4 vs 53.1 /
-// 50.3 us, FFN2 156.7 / 152.9 vs 163.5 / 164.2 us, the C2 step 27.3k vs 26.7k pairs/s.
+// The 16x16x32 MFMA form of gemm_big_kernel is the default (irc_gemm_set_big_mf16 selects
+// the 32x32x16 form at run time; the tests compare both).  Measured on MI355X,
+// interleaved (profiles/r04_f_*): out-proj 48.6 / 48.4 vs 53.1 / 50.3 us, FFN2 156.7 /
+// 152.9 vs 163.5 / 164.2 us, the C2 step 27.3k vs 26.7k pairs/s.
 inline std::atomic<int>& big_mf16_mode() {
-  static std::atomic<int> on{[] {
-    const char* e = getenv("IRC_BIG_MF16");
-    return (e && e[0] == '0') ? 0 : 1;
-  }()};
+  static std::atomic<int> on{1};
   return on;
 }
 inline bool big_mf16() { return big_mf16_mode().load(std::memory_order_relaxed) != 0; }
@@ -1378,15 +1371,10 @@ static int by_layout(int la, int lb, int epi, const Args& g, int batch, int spli
 
 using namespace irc;
 
-// IRC_GEMM_GROUP_M: grouped output-tile order of the 256-row GEMM kernels (rows per
-// group; 0 = row-major).  Read once.
-static int gemm_group_m() {
-  static const int gm = [] {
-    const char* e = getenv("IRC_GEMM_GROUP_M");
-    return e ? atoi(e) : 0;
-  }();
-  return gm;
-}
+// Grouped output-tile order of the 256-row GEMM kernels (row tiles per group): 0 =
+// row-major; grouping measured no faster (profiles/r02_group_i_*).  The kernels keep the
+// grouped form (grouped_tile) for callers that set PArgs / Args group_m themselves.
+static int gemm_group_m() { return 0; }
 
 // IRC_GEMM_PP=0 disables the ping-pong path (A/B experiments; read once).
 static bool pp_enabled() {

@@ -1133,13 +1133,11 @@ extern "C" int irc_pp_dbg_stamps(uint64_t* out /* [16] */) {
 #endif
 }
 
-// IRC_GEMM_PERSIST=0 turns the persistent form off (A/B experiments; read on first
-// use); irc_gemm_set_persistent switches it at run time (the tests compare both forms).
+// The persistent form is off by default (BERT shapes within +-2%, the GEMM scan filter
+// +3% at C2, profiles/r02_gemm_ab_f_*); irc_gemm_set_persistent switches it at run time
+// (the tests compare every mode bit for bit).
 static std::atomic<int>& pers_mode() {
-  static std::atomic<int> on{[] {
-    const char* e = getenv("IRC_GEMM_PERSIST");
-    return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 0;
-  }()};
+  static std::atomic<int> on{0};
   return on;
 }
 static bool pers_enabled() { return pers_mode().load(std::memory_order_relaxed) != 0; }

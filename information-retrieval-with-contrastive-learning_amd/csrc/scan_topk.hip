@@ -37,6 +37,11 @@
 // are in flight during the MFMAs and the epilogue instead of NBUF - 1 (0: the
 // round-2 order, the next DMA at the top of each iteration).
 #define IRC_SCAN_EARLY_ISSUE 1
+// 1: that DMA is issued piece by piece between the tile's MFMAs instead of all at once
+// ahead of them (A/B build flag)
+#ifndef IRC_SCAN_IL
+#define IRC_SCAN_IL 0
+#endif
 
 namespace irc {
 namespace scan {
@@ -185,6 +190,19 @@ void scan_tile_kernel(
     grow[t] = row;
     goff[t] = (uint32_t)(row * row_bytes + c * 16);
   }
+  // piece t (of PW) of this wave's share of tile `tile`'s DMA into ring slot `buf`
+  auto issue_piece = [&](int tile, int buf, int t) {
+    char* base = smem + buf * G::TILE_BYTES;
+    const char* src0 = reinterpret_cast<const char*>(docs) + (int64_t)tile * TD * row_bytes;
+    const bool tail = (tile + 1) * TD > NS;  // uniform
+    const int i = t * NW + wave;
+    if (G::GLDS_PER_TILE % NW == 0 || i < G::GLDS_PER_TILE) {
+      uint32_t off = goff[t];
+      if (tail && tile * TD + grow[t] >= NS)  // clamp: loaded but never kept
+        off -= (uint32_t)((tile * TD + grow[t] - (NS - 1)) * row_bytes);
+      glds16_pol<IRC_SCAN_AUX>(src0 + off, base + i * 1024);
+    }
+  };
   auto issue_tile = [&](int tile, int buf) {
     char* base = smem + buf * G::TILE_BYTES;
     const char* src0 = reinterpret_cast<const char*>(docs) + (int64_t)tile * TD * row_bytes;
@@ -280,7 +298,7 @@ void scan_tile_kernel(
       if (IRC_SCAN_EARLY_ISSUE) {
         // the slot is free once every wave's fragment reads have returned
         lds_barrier();
-        if (it + G::NBUF < my_tiles) issue_tile(tile + G::NBUF, it % G::NBUF);
+        if (!IRC_SCAN_IL && it + G::NBUF < my_tiles) issue_tile(tile + G::NBUF, it % G::NBUF);
       }
 #pragma unroll
       for (int c = 0; c < NCW; ++c) {
@@ -293,6 +311,13 @@ void scan_tile_kernel(
           const l2 a2 = __builtin_bit_cast(l2, af[c]), b2 = __builtin_bit_cast(l2, bq[c]);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a2[0], b2[0], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a2[1], b2[1], acc, 0, 0, 0);
+        }
+        if (IRC_SCAN_IL && IRC_SCAN_EARLY_ISSUE && it + G::NBUF < my_tiles) {
+          // the next DMA spread over the MFMA chain: a piece whose issue stalls on a full
+          // memory queue then no longer holds back the MFMAs behind it
+#pragma unroll
+          for (int t = 0; t < PW; ++t)
+            if (t * NCW / PW == c) issue_piece(tile + G::NBUF, it % G::NBUF, t);
         }
       }
     }

@@ -3,7 +3,6 @@ HIP stream, and the workspace allocator.  PyTorch is plumbing only here: memory,
 streams, autograd bookkeeping and torch.distributed -- never the compute."""
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -31,14 +30,11 @@ def stream_ptr(device: torch.device | None = None):
 _side: dict = {}
 
 
-# Streams created with the high priority: none by default.  The frozen encoder's feature
-# prefetch at high priority gained the C2 step 0.6-1.1% in round 4 (profiles/r04_q_priority_ab.txt)
-# and now costs it 0.5-1%; once such a stream exists in the process the pipelined retrieval
-# (search_many) runs slower too -- C2 3.58M -> 2.1M queries/s (round 4: serial calls unchanged)
-# (profiles/r05_zh_priority_ab.txt, r04_t_priority_retrieval.txt); the heads' streams at high
-# priority measured 3% slower.  IRC_HIGH_PRIORITY_STREAMS: comma-separated tags (A/B runs).
-HIGH_PRIORITY_TAGS: tuple = tuple(
-    t for t in os.environ.get("IRC_HIGH_PRIORITY_STREAMS", "").split(",") if t and t != "none")
+# Every side stream has the default priority.  The frozen encoder's feature prefetch at high
+# priority gained the C2 step 0.6-1.1% in round 4 (profiles/r04_q_priority_ab.txt) and later
+# cost it 0.5-1%; once such a stream exists in the process the pipelined retrieval
+# (search_many) runs slower too -- C2 3.58M -> 2.1M queries/s (profiles/r05_zh_priority_ab.txt,
+# r04_t_priority_retrieval.txt); the heads' streams at high priority measured 3% slower.
 
 
 _serial = [0]
@@ -65,8 +61,7 @@ def side_stream(device: torch.device, tag: str = "side") -> torch.cuda.Stream:
     key = (torch.device(device).index, tag)
     s = _side.get(key)
     if s is None:
-        prio = torch.cuda.Stream.priority_range()[1] if tag in HIGH_PRIORITY_TAGS else 0
-        s = _side[key] = torch.cuda.Stream(device=device, priority=prio)
+        s = _side[key] = torch.cuda.Stream(device=device)
     return s
 
 

@@ -19,7 +19,7 @@ from conftest import bf16_ulps
 pytestmark = pytest.mark.gpu
 
 ATT_FLOOR = 0.5  # the context's scale: averages of V rows ~ N(0, 1)
-ATT_ULPS = 5.0
+ATT_ULPS = 3.0  # measured on MI355X: at most 1.52 over L in [1, 512] (r6_b)
 
 
 def _ref(qkv, mask, B, L, H, heads):

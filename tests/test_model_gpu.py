@@ -54,7 +54,7 @@ def test_bert_tiny_bf16(gpu):
     np.testing.assert_allclose(out.float().cpu().numpy(), g["last_hidden_state"], atol=6e-2)
 
 
-@pytest.mark.parametrize("mode,atol", [("fp32", 3e-4), ("bf16", 8.0)])
+@pytest.mark.parametrize("mode,atol", [("fp32", 3e-4), ("bf16", 8.0)])  # bf16: 4.79 ulps measured
 def test_bert_long_512_matches_reference(gpu, mode, atol):
     """The reference's own bert_extract at the 512-token truncation
     (tests/golden/bert_long.npz, a 600-word sentence in the joint batch): L = 512

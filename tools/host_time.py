@@ -19,13 +19,7 @@ import bench  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--prio", action="store_true",
-                    help="heads (and their side streams) on high-priority streams")
     a = ap.parse_args()
-    if a.prio:
-        from irc_amd import _torch as T
-
-        T.HIGH_PRIORITY_TAGS = ("key_encoder", "lstm_wgrad", "heads")
     from src.model import build_model, get_optimizer
     from src.train import TrainState
 
@@ -40,9 +34,7 @@ def main():
     ids, mask = ids.to(dev), mask.to(dev)
     pending = [model.bert_extract_async(ids, mask, bench.TRAIN_B)]
 
-    from irc_amd._torch import side_stream
-
-    hs = side_stream(dev, "heads") if a.prio else torch.cuda.current_stream(dev)
+    hs = torch.cuda.current_stream(dev)
 
     def step():
         handle = pending[0]

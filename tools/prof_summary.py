@@ -50,4 +50,5 @@ if __name__ == "__main__":
             glob.glob(os.path.join(p, "**", "*kernel_trace.csv"), recursive=True)
         p = cands[0]
     rows = from_db(p) if p.endswith(".db") else from_csv(p)
-    print(summarise(rows))
+    top = [int(a.split("=", 1)[1]) for a in sys.argv[1:] if a.startswith("--top=")]
+    print(summarise(rows, top[0] if top else 25))
