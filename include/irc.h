@@ -414,6 +414,9 @@ int irc_enqueue(float* queue, const float* keys, int64_t* ptr, int64_t D, int64_
 int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t stream);
 /* y bf16 [C][R] = transpose of x fp32 [R][C] (weights as the NK GEMM operand). */
 int irc_cast_bf16_t(const float* x, void* y, int64_t R, int64_t C, irc_stream_t stream);
+/* irc_cast_bf16_t over `batch` matrices: x + b * sx (floats) -> y + b * sy (bf16 elements). */
+int irc_cast_bf16_t_batched(const float* x, void* y, int64_t R, int64_t C, int64_t batch,
+                            int64_t sx, int64_t sy, irc_stream_t stream);
 int irc_axpby(float* out, const float* x, const float* y, float a, float b, int64_t n,
               irc_stream_t stream);
 /* column sums of x [R][C] (dtype 0 bf16, 1 fp32) into fp32 out; partial holds

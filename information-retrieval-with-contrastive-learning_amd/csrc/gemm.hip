@@ -1385,13 +1385,11 @@ static bool pp_enabled() {
   return on;
 }
 
-#ifndef IRC_SPLIT_BLOCKS_DEFAULT  // diagnostic builds: another default split-K cap
-#define IRC_SPLIT_BLOCKS_DEFAULT 256
-#endif
+constexpr int64_t SPLIT_BLOCKS_DEFAULT = 256;  // split-K budget: one wave of 256 x 256 blocks
 // max_blocks > 0: the split-K budget; < 0: a grid cap of -max_blocks workgroups on an
 // unsplit launch (the split-K budget stays the default); 0: neither.
 static inline int64_t split_budget(int64_t max_blocks) {
-  return max_blocks > 0 ? max_blocks : IRC_SPLIT_BLOCKS_DEFAULT;
+  return max_blocks > 0 ? max_blocks : SPLIT_BLOCKS_DEFAULT;
 }
 static inline int64_t grid_cap(int64_t max_blocks) { return max_blocks < 0 ? -max_blocks : 0; }
 

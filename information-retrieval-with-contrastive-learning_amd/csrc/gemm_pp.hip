@@ -701,10 +701,6 @@ __device__ __forceinline__ void epilogue_scan(const PArgs& g, const f32x4 (&acc)
     thk[threadIdx.x] = t;
     const uint32_t hi = (uint32_t)(t >> 32);
     // padded query rows never pass; no threshold (hi == 0) admits everything
-#ifdef IRC_PP_SCAN_NOPASS  // diagnostic build: nothing passes
-    thf[threadIdx.x] = __builtin_huge_valf();
-    if (true) {} else
-#endif
     thf[threadIdx.x] = q >= g.M ? __builtin_huge_valf()
                                 : (hi == 0 ? -__builtin_huge_valf() : unorderable_f32(hi));
   }
@@ -738,11 +734,6 @@ __device__ __forceinline__ void epilogue_scan(const PArgs& g, const f32x4 (&acc)
       }
   }
   PSTAMP(2);
-#ifdef IRC_PP_SCAN_MASKONLY  // diagnostic build: mask, no exact path
-  if (threadIdx.x < 256 && m0 + (int)threadIdx.x < g.qpad)
-    g.counts[(int64_t)tn * g.qpad + m0 + threadIdx.x] = __popcll(pm[0] | pm[1]) == 999 ? 1u : 0u;
-  return;
-#endif
 #pragma unroll
   for (int qq = 0; qq < 4; ++qq) {
     uint32_t bits = (uint32_t)(pm[qq >> 1] >> (32 * (qq & 1)));
@@ -1314,11 +1305,7 @@ bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, i
     const int64_t t256 = ((M + 255) / 256) * ((N + 255) / 256) * batch;
     int64_t ncu = cu_count();
     if (ncu <= 0) ncu = 256;
-#ifdef IRC_PP_TIES_PP  // diagnostic build: ties to the 256x256 kernel (the round-4 rule)
-    if (3 * ((t384 + ncu - 1) / ncu) < 2 * ((t256 + ncu - 1) / ncu)) return false;
-#else
     if (3 * ((t384 + ncu - 1) / ncu) <= 2 * ((t256 + ncu - 1) / ncu)) return false;
-#endif
   }
   if ((uintptr_t)A % 16 || (uintptr_t)B % 16) return false;
   if (lda % 8 || ldb % 8 || sA % 8 || sB % 8) return false;

@@ -38,9 +38,13 @@
 // round-2 order, the next DMA at the top of each iteration).
 #define IRC_SCAN_EARLY_ISSUE 1
 // 1: that DMA is issued piece by piece between the tile's MFMAs instead of all at once
-// ahead of them (A/B build flag)
+// ahead of them, so a piece whose issue waits on a full memory queue no longer holds the
+// MFMAs back.  C3 shard (250k x 768), filter: Q = 48 / 64 / 96 / 128 single pass
+// 92.6-95.4 / 92.9-93.1 / 108.6-109.0 / 111.0-111.7 -> 87.5-88.5 / 88.0-88.4 / 105.0-105.2 /
+// 108.1-108.6 us, the sampled pipeline at Q = 64 84.6 -> 79.5-79.9 us, Q <= 16 within
+// +-1 us (two interleaved runs, profiles/r06_e_*); same results (0: the all-at-once form).
 #ifndef IRC_SCAN_IL
-#define IRC_SCAN_IL 0
+#define IRC_SCAN_IL 1
 #endif
 
 namespace irc {
@@ -1217,218 +1221,6 @@ __global__ __launch_bounds__(SEL_NT) void select_kernel_bigk(Src src, int k, int
   select_body<Src, true>(src, k, mode, thr_out, out_score, out_idx, smul);
 }
 
-// Wave-per-query select for region sources (the scan's two selects): the same
-// exact radix select (8-bit digits, MSB first, early exit when the chosen bucket
-// holds exactly the remaining rank) and the same outputs as select_kernel, but
-// one wave per query (SWQ per workgroup), so every step is
-// wave-synchronous (no workgroup barriers).  Candidates are staged in the wave's
-// LDS slice (up to SW keys); a query with more candidates visits its regions in
-// global memory on every pass instead, lanes striding over regions (slower, same
-// result).  k <= SW.
-constexpr int SW = 8192;  // 64 KB of staged keys per query
-constexpr int SWQ = 1;   // queries (waves) per workgroup
-
-__device__ __forceinline__ void wsync() {
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-
-__global__ __launch_bounds__(64 * SWQ) void select_wave_kernel(RegionSource src, int Q, int k,
-                                                               int mode,
-                                                               uint64_t* __restrict__ thr_out,
-                                                               float* __restrict__ out_score,
-                                                               int64_t* __restrict__ out_idx,
-                                                               float smul) {
-  __shared__ uint64_t stage_all[SWQ][SW];
-  __shared__ uint32_t hist_all[SWQ][256];
-  __shared__ uint16_t rid_all[SWQ][SW];
-  __shared__ uint32_t roff_all[SWQ][SEL_MAXR + 1];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int q = blockIdx.x * SWQ + wv;
-  if (q >= Q) return;  // whole wave; nothing below synchronises across waves
-  uint64_t* stage = stage_all[wv];
-  uint32_t* hist = hist_all[wv];
-  const int R = src.nregions();
-  // total candidates
-  uint32_t M = 0;
-  for (int r = lane; r < R; r += 64) M += src.count(q, r);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) M += __shfl_xor(M, o, 64);
-  const bool staged = M <= (uint32_t)SW && R <= SEL_MAXR;
-  if (staged) {
-    // region offsets (running wave scan) + a region-id map in LDS, then a flat
-    // copy with 8 independent loads in flight per lane
-    uint16_t* rid = rid_all[wv];
-    uint32_t* roff = roff_all[wv];
-    uint32_t base = 0;
-    for (int r0 = 0; r0 < R; r0 += 64) {
-      const int r = r0 + lane;
-      const uint32_t c = r < R ? src.count(q, r) : 0u;
-      uint32_t incl = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-      }
-      const uint32_t off = base + incl - c;
-      if (r < R) roff[r] = off;
-      for (uint32_t j = 0; j < c; ++j) rid[off + j] = (uint16_t)r;
-      base += __shfl(incl, 63, 64);
-    }
-    wsync();
-    constexpr int U = 8;
-    for (uint32_t i0 = lane; i0 < M; i0 += 64 * U) {
-      uint64_t v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t i = i0 + 64 * u;
-        if (i < M) {
-          const int r = rid[i];
-          v[u] = src.region(q, r)[i - roff[r]];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t i = i0 + 64 * u;
-        if (i < M) stage[i] = v[u];
-      }
-    }
-    wsync();
-  }
-  auto visit = [&](auto&& f) {  // f must not use cross-lane operations
-    if (staged) {
-      for (uint32_t i = lane; i < M; i += 64) f(stage[i]);
-    } else {
-      for (int r = lane; r < R; r += 64) {
-        const uint32_t n = src.count(q, r);
-        const uint64_t* rp = src.region(q, r);
-        for (uint32_t j = 0; j < n; ++j) f(rp[j]);
-      }
-    }
-  };
-  uint64_t kth = 0;
-  if (M > (uint32_t)k) {
-    uint64_t mn = ~0ull, mx = 0;
-    visit([&](uint64_t key) {
-      mn = key < mn ? key : mn;
-      mx = key > mx ? key : mx;
-    });
-    mn = wave_min_u64(mn);
-    mx = wave_max_u64(mx);
-    const int top = 63 - __builtin_clzll((mn ^ mx) | 1ull);
-    const int first_shift = (top / 8) * 8;
-    const int last_shift = (mode == SEL_THRESHOLD) ? 48 : 0;
-    uint64_t pmask = first_shift >= 56 ? 0ull : (~0ull << (first_shift + 8));
-    uint64_t prefix = mn & pmask;
-    uint32_t kr = (uint32_t)k;
-    for (int shift = first_shift; shift >= last_shift; shift -= 8) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) hist[4 * lane + t] = 0;
-      wsync();
-      visit([&](uint64_t key) {
-        if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
-      });
-      wsync();
-      uint32_t bb[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) bb[t] = hist[4 * lane + t];
-      const uint32_t mine = bb[0] + bb[1] + bb[2] + bb[3];
-      uint32_t suf = mine;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_down(suf, o, 64);
-        if (lane + o < 64) suf += t;
-      }
-      const uint32_t above = suf - mine;
-      // the lane whose 4 digits contain the kr-th largest
-      const bool hit = suf >= kr && above < kr;
-      uint32_t sel = 0, rem = 0, selc = 0;
-      if (hit) {
-        uint32_t acc = above;
-        for (int t = 3; t >= 0; --t) {
-          if (acc + bb[t] >= kr) {
-            sel = 4 * lane + t;
-            selc = bb[t];
-            break;
-          }
-          acc += bb[t];
-        }
-        rem = kr - acc;
-      }
-      const int src_lane = __builtin_ctzll(__ballot(hit));
-      sel = __shfl(sel, src_lane, 64);
-      rem = __shfl(rem, src_lane, 64);
-      selc = __shfl(selc, src_lane, 64);
-      prefix |= (uint64_t)sel << shift;
-      pmask |= (uint64_t)0xff << shift;
-      kr = rem;
-      if (selc == rem) break;  // the bucket holds exactly the remaining rank
-    }
-    kth = (mode == SEL_THRESHOLD) ? (prefix & (~0ull << 48)) : prefix;
-  }
-  if (mode == SEL_THRESHOLD) {
-    if (lane == 0) thr_out[q] = kth;
-    return;
-  }
-  // collect the min(M, k) keys >= kth (wave prefix-sum compaction), then sort
-  const int cnt = (int)(M < (uint32_t)k ? M : (uint32_t)k);
-  int npow = 1;
-  while (npow < cnt) npow <<= 1;
-  // In-place compaction: chunk i0 is read by every lane before any of its slots
-  // is written, and the write position never passes the read position.
-  uint64_t* cand = stage;
-  uint32_t wpos = 0;
-  if (staged) {
-    for (uint32_t i0 = 0; i0 < M; i0 += 64) {
-      const uint32_t i = i0 + lane;
-      const uint64_t key = i < M ? stage[i] : 0ull;
-      const bool take = i < M && key >= kth;
-      const uint64_t bal = __ballot(take);
-      wsync();  // every lane has read its key before any slot of this chunk is written
-      if (take) cand[wpos + __popcll(bal & ((1ull << lane) - 1))] = key;
-      wpos += (uint32_t)__popcll(bal);
-      wsync();
-    }
-  } else {  // order is irrelevant (sorted below): an LDS slot counter
-    if (lane == 0) hist[0] = 0;
-    wsync();
-    visit([&](uint64_t key) {
-      if (key >= kth) cand[atomicAdd(&hist[0], 1u)] = key;
-    });
-    wsync();
-  }
-  for (int i = cnt + lane; i < npow; i += 64) cand[i] = 0ull;
-  wsync();
-  for (int size = 2; size <= npow; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = lane; i < npow; i += 64) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const bool desc = ((i & size) == 0);
-          const uint64_t x = cand[i], y = cand[j];
-          if (desc ? (x < y) : (x > y)) {
-            cand[i] = y;
-            cand[j] = x;
-          }
-        }
-      }
-      wsync();
-    }
-  }
-  for (int i = lane; i < k; i += 64) {
-    float sc = -__builtin_huge_valf();
-    int64_t id = -1;
-    if (i < cnt) {
-      const uint64_t key = cand[i];
-      sc = unorderable_f32((uint32_t)(key >> 32)) * smul;
-      id = (int64_t)(uint32_t)(~(uint32_t)key);
-    }
-    out_score[(int64_t)q * k + i] = sc;
-    out_idx[(int64_t)q * k + i] = id;
-  }
-}
-
 // ------------------------------------------------------------- select_dense
 // Final select of the single-pass LTOP scan (no sample pass, no threshold
 // select).  Per query: LS lists of LT_M keys (one per (worker, slice)), dense.
@@ -1940,25 +1732,12 @@ __global__ __launch_bounds__(SEL_NT) void select_dense_kernel(DenseArgs a) {
   STAMP(2, 20);
 }
 
-// The 256-thread select_kernel is the default: measured on MI355X (100k x 768,
-// k=100) the wave-per-query variant made the whole call 40 us slower at Q=1 and
-// 35 us slower at Q=256 (one wave walks every region and every radix pass alone).
-// IRC_SCAN_WAVE_SELECT=1 selects it, for comparison.
-static bool wave_select() {
-  static const bool v = [] {
-    const char* e = getenv("IRC_SCAN_WAVE_SELECT");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
+// One 256-thread workgroup per query (a wave-per-query variant made the whole call
+// 40 us slower at Q = 1 and 35 us at Q = 256 on MI355X, 100k x 768, k = 100: one wave
+// walked every region and every radix pass alone; removed in round 6).
 static void launch_select(const RegionSource& src, int Q, int k, int mode, uint64_t* thr,
                           float* out_score, int64_t* out_idx, float smul, hipStream_t st) {
-  if (wave_select())
-    hipLaunchKernelGGL(select_wave_kernel, dim3((unsigned)((Q + SWQ - 1) / SWQ)), dim3(64 * SWQ),
-                       0, st, src, Q, k, mode, thr, out_score, out_idx, smul);
-  else
-    if (k > 512)
+  if (k > 512)
       hipLaunchKernelGGL((select_kernel_bigk<RegionSource>), dim3((unsigned)Q), dim3(SEL_NT), 0,
                          st, src, k, mode, thr, out_score, out_idx, smul);
     else
@@ -2019,8 +1798,9 @@ struct Plan {
   size_t off_thr, off_cnt, off_keys, bytes;
 };
 
-// IRC_SCAN_PP=0 disables the GEMM-kernel filter; IRC_SCAN_PP_MINQ sets its Q floor;
-// IRC_SCAN_PP_MAX_GB caps its survivor workspace (256 slots per (256-doc tile,
+// IRC_SCAN_PP_MINQ sets the GEMM-kernel filter's Q floor (default 192; a value above
+// every Q keeps the stationary-query kernel at every Q); IRC_SCAN_PP_MAX_GB caps its
+// survivor workspace (256 slots per (256-doc tile,
 // query) region: exact for any input, 8 KB x Q x N/256; default 24 GB of the
 // 288 GB HBM, i.e. up to Q = 2048 over a 1.5M-doc shard).
 static size_t pp_max_bytes() {
@@ -2033,28 +1813,19 @@ static size_t pp_max_bytes() {
 
 static int pp_min_q() {
   static const int v = [] {
-    const char* e = getenv("IRC_SCAN_PP");
-    if (e && e[0] == '0') return 1 << 30;
     const char* m = getenv("IRC_SCAN_PP_MINQ");
     return m ? atoi(m) : 192;
   }();
   return v;
 }
 
-// IRC_SCAN_LTOP=0 keeps the sampled-threshold pipeline where LTOP would apply.
-static bool ltop_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("IRC_SCAN_LTOP");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-// LTOP up to IRC_SCAN_LTOP_MAXQ queries (default 64).  C2 corpus (100k x 768) on
-// MI355X, whole call: Q = 1 / 16 / 32 / 64: 51.4 / 56.5 / 58.4 / 61.9 us against
-// 60.0 / 64.9 / 67.3 / 71.5 with the sampled threshold; at Q = 128 the list
-// insertions (+10 us in the filter) and an occasional rescan (~1 query of 128 on
-// Gaussian data, ~12 us) cancel the gain (84.6 vs 83.1).
+// LTOP up to IRC_SCAN_LTOP_MAXQ queries (default 64; 0 keeps the sampled-threshold
+// pipeline, same results).  C2 corpus (100k x 768) on MI355X, whole call: Q = 1 / 16 /
+// 32 / 64: 51.4 / 56.5 / 58.4 / 61.9 us against 60.0 / 64.9 / 67.3 / 71.5 with the sampled
+// threshold; at Q = 96 / 128 the two pipelines are within each other's spread on the C3
+// shard (145.7-149.9 vs 140.8-144.7 us / 146.1-149.0 vs 146.2-147.6 us), the single pass
+// ahead at C2 Q = 128 (72.7-73.6 vs 87.3-89.0 us) and level at Q = 96, with a rescan
+// (~15 us in select_dense) in some batches (profiles/r06_e_*).
 static int ltop_max_q() {
   static const int v = [] {
     const char* e = getenv("IRC_SCAN_LTOP_MAXQ");
@@ -2063,32 +1834,16 @@ static int ltop_max_q() {
   return v;
 }
 
-// IRC_SCAN_PPL_MINQ sets the smallest Q of the single-pass GEMM filter (its largest is
-// 256, one query tile); unset or IRC_SCAN_PPL=0: off.
-// irc_scan_set_ppl_min_q changes it at run time (the tests compare both pipelines).
+// Smallest Q of the single-pass GEMM filter (its largest is 256, one query tile): off by
+// default -- at C2 (Q = 256) the 4-key-list epilogue costs the filter 26 us (77.7 vs 51.8)
+// and select_dense's rescans 32 us, against 36 us of sample pass + two selects
+// (profiles/r04_d_scan_*_kernels.txt); irc_scan_set_ppl_min_q changes it at run time (the
+// tests compare both pipelines).
 static std::atomic<int>& ppl_min_q_ref() {
-  static std::atomic<int> v{[] {
-    const char* e = getenv("IRC_SCAN_PPL");
-    if (e && e[0] == '0') return 1 << 30;
-    const char* m = getenv("IRC_SCAN_PPL_MINQ");
-    // off by default: at C2 (Q = 256) the 4-key-list epilogue costs the filter 26 us
-    // (77.7 vs 51.8) and select_dense's rescans 32 us, against 36 us of sample pass +
-    // two selects (profiles/r04_d_scan_*_kernels.txt)
-    return m ? atoi(m) : 1 << 30;
-  }()};
+  static std::atomic<int> v{1 << 30};
   return v;
 }
 static int ppl_min_q() { return ppl_min_q_ref().load(std::memory_order_relaxed); }
-
-// IRC_SCAN_PP_SAMPLE=0: the sampled pipeline's threshold pass stays on the tile kernel
-// (GMAX) where the filter runs on the GEMM kernel (A/B; default: the GEMM kernel).
-static bool pp_sample_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("IRC_SCAN_PP_SAMPLE");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
 
 static int pick_ks(int64_t D) { return D > 512 ? 2 : 1; }  // <= 128 fragment VGPRs/wave
 
@@ -2106,19 +1861,12 @@ static size_t tile_lds_bytes() {
   return (size_t)G::NBUF * G::TILE_BYTES + G::XBUF_BYTES;
 }
 
-// IRC_SCAN_LTOP_KS4 (read once): four k-slices in the single-pass scan for one
-// 32-query group (Q <= 32; default 1), also for two (Q <= 64; 2), or never (0).
-// Four slices give each wave half the DMA issue, MFMA chain and list insertions of a
-// tile.  C3 shard (250k x 768) filter at Q = 1 / 16 / 32: 78.5 / 85.0 / 86.0 ->
-// 74.3 / 79.7 / 79.1 us; C2: 38.7 / 43.3 / 44.4 -> 34.5 / 37.8 / 38.0 us.  Two groups
-// (8 waves): no gain (C3 Q = 33 / 64: 90.7 / 94.0 -> 90.2 / 95.6 us), so off there.
-static int ltop_ks4() {
-  static const int v = [] {
-    const char* e = getenv("IRC_SCAN_LTOP_KS4");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
+// Four k-slices in the single-pass scan for one 32-query group (Q <= 32) at D = 768 / 1024
+// bf16: each wave gets half the DMA issue, MFMA chain and list insertions of a tile.  C3
+// shard (250k x 768) filter at Q = 1 / 16 / 32: 78.5 / 85.0 / 86.0 -> 74.3 / 79.7 / 79.1 us;
+// C2: 38.7 / 43.3 / 44.4 -> 34.5 / 37.8 / 38.0 us.  Two groups (8 waves): no gain (C3 Q =
+// 33 / 64: 90.7 / 94.0 -> 90.2 / 95.6 us), so off there.
+constexpr int LTOP_KS4_GROUPS = 1;
 
 template <int EB>
 static size_t lds_bytes_eb(int64_t D) {
@@ -2155,31 +1903,13 @@ static void plan_workers(int64_t ntiles, int gy, int64_t D, int eb, int nw, int*
   *g = (int)gg;
 }
 
-// Threshold sample = N / sample_div() docs (IRC_SCAN_SAMPLE_DIV, read once; default 16:
-// C2 whole call at Q = 64 / 256 / 1024 75.3 / 98.0 / 258 us against 75.8 / 101.6 / 274 at 8,
-// and 98 / 115 / 296 at 32, tools/g4.sh).
-// Any value keeps the result exact (the threshold is the 2*KS-th group maximum of real
-// scores); it trades the sample pass against the filter's survivor count.
-// Minimum tiles per sample worker (IRC_SCAN_SAMPLE_TPW, default 1 = plan_workers'
-// choice).  Fewer, longer workers amortise each workgroup's query-fragment loads
-// but lose parallelism: C2 whole call at Q = 256 92.5 / 93.5 / 96.1 / 102.1 us for
-// 1 / 3 / 5 / 8 (MI355X).
-static int sample_min_tpw() {
-  static const int v = [] {
-    const char* e = getenv("IRC_SCAN_SAMPLE_TPW");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-static int64_t sample_div() {
-  static const int64_t v = [] {
-    const char* e = getenv("IRC_SCAN_SAMPLE_DIV");
-    const long x = e ? atol(e) : 16;
-    return (int64_t)(x >= 1 ? x : 16);
-  }();
-  return v;
-}
+// Threshold sample = N / SAMPLE_DIV docs (C2 whole call at Q = 64 / 256 / 1024 75.3 / 98.0 /
+// 258 us against 75.8 / 101.6 / 274 at 8, and 98 / 115 / 296 at 32, tools/g4.sh).  Any
+// value keeps the result exact (the threshold is the 2*KS-th group maximum of real
+// scores); it trades the sample pass against the filter's survivor count.  Longer sample
+// workers (more tiles each, fewer query-fragment loads) measured slower: C2 whole call
+// at Q = 256 92.5 / 93.5 / 96.1 / 102.1 us for 1 / 3 / 5 / 8 tiles minimum (MI355X).
+constexpr int64_t SAMPLE_DIV = 16;
 
 static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   Plan p{};
@@ -2195,8 +1925,7 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   // The filter's survivors ~ k * N / S (~1.6k per query at k = 100, N / S = 16; at the cap, e.g. a 625k
   // shard, ~k * N / 32768).
   int64_t s_target = 32 * k;
-  const int64_t sdiv = sample_div();
-  if (N / sdiv > s_target) s_target = N / sdiv;
+  if (N / SAMPLE_DIV > s_target) s_target = N / SAMPLE_DIV;
   const int64_t s_cap = (int64_t)SEL_STAGE * TD / (2 * p.ks);
   if (s_target > s_cap) s_target = s_cap;
   p.stride = s_target > 0 ? N / s_target : 1;
@@ -2204,11 +1933,6 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   p.two_phase = p.stride > 1;
   p.S = p.two_phase ? (N + p.stride - 1) / p.stride : N;
   plan_workers((p.S + TD - 1) / TD, p.gy, D, eb, p.nw, &p.g_s, &p.tpw_s);
-  if (p.tpw_s < sample_min_tpw()) {  // fewer, longer sample workers (query loads amortised)
-    const int64_t st = (p.S + TD - 1) / TD;
-    p.tpw_s = sample_min_tpw();
-    p.g_s = (int)(((st + p.tpw_s - 1) / p.tpw_s + 7) / 8 * 8);
-  }
   p.cap_s = (int64_t)p.tpw_s * TD;
   plan_workers((N + TD - 1) / TD, p.gy, D, eb, p.nw, &p.g_f, &p.tpw_f);
   p.cap_f = (int64_t)p.tpw_f * TD;
@@ -2245,13 +1969,13 @@ static Plan make_plan(int64_t Q, int64_t N, int64_t D, int64_t k, int eb) {
   }
   // LTOP where the GEMM filter does not run and all lists fit one select stage
   p.ls = p.g_f * 2 * p.ks;
-  p.ltop = !p.pp && !p.ppl && ltop_enabled() && Q <= ltop_max_q() && (int64_t)p.ls * LT_M <= SEL_STAGE &&
+  p.ltop = !p.pp && !p.ppl && Q <= ltop_max_q() && (int64_t)p.ls * LT_M <= SEL_STAGE &&
            k <= SEL_NT;
   if (p.ltop) {
     p.two_phase = false;
     // four k-slices: same LDS (ring + a 16 KB exchange) and the same 4 lists per
     // worker and query (the half-lane lists are merged), so g_f / ls stand
-    if (eb == 2 && (D == 768 || D == 1024) && p.nq <= ltop_ks4()) {
+    if (eb == 2 && (D == 768 || D == 1024) && p.nq <= LTOP_KS4_GROUPS) {
       p.ks = 4;
       p.nw = p.nq * 4;
     }
@@ -2519,7 +2243,7 @@ static int scan_topk_impl(int eb, float smul, const void* queries, const void* d
     launch_dense(eb, D, 0, (int)Q, da, st);
     return check_launch("select_dense_kernel(gemm lists)");
   }
-  if (p.two_phase && p.pp && pp_sample_enabled() && p.pp_sG * LT_M <= SEL_STAGE &&
+  if (p.two_phase && p.pp && p.pp_sG * LT_M <= SEL_STAGE &&
       p.pp_sG * LT_M >= 4 * k) {
     // threshold sample on the GEMM kernel: the sample docs (every stride-th row) as B
     // with row stride ldb = stride * D, the 4 largest keys per (256-doc sample tile,

@@ -491,9 +491,12 @@ __global__ void colsum_b_stage2(const float* __restrict__ partial, int nch, int 
 
 // W [R][C] fp32 -> W^T [C][R] bf16 through 32x33 LDS tiles (the nn.Linear-layout
 // operand of GEMMs that consume W as [K][N]).
+// Batched over blockIdx.z: matrix b at x + b * sx, its transpose at y + b * sy.
 __global__ void cast_bf16_t_kernel(const float* __restrict__ x, unsigned short* __restrict__ y,
-                                   int R, int C) {
+                                   int R, int C, int64_t sx = 0, int64_t sy = 0) {
   __shared__ float tile[32][33];
+  x += (int64_t)blockIdx.z * sx;
+  y += (int64_t)blockIdx.z * sy;
   const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
   for (int i = ty; i < 32; i += 8) {
@@ -724,6 +727,20 @@ extern "C" int irc_cast_bf16_t(const float* x, void* y, int64_t R, int64_t C,
   hipLaunchKernelGGL(cast_bf16_t_kernel, dim3((unsigned)((C + 31) / 32), (unsigned)((R + 31) / 32)),
                      dim3(256), 0, as_stream(stream), x, (unsigned short*)y, (int)R, (int)C);
   return check_launch("cast_bf16_t");
+}
+
+// batch matrices [R][C] fp32, sx floats apart -> their transposes [C][R] bf16, sy elements
+// apart: one launch for every layer's copy of one weight (the trainable encoder's dX
+// operands; 48 launches a step became 4).
+extern "C" int irc_cast_bf16_t_batched(const float* x, void* y, int64_t R, int64_t C,
+                                       int64_t batch, int64_t sx, int64_t sy,
+                                       irc_stream_t stream) {
+  IRC_REQUIRE(batch >= 1 && batch < 65536, "cast_bf16_t_batched: batch %lld", (long long)batch);
+  if (R == 0 || C == 0) return IRC_OK;
+  hipLaunchKernelGGL(cast_bf16_t_kernel,
+                     dim3((unsigned)((C + 31) / 32), (unsigned)((R + 31) / 32), (unsigned)batch),
+                     dim3(256), 0, as_stream(stream), x, (unsigned short*)y, (int)R, (int)C, sx, sy);
+  return check_launch("cast_bf16_t_batched");
 }
 
 extern "C" int irc_cast_bf16(const float* x, void* y, int64_t n, irc_stream_t stream) {

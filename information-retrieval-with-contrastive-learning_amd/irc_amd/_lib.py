@@ -107,6 +107,7 @@ SIGNATURES = {
     "irc_enqueue": (I32, [P, P, P, I64, I64, I64, P]),
     "irc_cast_bf16": (I32, [P, P, I64, P]),
     "irc_cast_bf16_t": (I32, [P, P, I64, I64, P]),
+    "irc_cast_bf16_t_batched": (I32, [P, P, I64, I64, I64, I64, I64, P]),
     "irc_colsum": (I32, [I32, P, P, I64, I64, I64, I32, P, P]),
     "irc_colsum_batched_workspace": (I64, [I64, I64, I64]),
     "irc_colsum_batched": (I32, [I32, P, I64, I64, I64, I64, I64, P, I64, I32, P, I64, P]),

@@ -111,6 +111,13 @@ class BertEncoder(nn.Module):
         self._reduce_group = None
         self._reduce_works = []
         self.reduce_bucket_layers = 4
+        # single process: the same buckets' weight gradients on the side stream during the
+        # dX chain (whose N = 768 GEMMs fill three quarters of a wave at B L = 16384), under
+        # a split-K cap of wgrad_max_blocks 256 x 256 blocks (0 = one wave).  --model BERT
+        # step: 19.19-19.43 ms after the chain, 18.95-18.98 overlapped, 18.73-18.76 with the
+        # cap of 128 (three interleaved runs, profiles/r06_d_wgrad_ab.log)
+        self.overlap_wgrad = True
+        self.wgrad_max_blocks = 128
         if init_from is not None:
             self.load_from_bert(init_from)
         else:
@@ -202,19 +209,33 @@ class BertEncoder(nn.Module):
                     (p + "output.dense.weight", (H, c.intermediate_size))]
         return out
 
+    _KINDS = ("attention.self.query.weight", "attention.output.dense.weight",
+              "intermediate.dense.weight", "output.dense.weight")
+
     def shadow_t(self):
-        """{weight name: bf16 W^T} for the dX GEMMs (rebuilt after each update)."""
+        """{weight name: bf16 W^T} for the dX GEMMs (rebuilt after each update): per weight
+        kind one [layers, in, out] buffer, rebuilt by ONE batched transposing cast over the
+        layers' identically laid-out flat slices (48 launches a step -> 4)."""
+        c = self.config
+        nl = c.num_hidden_layers
+        shapes = dict(self._matrices())
         if self._shadow_t is None or next(iter(self._shadow_t.values())).device != \
                 self.flat.device:
-            self._shadow_t = {n: torch.empty((s[1], s[0]), dtype=torch.bfloat16,
-                                             device=self.flat.device)
-                              for n, s in self._matrices()}
+            self._shadow_t, self._shadow_t_kind = {}, {}
+            for kind in self._KINDS:
+                r, cc = shapes[f"encoder.layer.0.{kind}"]
+                buf = torch.empty((nl, cc, r), dtype=torch.bfloat16, device=self.flat.device)
+                self._shadow_t_kind[kind] = buf
+                for l in range(nl):
+                    self._shadow_t[f"encoder.layer.{l}.{kind}"] = buf[l]
             self._shadow_t_ok = False
         if not self._shadow_t_ok:
             flat = self.flat.detach()
-            for n, (r, cc) in self._matrices():
-                o = self.offsets[n]
-                ops.cast_bf16_t_into(flat[o:o + r * cc].view(r, cc), self._shadow_t[n])
+            for kind in self._KINDS:
+                r, cc = shapes[f"encoder.layer.0.{kind}"]
+                o = self.offsets[f"encoder.layer.0.{kind}"]
+                ops.cast_bf16_t_batched(flat[o:], self._shadow_t_kind[kind], r, cc, nl,
+                                        self._layer_stride(kind))
             self._shadow_t_ok = True
         return self._shadow_t
 
@@ -352,12 +373,14 @@ class BertEncoder(nn.Module):
         ds2s = torch.empty((nl, BL, H), dtype=dt, device=dev)
         dm = ops.l2norm_bwd(demb.float().contiguous(), emb, nrm)  # [B, H] fp32
         dy, bcast = dm, L  # top layer: the mean-pool backward folded into LN2's
-        # DP: buckets of reduce_bucket_layers layers, top bucket first; bucket_lo
-        # maps each bucket's lowest layer to its (exclusive) top
+        # DP (and, with overlap_wgrad, one process): buckets of reduce_bucket_layers
+        # layers, top bucket first; bucket_lo maps each bucket's lowest layer to its
+        # (exclusive) top
         reduce_on = self._reduce_group is not None
+        overlap = reduce_on or (self.overlap_wgrad and g.is_cuda)
         nb = max(1, int(self.reduce_bucket_layers))
         bucket_lo = {}
-        if reduce_on:
+        if overlap:
             hi = nl
             while hi > 0:
                 lo = max(0, hi - nb)
@@ -383,10 +406,11 @@ class BertEncoder(nn.Module):
             dqkv = ops.attention_bwd(qkv, mask, ctxs[l], dctx, B, L, H, heads, out=dqkvs[l])
             dy = self._dx_gemm(dqkv, lw["wqkv"], lw.get("wqkvT"), epilogue=ops.EPI_RESID,
                                residual=ds1)
-            if reduce_on and l in bucket_lo and l > 0:
-                self._bucket_wgrad_reduce(l, bucket_lo[l], acts, (dqkvs, ds1s, dus, ds2s))
+            if overlap and l in bucket_lo and l > 0:
+                self._bucket_wgrad_reduce(l, bucket_lo[l], acts, (dqkvs, ds1s, dus, ds2s),
+                                          reduce=reduce_on)
         # layer-batched weight / bias gradients (the layers not yet reduced)
-        lo_end = bucket_lo[0] if reduce_on else nl
+        lo_end = bucket_lo[0] if overlap else nl
         self._wgrad_layers(0, lo_end, acts, (dqkvs, ds1s, dus, ds2s))
         # embeddings: LN backward on the rebuilt fp32 sum, then the table scatter
         e = ops.embed_sum(ids, w["word"], w["pos"], w["type0"])
@@ -398,6 +422,8 @@ class BertEncoder(nn.Module):
                       c.pad_token_id)
         if reduce_on:  # last bucket: embeddings + the bottom layers, on this stream
             self._reduce_async(0, self._layer_start(lo_end))
+        elif overlap and len(bucket_lo) > 1:  # the side stream's buckets, before any reader
+            torch.cuda.current_stream(dev).wait_stream(side_stream(dev, "grad_reduce"))
 
     # ---- data-parallel gradient all-reduce, bucketed and overlapped -------------
     def set_grad_reduce(self, group):
@@ -429,7 +455,7 @@ class BertEncoder(nn.Module):
                                                   op=dist.ReduceOp.SUM,
                                                   group=self._reduce_group, async_op=True))
 
-    def _wgrad_layers(self, lo, hi, acts, grads):
+    def _wgrad_layers(self, lo, hi, acts, grads, max_blocks=0):
         xs, ctxs, as_, gs = acts
         dqkvs, ds1s, dus, ds2s = grads
         if hi <= lo:
@@ -441,19 +467,22 @@ class BertEncoder(nn.Module):
                                     (dus, as_, "intermediate.dense.weight",
                                      "intermediate.dense.bias"),
                                     (ds2s, gs, "output.dense.weight", "output.dense.bias")):
-            self._wgrad_batched(dY[lo:hi], X[lo:hi], wname, bname, first=lo)
+            self._wgrad_batched(dY[lo:hi], X[lo:hi], wname, bname, first=lo,
+                                max_blocks=max_blocks)
 
-    def _bucket_wgrad_reduce(self, lo, hi, acts, grads):
-        """Layers [lo, hi): weight gradients + all-reduce of their flat slice (plus
-        everything above it for the top bucket) on the "grad_reduce" side stream."""
+    def _bucket_wgrad_reduce(self, lo, hi, acts, grads, reduce=True):
+        """Layers [lo, hi): weight gradients (+ with reduce, the all-reduce of their flat
+        slice, plus everything above it for the top bucket) on the "grad_reduce" side
+        stream."""
         cur = torch.cuda.current_stream(self.flat_grad.device)
         side = side_stream(self.flat_grad.device, "grad_reduce")
         side.wait_stream(cur)
         with torch.cuda.stream(side):
-            self._wgrad_layers(lo, hi, acts, grads)
-            top = hi >= self.config.num_hidden_layers
-            self._reduce_async(self._layer_start(lo),
-                               self.numel_flat if top else self._layer_start(hi))
+            self._wgrad_layers(lo, hi, acts, grads, self.wgrad_max_blocks)
+            if reduce:
+                top = hi >= self.config.num_hidden_layers
+                self._reduce_async(self._layer_start(lo),
+                                   self.numel_flat if top else self._layer_start(hi))
         for t in list(acts) + list(grads):
             t.record_stream(side)
         # no join here: the dX chain goes on; wait_grad_reduce() joins through the
@@ -469,7 +498,7 @@ class BertEncoder(nn.Module):
                 self.offsets[f"encoder.layer.{l - 1}.{name}"] == st
         return st
 
-    def _wgrad_batched(self, dY, X, wname, bname, first=0):
+    def _wgrad_batched(self, dY, X, wname, bname, first=0, max_blocks=0):
         """dW[l] += dY[l]^T X[l] and db[l] += colsum(dY[l]) for the layers
         first .. first + len(dY) - 1."""
         g = self.flat_grad.detach()
@@ -480,7 +509,7 @@ class BertEncoder(nn.Module):
         sw, sb = self._layer_stride(wname), self._layer_stride(bname)
         ops.gemm_strided(dY, X, g[ow:], M=out_n, N=in_n, K=BL, batch=nl, lda=out_n,
                          sA=BL * out_n, ldb=in_n, sB=BL * in_n, ldc=in_n, sC=sw, trans_a=True,
-                         b_is_nk=False, accumulate=True)
+                         b_is_nk=False, accumulate=True, max_blocks=max_blocks)
         ops.colsum_batched(dY, g[ob:], sb, accumulate=True)
 
     def encode(self, input_ids, attention_mask):

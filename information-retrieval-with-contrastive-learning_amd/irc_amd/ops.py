@@ -625,6 +625,15 @@ def cast_bf16_t_into(x, y):
     return y
 
 
+def cast_bf16_t_batched(x_first, y, R, C, batch, sx):
+    """y bf16 [batch, C, R] <- the transposes of `batch` fp32 [R, C] matrices that start at
+    x_first's storage and lie sx floats apart (irc_cast_bf16_t_batched)."""
+    require_hip(x_first, y)
+    _lib.call("irc_cast_bf16_t_batched", ptr(x_first), ptr(y), R, C, batch, sx, C * R,
+              stream_ptr(y.device))
+    return y
+
+
 def cast_bf16_into(x, y):
     require_hip(x, y)
     _lib.call("irc_cast_bf16", ptr(x), ptr(y), x.numel(), stream_ptr(x.device))

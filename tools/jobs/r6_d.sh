@@ -6,6 +6,11 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r6_d
 mkdir -p $O
 export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+  tests/test_bert_train_gpu.py tests/test_dist_gpu.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 400 python tools/bert_wgrad_ab.py --steps 10 --reps 3 --cap 0 128 > $O/wgrad_ab.log 2>&1 || { tail $O/wgrad_ab.log; exit 1; }
+cat $O/wgrad_ab.log
 timeout -k 10 300 python bench.py --part bert --steps 10 --warmup 3 --no-cpu-baseline > $O/bench_bert.log 2>&1 || { tail $O/bench_bert.log; exit 1; }
 tail -1 $O/bench_bert.log | cut -c1-600
 export TMPDIR=/tmp
