@@ -26,6 +26,11 @@
 
 #include <atomic>
 
+// Grouped output-tile order of the GEMM kernels' tiles (see gemm_group_m; 0 = row-major).
+#ifndef IRC_GEMM_GROUP_M
+#define IRC_GEMM_GROUP_M 0
+#endif
+
 namespace irc {
 namespace gemm {
 
@@ -1106,7 +1111,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
   int tm, tn;
-  grouped_tile(bid, tiles_m, tiles_n, 0, tm, tn);
+  grouped_tile(bid, tiles_m, tiles_n, IRC_GEMM_GROUP_M, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1371,10 +1376,11 @@ static int by_layout(int la, int lb, int epi, const Args& g, int batch, int spli
 
 using namespace irc;
 
-// Grouped output-tile order of the 256-row GEMM kernels (row tiles per group): 0 =
-// row-major; grouping measured no faster (profiles/r02_group_i_*).  The kernels keep the
-// grouped form (grouped_tile) for callers that set PArgs / Args group_m themselves.
-static int gemm_group_m() { return 0; }
+// Grouped output-tile order of the 256-row GEMM kernels (row tiles per group, rows walked
+// fastest inside a group; 0 = row-major): the tiles an XCD has in flight then share a few
+// column tiles of B, which stays in that XCD's 4 MB L2 across the group, instead of every
+// wave of row tiles streaming all of B again (FFN1 / QKV: W is 4.7-8 MB).
+static int gemm_group_m() { return IRC_GEMM_GROUP_M; }
 
 // IRC_GEMM_PP=0 disables the ping-pong path (A/B experiments; read once).
 static bool pp_enabled() {

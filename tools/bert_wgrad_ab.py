@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cap", type=int, nargs="*", default=[0])
+    ap.add_argument("--bucket", type=int, nargs="*", default=[4],
+                    help="layers per weight-gradient bucket (reduce_bucket_layers)")
     a = ap.parse_args()
     from src.model import build_model, get_optimizer
     from src.train import TrainState
@@ -39,8 +41,8 @@ def main():
     ids, mask = ids.to(dev), mask.to(dev)
     enc = model.encoder_q
 
-    def run(overlap, cap):
-        enc.overlap_wgrad, enc.wgrad_max_blocks = overlap, cap
+    def run(overlap, cap, bucket=4):
+        enc.overlap_wgrad, enc.wgrad_max_blocks, enc.reduce_bucket_layers = overlap, cap, bucket
         for _ in range(3):
             st.micro_batch(bench.TRAIN_B, lambda: model.forward_ids(ids, mask, bench.TRAIN_B),
                            sync_loss=False)
@@ -56,10 +58,11 @@ def main():
         dt = run(False, 0)
         print(f"rep {r} overlap=off       {dt * 1e3:7.2f} ms/step {bench.TRAIN_B / dt:8.0f} pairs/s",
               flush=True)
-        for cap in a.cap:
-            dt = run(True, cap)
-            print(f"rep {r} overlap=on cap={cap:<4d}{dt * 1e3:7.2f} ms/step "
-                  f"{bench.TRAIN_B / dt:8.0f} pairs/s", flush=True)
+        for bucket in a.bucket:
+            for cap in a.cap:
+                dt = run(True, cap, bucket)
+                print(f"rep {r} overlap=on bucket={bucket} cap={cap:<4d}{dt * 1e3:7.2f} ms/step "
+                      f"{bench.TRAIN_B / dt:8.0f} pairs/s", flush=True)
 
 
 if __name__ == "__main__":
