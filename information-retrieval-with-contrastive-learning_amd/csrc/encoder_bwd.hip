@@ -413,6 +413,21 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const T* __restrict__ qkv
   }
 }
 
+// Rows (r, r + 1) of column c, held by this lane as v0 / v1 (32x32 accumulator elements e,
+// e + 1 for even e), leave as ONE 4-byte store: the DPP neighbour swap (quad_perm
+// [1,0,3,2]: lane ^ 1 holds column c ^ 1) gives the even lane columns (c, c + 1) of row r and
+// the odd lane those of row r + 1 -- half the store instructions of per-element 2-byte
+// stores, same bytes.  row_r points at row r's element of column 0 of the lane's column
+// block; ld is the row stride.
+__device__ __forceinline__ void store_row_pair(unsigned short* row_r, int64_t ld, int c, float v0,
+                                               float v1, int lane) {
+  const uint32_t w = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+  const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false);
+  const int odd = lane & 1;
+  const uint32_t v = odd ? ((x >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (x << 16));
+  *reinterpret_cast<uint32_t*>(row_r + odd * ld + c - odd) = v;
+}
+
 // MFMA (bf16, DH = 64, L = 32*NJ): one workgroup of NJ waves per (sequence, head).
 // The 32x32x16 C layout of X^T (rows j, lanes = columns i) is, with the k order
 // permuted, the A operand of X (rows i, k over j) -- the forward's P.V trick --
@@ -561,9 +576,10 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
+      for (int e = 0; e < 16; e += 2) {  // rows ii, ii + 1 (e even): one paired store
         const int ii = 32 * ib + (e & 3) + 8 * (e >> 2) + 4 * h;
-        gb[(int64_t)ii * ld3 + 32 * db + r32] = f32_to_bf16(o[db][e] * scale);
+        store_row_pair(gb + (int64_t)ii * ld3, ld3, 32 * db + r32, o[db][e] * scale,
+                       o[db][e + 1] * scale, lane);
       }
   }
   __syncthreads();
@@ -635,10 +651,12 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
+      for (int e = 0; e < 16; e += 2) {
         const int jj = 32 * jb + (e & 3) + 8 * (e >> 2) + 4 * h;
-        gb[(int64_t)jj * ld3 + H + 32 * db + r32] = f32_to_bf16(dk[db][e] * scale);
-        gb[(int64_t)jj * ld3 + 2 * H + 32 * db + r32] = f32_to_bf16(dv[db][e]);
+        store_row_pair(gb + (int64_t)jj * ld3 + H, ld3, 32 * db + r32, dk[db][e] * scale,
+                       dk[db][e + 1] * scale, lane);
+        store_row_pair(gb + (int64_t)jj * ld3 + 2 * H, ld3, 32 * db + r32, dv[db][e],
+                       dv[db][e + 1], lane);
       }
   }
 }

@@ -1379,8 +1379,17 @@ using namespace irc;
 // Grouped output-tile order of the 256-row GEMM kernels (row tiles per group, rows walked
 // fastest inside a group; 0 = row-major): the tiles an XCD has in flight then share a few
 // column tiles of B, which stays in that XCD's 4 MB L2 across the group, instead of every
-// wave of row tiles streaming all of B again (FFN1 / QKV: W is 4.7-8 MB).
-static int gemm_group_m() { return IRC_GEMM_GROUP_M; }
+// wave of row tiles streaming all of B again.  Taken where a launch has at least 12 column
+// tiles of its kernel's width bn (BERT-large FFN1, N = 4096, whose 8 MB weight streamed once per wave of row
+// tiles: 606 MB read per launch against 75 MB algorithmic, profiles/r06_g_pmc.log).  With 8
+// rows per group for every launch: C4 step 11.17-11.20k -> 11.31-11.34k pairs/s and C4 GEMM
+// traffic 460 -> 407 MB per launch, C2 step 31.87-31.94k -> 31.81-31.88k (its widest launch
+// has 8 column tiles; profiles/r06_h_*), hence the threshold.  IRC_GEMM_GROUP_M (build
+// flag) forces one value for every launch.
+static int gemm_group_m(int64_t N, int64_t bn) {
+  if (IRC_GEMM_GROUP_M != 0) return IRC_GEMM_GROUP_M;
+  return (N + bn - 1) / bn >= 12 ? 8 : 0;
+}
 
 // IRC_GEMM_PP=0 disables the ping-pong path (A/B experiments; read once).
 static bool pp_enabled() {
@@ -1454,7 +1463,7 @@ extern "C" int irc_gemm_ln(int epilogue, int64_t M, int64_t N, int64_t K, const 
   hipStream_t st = as_stream(stream);
   const double flops = 2.0 * M * N * K;
   Args g{A, B, C, bias, R, (int)M, (int)N, (int)K, lda, ldb, ldc, ldr, 0, 0, 0, 0, 0, 1.0f, 0, 1, 1,
-         1, 0, nullptr, gemm_group_m()};
+         1, 0, nullptr, gemm_group_m(N, 384)};
   const int wnb = big_wnb(g, 1, ROW, ROW);
   // the 256 x 256 kernel unless the big-tile one is preferred and applies (small shapes
   // that neither kernel's heuristics take also run 256 x 256)
@@ -1462,7 +1471,7 @@ extern "C" int irc_gemm_ln(int epilogue, int64_t M, int64_t N, int64_t K, const 
     gpp::PArgs pa{static_cast<const unsigned short*>(A), static_cast<const unsigned short*>(B), C,
                   bias, R, nullptr, (int)M, (int)N, (int)K, (int)K, lda, ldb, ldc, ldr, 0, 0, 0, 0,
                   0, 1.0f, 0, 1};
-    pa.group_m = gemm_group_m();
+    pa.group_m = gemm_group_m(N, 256);
     ln.nt_out = (int)((N + 255) / 256);
     pa.ln = ln;
     if (stats_nt_out) *stats_nt_out = ln.nt_out;
@@ -1573,7 +1582,7 @@ extern "C" int irc_gemm_ex(int in_dtype, int out_dtype, int a_layout, int b_layo
   gemm::Args g{A, B, C, bias, R, (int)M, (int)N, (int)K, lda, ldb, ldc, ldr,
                strideA, strideB, strideC, strideR, strideBias, alpha, accumulate, vec_a, vec_b,
                vec_c, 0, splits > 1 ? static_cast<float*>(workspace) : nullptr,
-               gemm_group_m()};
+               gemm_group_m(N, 384)};
   hipStream_t st = as_stream(stream);
   const int nb = (int)batch;
   if (in_dtype == 0 && pp_enabled()) {
@@ -1587,7 +1596,7 @@ extern "C" int irc_gemm_ex(int in_dtype, int out_dtype, int a_layout, int b_layo
                     (int)K, sp > 1 ? (int)(((K + sp - 1) / sp + 63) / 64 * 64) : (int)K,
                     lda, ldb, ldc, ldr, strideA, strideB, strideC, strideR, strideBias, alpha,
                     accumulate, vec_c};
-      pa.group_m = gemm_group_m();
+      pa.group_m = gemm_group_m(N, 256);
       prof_begin(st);
       gpp::run(out_dtype == 1, a_layout, b_layout, epilogue, pa, batch, sp, st, grid_cap(max_blocks));
       if (sp > 1) {

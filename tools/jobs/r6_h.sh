@@ -8,6 +8,10 @@ O=$R/gpurun_out/r6_h
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 V=$R/information-retrieval-with-contrastive-learning_amd/irc_amd/lib/variants
+# the attention backward's paired 4-byte stores: the whole-encoder gradient and attention tests
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+  tests/test_bert_train_gpu.py tests/test_attention_gpu.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
 for rep in 1 2; do
   for v in release group8 group4; do
     if [ $v = release ]; then unset IRC_LIB_PATH; else export IRC_LIB_PATH=$V/$v.so; fi
