@@ -65,7 +65,8 @@ STRONG_CHUNKS = 8  # the corpus is drawn in n_total / 8 chunks, each from its ow
 # the docs (and the top-k) are the same at 1, 2, 4 and 8 ranks
 PP_MIN_Q = 192  # irc_scan_topk's filter runs on the ping-pong GEMM kernel from this Q
 SCAN_DEPTH = 3  # query batches in flight in the retrieval legs (search_many; 2 -> 3: C2 +13%,
-# profiles/r05_zd_scan_depth.txt)
+# profiles/r05_zd_scan_depth.txt; 4 on the one-call native loop: 3.41-3.59M against
+# 3.97-3.99M queries/s at 3, interleaved on one box, profiles/r06_m/)
 
 
 def _cpu_model():
@@ -450,7 +451,7 @@ def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16", nq=
     batches = [myq] * reps
     for _ in range(max(args.warmup, 3)):
         index.search(myq, SCAN_K, equal_counts=True)
-    index.search_many(batches[:4], SCAN_K, depth=SCAN_DEPTH, equal_counts=True)
+    index.search_many(batches[:4], SCAN_K, depth=args.scan_depth, equal_counts=True)
     torch.cuda.synchronize()
     # serial calls first: the single-call latency (whole irc_scan_topk + collectives);
     # the filter kernel's HIP-event durations (roofline) come from these calls, where
@@ -469,7 +470,7 @@ def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16", nq=
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    index.search_many(batches, SCAN_K, depth=SCAN_DEPTH, equal_counts=True)
+    index.search_many(batches, SCAN_K, depth=args.scan_depth, equal_counts=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -503,7 +504,7 @@ def run_scan(args, rank, world, dev, n_per_gpu=SCAN_N_PER_GPU, dtype="bf16", nq=
                                   "algorithmic bytes; frac/achieved are the filter kernel's"})
     return {
         "value": nq * reps / dt, "unit": "queries/s", "batches_timed": reps,
-        "ms_per_batch": dt * 1e3 / reps, "dtype": dtype, "batches_in_flight": SCAN_DEPTH,
+        "ms_per_batch": dt * 1e3 / reps, "dtype": dtype, "batches_in_flight": args.scan_depth,
         "call_level": {
             "note": "whole search (sample pass, threshold select, filter, final select, "
                     "collectives) vs HBM peak on the call's algorithmic bytes",
@@ -553,7 +554,7 @@ def run_scan_strong(args, rank, world, dev, n_total, dtype, nq, dim, k=SCAN_K, m
     """Strong scaling of the sharded scan: the fixed corpus of n_total
     docs split n_total / world per rank (ShardedDenseIndex), the same nq global queries
     per batch (each rank contributes nq / world and receives the global top-k of all
-    nq).  Reports global queries/s (serial calls and `SCAN_DEPTH` batches in flight),
+    nq).  Reports global queries/s (serial calls and `--scan-depth` batches in flight),
     the ranks and backend the collectives ran on, and the three steps of one search
     timed apart -- query all-gather, local scan, per-shard list all-gather + merge --
     each max over ranks.  make_index(rank, world, dev) -> index lets the CPU tests
@@ -588,8 +589,8 @@ def run_scan_strong(args, rank, world, dev, n_total, dtype, nq, dim, k=SCAN_K, m
     _sync(dev)
     t_call = timed(search, reps)
     if dev.type == "cuda":
-        index.search_many([myq] * 4, k, depth=SCAN_DEPTH, equal_counts=equal)
-        t_pipe = timed(lambda: index.search_many([myq] * reps, k, depth=SCAN_DEPTH,
+        index.search_many([myq] * 4, k, depth=args.scan_depth, equal_counts=equal)
+        t_pipe = timed(lambda: index.search_many([myq] * reps, k, depth=args.scan_depth,
                                                  equal_counts=equal), 1) / reps
     else:
         t_pipe = t_call
@@ -610,7 +611,7 @@ def run_scan_strong(args, rank, world, dev, n_total, dtype, nq, dim, k=SCAN_K, m
     return {
         "value": nq / t_pipe, "unit": "queries/s", "scaling": "strong",
         "serial_queries_per_s": nq / t_call, "serial_us_per_call": t_call * 1e6,
-        "pipelined_us_per_batch": t_pipe * 1e6, "batches_in_flight": SCAN_DEPTH,
+        "pipelined_us_per_batch": t_pipe * 1e6, "batches_in_flight": args.scan_depth,
         "phases": phases,
         "ranks": world, "backend": dist.get_backend() if world > 1 else None,
         "docs_total": n_total, "docs_per_rank": per_rank, "queries": nq,
@@ -830,6 +831,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--scan-depth", type=int, default=SCAN_DEPTH,
+                    help="query batches in flight in the retrieval legs")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:

@@ -57,6 +57,20 @@ int irc_scan_topk(const void* queries, const void* docs, int64_t Q, int64_t N, i
                   int64_t k, int64_t doc_offset, void* workspace, int64_t workspace_bytes,
                   float* out_score, int64_t* out_idx, irc_stream_t stream);
 
+/* `batches` bf16 query batches of one shape [Q][D] (queries[b]) against one shard, with
+ * `depth` (<= 16) of them in flight: batch b runs as irc_scan_topk on streams[b % depth]
+ * with workspaces[b % depth] (each of workspace_bytes, irc_scan_topk_workspace) and writes
+ * rows [b Q, (b + 1) Q) of out_score / out_idx ([batches Q][k]).  Every stream first waits
+ * for the work queued on `origin`, and `origin` then waits for every stream, so the
+ * results are ready in `origin`'s order.  The serving loop of search_many in one call (the
+ * reference's predict() takes its claims batch by batch, src/evaluation.py:98-112);
+ * results identical to the per-batch calls. */
+int irc_scan_topk_many(const void* const* queries, int64_t batches, const void* docs, int64_t Q,
+                       int64_t N, int64_t D, int64_t k, int64_t doc_offset,
+                       void* const* workspaces, int64_t workspace_bytes, int64_t depth,
+                       float* out_score, int64_t* out_idx, const irc_stream_t* streams,
+                       irc_stream_t origin);
+
 /* Rescan statistics of the single-pass scan (Q <= 64): out[0] = queries whose
  * exact select had to rescan a worker's docs (a truncated 4-key list could hide
  * a winner), out[1] = workers rescanned, since the last reset.  out is a HOST
@@ -206,12 +220,14 @@ int irc_layernorm(int dtype, const void* x, void* y, const float* gamma, const f
 int irc_attention(int dtype, const void* qkv, const int64_t* mask, void* ctx, int64_t B,
                   int64_t L, int64_t H, int64_t heads, irc_stream_t stream);
 /* QKV projection + self-attention in one launch (replaces irc_gemm(QKV) + irc_attention
- * for the bf16 frozen encoder at L = 64, head dim 64, H % 128 == 0): ctx [M = B*64][H]
+ * for the bf16 frozen encoder at L <= 128, head dim 64, H % 128 == 0): ctx [M = B*L][H]
  * (row stride ldc) = attention(x . Wqkv^T + b) with the same arithmetic as the unfused
  * pair.  wqkv_perm / bias_perm: Wqkv [3H][H] and its bias with the rows permuted so that
  * each 384-row block n holds the Q, K, V rows of heads 2n and 2n + 1 (64 each, in that
  * order) -- the QKV activation never leaves the CU.  x [M][H] (row stride ldx), mask
- * [M / 64][64] int64 (nonzero = visible) or NULL. */
+ * [M / L][L] int64 (nonzero = visible) or NULL.  A 256-row tile holds 4 (L <= 64) or 2
+ * sequences in fixed slots, or 256 / L packed sequences where that takes fewer waves of
+ * tiles over the device's CUs. */
 int irc_qkv_attention(int64_t M, int64_t H, int64_t heads, int64_t L, const void* x, int64_t ldx,
                       const void* wqkv_perm, const float* bias_perm, const int64_t* mask,
                       void* ctx, int64_t ldc, irc_stream_t stream);

@@ -24,6 +24,7 @@
 // in that XCD's L2).
 #include "gemm_pp.h"
 
+#include <algorithm>
 #include <atomic>
 
 // Grouped output-tile order of the GEMM kernels' tiles (see gemm_group_m; 0 = row-major).
@@ -1091,18 +1092,31 @@ struct QaArgs {
   int L;                    // sequence length, 1..64 (one 64-row slot per sequence)
 };
 
+//
+// SL = 0, the packed form (any L <= 128; launched where it takes fewer waves of tiles, see
+// irc_qkv_attention): a 256-row tile holds 256 / L whole sequences as contiguous rows (L =
+// 80: three, where 128-row slots take two), and the epilogue stages one head at a time for all
+// 256 rows -- T [256][264]: that head's Q | K | V columns, 135 KB -- because a sequence now
+// straddles the 128-row halves.  Per head the 8 waves take (sequence, 32 queries) items in
+// turn, with the same per-item arithmetic, so the context is again bit-identical to the
+// unfused form.  Key and query rows past the tile's 256 (a last sequence's last key block)
+// are read from row 255: finite values whose probabilities the -3e30 past-L bias zeroes,
+// and whose queries are not stored.
 template <int SL>
 __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
+  constexpr bool PACK = SL == 0;
   constexpr int WNB = 3, BM = big::BM, BN = 128 * WNB, TP = BN + 8;
-  constexpr int SPT = BM / SL;         // sequences per tile: 4 (SL = 64) or 2 (SL = 128)
-  constexpr int SH = SL == 64 ? 6 : 7;
-  constexpr int NJM = SL / 32;         // key blocks of 32 per sequence, at most
+  constexpr int SLX = PACK ? 128 : SL;  // key rows of a sequence, at most
+  constexpr int SH = SLX == 64 ? 6 : 7;
+  constexpr int NJM = SLX / 32;         // key blocks of 32 per sequence, at most
   __shared__ __attribute__((aligned(1024))) char lds[2 * (BM + BN) * big::ROW_BYTES];
-  static_assert(128 * TP * 2 + 8 * SL * 4 <= 2 * (BM + BN) * big::ROW_BYTES,
+  static_assert(128 * TP * 2 + 8 * SLX * 4 <= 2 * (BM + BN) * big::ROW_BYTES,
                 "staged half and mask biases fit the LDS");
   const int nseq = g.M / g.L;
-  const int ls = g.L == SL ? 0 : g.L;  // 0: contiguous rows (slots are the sequences)
-  const int tiles_m = (nseq + SPT - 1) / SPT;
+  // sequences per tile: 4 (SL = 64), 2 (SL = 128) or 256 / L (packed)
+  const int spt = PACK ? BM / g.L : BM / SLX;
+  const int ls = PACK || g.L == SL ? 0 : g.L;  // 0: contiguous rows
+  const int tiles_m = (nseq + spt - 1) / spt;
   const int tiles_n = 3 * g.H / BN;
   const int ntiles = tiles_m * tiles_n;
   int bid = blockIdx.x;
@@ -1112,7 +1126,8 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
   }
   int tm, tn;
   grouped_tile(bid, tiles_m, tiles_n, IRC_GEMM_GROUP_M, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
+  // packed: first token row of the tile's first sequence; slots: first slot row
+  const int m0 = PACK ? tm * spt * g.L : tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;
@@ -1149,6 +1164,133 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
   }
   const int h = lane >> 5, r32 = lane & 31;
   const int nj = (g.L + 31) / 32;  // key (and query) blocks of 32 of a sequence
+  if constexpr (PACK) {
+    constexpr int TQ = 264;  // 192 columns + pad: a 132-dword row stride, as TP's 196 = 4 mod 64
+    static_assert(BM * TQ * 2 + 8 * 128 * 4 <= 2 * (BM + BN) * big::ROW_BYTES,
+                  "staged head and mask biases fit the LDS");
+    unsigned short* Tq = reinterpret_cast<unsigned short*>(lds);  // [256][TQ] one head
+    float* mb = reinterpret_cast<float*>(lds + BM * TQ * 2) + 128 * wave;
+    const int odd = lane & 1;
+    const int nsq = min(spt, nseq - tm * spt);  // sequences in this tile
+    const int nit = nsq * nj;                   // (sequence, query block) items per head
+#pragma unroll
+    for (int hd = 0; hd < 2; ++hd) {
+      // this head's columns of every wave's accumulators -> Tq (Q at 0, K at 64, V at 128);
+      // tile column b of a 16-column group: part b >> 7, head (b >> 6) & 1
+#pragma unroll
+      for (int j = 0; j < 2 * WNB; ++j) {
+        const int b = wn * 32 * WNB + 16 * j;
+        if (((b >> 6) & 1) != hd) continue;
+        const int tc = 64 * (b >> 7) + (b & 63) + (lane & 14);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int e2 = 0; e2 < 2; ++e2) {
+            const uint32_t w = pk[i][j][e2];
+            const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false);
+            const uint32_t v = odd ? ((x >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (x << 16));
+            const int rl = 128 * wm + 16 * i + 4 * (lane >> 4) + 2 * e2 + odd;
+            *reinterpret_cast<uint32_t*>(&Tq[rl * TQ + tc]) = v;
+          }
+      }
+      __syncthreads();  // the head is staged
+      for (int it = wave; it < nit; it += 8) {
+        const int s = it / nj, ib = it - s * nj;
+        const int t0 = s * g.L;                  // the sequence's first tile row
+        const int r0 = (tm * spt + s) * g.L;     // its first token
+#pragma unroll
+        for (int j = lane; j < 128; j += 64)
+          mb[j] = j >= g.L ? -3e30f
+                           : ((g.mask == nullptr || g.mask[r0 + j] != 0) ? 0.f : -1e30f);
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned short* Q = Tq;
+        const unsigned short* Kp = Tq + 64;
+        const unsigned short* V = Tq + 128;
+        unsigned short* out = g.ctx + (int64_t)r0 * g.ldc + (2 * tn + hd) * 64;
+        bf16x8 qf[4];
+        const int qr = min(t0 + 32 * ib + r32, BM - 1);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          qf[kk] = *reinterpret_cast<const bf16x8*>(Q + qr * TQ + 16 * kk + 8 * h);
+        f32x16 sc[NJM];
+#pragma unroll
+        for (int jb = 0; jb < NJM; ++jb) {
+          sc[jb] = (f32x16)0.f;
+          if (jb < nj) {
+            const int kr = min(t0 + 32 * jb + r32, BM - 1);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+              const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kp + kr * TQ + 16 * kk + 8 * h);
+              sc[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[jb], 0, 0, 0);
+            }
+          }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int jb = 0; jb < NJM; ++jb) {
+          if (jb >= nj) break;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4 bias = *reinterpret_cast<const f32x4*>(&mb[32 * jb + 8 * q + 4 * h]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = sc[jb][4 * q + r] * g.scale + bias[r];
+              sc[jb][4 * q + r] = v;
+              mx = fmaxf(mx, v);
+            }
+          }
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        float sum = 0.f;
+#pragma unroll
+        for (int jb = 0; jb < NJM; ++jb) {
+          if (jb >= nj) break;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float p = __expf(sc[jb][e] - mx);
+            sc[jb][e] = p;
+            sum += p;
+          }
+        }
+        sum += __shfl_xor(sum, 32, 64);
+        const float inv = 1.f / sum;
+        f32x16 o[2] = {(f32x16)0.f, (f32x16)0.f};
+#pragma unroll
+        for (int jb = 0; jb < NJM; ++jb) {
+          if (jb >= nj) break;
+#pragma unroll
+          for (int k2 = 0; k2 < 2; ++k2) {
+            bf16x8 pa;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) pa[t] = (__bf16)(sc[jb][8 * k2 + t] * inv);
+            const int j0 = 32 * jb + 16 * k2 + 4 * h;
+            const int i16 = lane & 15;
+            const int vr = t0 + j0 + (i16 >> 2);
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+              const int vc = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+              const v4s lo = ds_tr16(reinterpret_cast<const char*>(V + min(vr, BM - 1) * TQ + vc));
+              const v4s hi =
+                  ds_tr16(reinterpret_cast<const char*>(V + min(vr + 8, BM - 1) * TQ + vc));
+              const v4s both[2] = {lo, hi};
+              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(bf16x8, both),
+                                                              o[db], 0, 0, 0);
+            }
+          }
+        }
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int i = 32 * ib + (e & 3) + 8 * (e >> 2) + 4 * h;
+            if (i < g.L) out[(int64_t)i * g.ldc + 32 * db + r32] = f32_to_bf16(o[db][e]);
+          }
+      }
+      if (hd == 0) __syncthreads();  // every wave is done with head 0's Tq
+    }
+    return;
+  }
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     if (wm == hf) {  // this half's accumulators -> T [128][TP]
@@ -1176,7 +1318,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
     // wave = (query block wave >> 1, head wave & 1)
     const int sl = SL == 64 ? wn >> 1 : 0, hh = SL == 64 ? wn & 1 : wave & 1;
     const int ib = SL == 64 ? wm : wave >> 1;
-    const int seq = SPT * tm + (SL == 64 ? 2 * hf + sl : hf);
+    const int seq = spt * tm + (SL == 64 ? 2 * hf + sl : hf);
     const int r0 = seq * g.L;  // first token of the sequence
     if (seq < nseq && ib < nj) {
 #pragma unroll
@@ -1384,7 +1526,7 @@ using namespace irc;
 // tiles: 606 MB read per launch against 75 MB algorithmic, profiles/r06_g_pmc.log).  With 8
 // rows per group for every launch: C4 step 11.17-11.20k -> 11.31-11.34k pairs/s and C4 GEMM
 // traffic 460 -> 407 MB per launch, C2 step 31.87-31.94k -> 31.81-31.88k (its widest launch
-// has 8 column tiles; profiles/r06_h_*), hence the threshold.  IRC_GEMM_GROUP_M (build
+// has 8 column tiles; profiles/r06_h/), hence the threshold.  IRC_GEMM_GROUP_M (build
 // flag) forces one value for every launch.
 static int gemm_group_m(int64_t N, int64_t bn) {
   if (IRC_GEMM_GROUP_M != 0) return IRC_GEMM_GROUP_M;
@@ -1509,10 +1651,24 @@ extern "C" int irc_qkv_attention(int64_t M, int64_t H, int64_t heads, int64_t L,
            bias_perm, mask, static_cast<unsigned short*>(ctx), (int)M, (int)H, (int)H, ldx, ldc,
            0.125f, (int)L};
   hipStream_t st = as_stream(stream);
-  const int spt = L <= 64 ? 4 : 2;  // sequences per 256-row tile (64- or 128-row slots)
-  const int tiles = (int)((M / L + spt - 1) / spt) * (int)(3 * H / 384);
+  // Sequences per 256-row tile: 64- or 128-row slots, or packed (256 / L) where that takes
+  // fewer waves of tiles over the CUs.  Packed tiles pay an attention round per 8 (sequence,
+  // query block) items of a head (~5 us a tile each), so at equal waves the slots stay.
+  // B = 512 (a C2 / C4 micro-batch), fused us per layer, slots -> packed where it applies
+  // (profiles/r06_k/): L = 16: 116-122 -> 49-50, L = 32: 75-76 (packed in both), L = 34:
+  // 115 -> 91-92, L = 72: 236-239 -> 222-223, L = 85: 238-239 -> 225-226; L = 48 keeps slots
+  // (120-122 against 130-131 packed: both 3 waves).
+  const int64_t nseq = M / L, tiles_n = 3 * H / 384;
+  const int slot = L <= 64 ? 4 : 2;
+  const int64_t ncu = std::max(1, gpp::cu_count() > 0 ? gpp::cu_count() : 256);
+  const auto waves = [&](int64_t s) { return ((nseq + s - 1) / s * tiles_n + ncu - 1) / ncu; };
+  const bool packed = 256 / L > slot && waves(256 / L) < waves(slot);
+  const int spt = packed ? (int)(256 / L) : slot;
+  const int tiles = (int)(((nseq + spt - 1) / spt) * tiles_n);
   prof_begin(st);
-  if (L <= 64)
+  if (packed)
+    hipLaunchKernelGGL(qkv_attn_kernel<0>, dim3(tiles), dim3(big::NT), 0, st, a);
+  else if (L <= 64)
     hipLaunchKernelGGL(qkv_attn_kernel<64>, dim3(tiles), dim3(big::NT), 0, st, a);
   else
     hipLaunchKernelGGL(qkv_attn_kernel<128>, dim3(tiles), dim3(big::NT), 0, st, a);

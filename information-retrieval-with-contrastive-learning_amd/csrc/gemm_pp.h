@@ -90,6 +90,8 @@ int splits_for(int out_f32, int epi, int64_t M, int64_t N, int64_t K, int64_t ba
                int64_t budget = 256);
 // CUs of the current device (256 when the query fails)
 int device_cu_count();
+// compute units of the current device (cached per device; 0 if unknown)
+int cu_count();
 bool qualifies(int la, int lb, int64_t M, int64_t N, int64_t K, const void* A, int64_t lda,
                int64_t sA, const void* B, int64_t ldb, int64_t sB, int64_t batch, int splits);
 // max_grid > 0: at most that many workgroups -- a launch of more tiles runs as a static

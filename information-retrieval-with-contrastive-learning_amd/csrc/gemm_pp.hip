@@ -1133,7 +1133,7 @@ static std::atomic<int>& pers_mode() {
 }
 static bool pers_enabled() { return pers_mode().load(std::memory_order_relaxed) != 0; }
 
-static int cu_count() {
+int cu_count() {
   static int cus[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;

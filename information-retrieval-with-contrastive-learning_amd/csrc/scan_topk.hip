@@ -2386,6 +2386,46 @@ extern "C" int irc_scan_topk(const void* queries, const void* docs, int64_t Q, i
                         workspace_bytes, out_score, out_idx, as_stream(stream));
 }
 
+// `batches` query batches of one shape against one shard with `depth` of them in flight:
+// the host loop of ShardedDenseIndex.search_many (irc_amd/retrieval.py) in one call, so a
+// C2 batch (~70 us of GPU work) is not paced by the Python side of one search() per batch.
+// Every stream first waits for the work queued on `origin`; batch b runs irc_scan_topk on
+// streams[b % depth] with workspaces[b % depth] into rows [b Q, (b + 1) Q) of the outputs;
+// `origin` then waits for every stream (also after an error, for what was queued).
+extern "C" int irc_scan_topk_many(const void* const* queries, int64_t batches, const void* docs,
+                                  int64_t Q, int64_t N, int64_t D, int64_t k, int64_t doc_offset,
+                                  void* const* workspaces, int64_t workspace_bytes, int64_t depth,
+                                  float* out_score, int64_t* out_idx,
+                                  const irc_stream_t* streams, irc_stream_t origin) {
+  IRC_REQUIRE(batches >= 0 && depth >= 1 && depth <= 16, "scan_topk_many: bad batches / depth");
+  IRC_REQUIRE(batches == 0 || (queries && workspaces && streams && out_score && out_idx),
+              "scan_topk_many: null array");
+  if (batches == 0) return IRC_OK;
+  const hipStream_t org = as_stream(origin);
+  const int nd = (int)std::min<int64_t>(depth, batches);
+  hipEvent_t ev[17];
+  for (int s = 0; s <= nd; ++s)
+    if (hipEventCreateWithFlags(&ev[s], hipEventDisableTiming) != hipSuccess) {
+      for (int t = 0; t < s; ++t) hipEventDestroy(ev[t]);
+      return check_launch("scan_topk_many: event");
+    }
+  hipEventRecord(ev[nd], org);
+  for (int s = 0; s < nd; ++s) hipStreamWaitEvent(as_stream(streams[s]), ev[nd], 0);
+  int rc = IRC_OK;
+  for (int64_t b = 0; b < batches && rc == IRC_OK; ++b) {
+    const int s = (int)(b % nd);
+    rc = scan_topk_impl(2, 1.0f, queries[b], docs, Q, N, D, k, doc_offset, workspaces[s],
+                        workspace_bytes, out_score + b * Q * k, out_idx + b * Q * k,
+                        as_stream(streams[s]));
+  }
+  for (int s = 0; s < nd; ++s) {
+    hipEventRecord(ev[s], as_stream(streams[s]));
+    hipStreamWaitEvent(org, ev[s], 0);
+  }
+  for (int s = 0; s <= nd; ++s) hipEventDestroy(ev[s]);
+  return rc;
+}
+
 static bool pow2_scale(float s) {
   int e;
   return s > 0.f && std::isfinite(s) && std::frexp(s, &e) == 0.5f;

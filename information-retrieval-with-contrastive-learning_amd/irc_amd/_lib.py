@@ -28,6 +28,7 @@ SIGNATURES = {
     "irc_abi_version": (I32, []),
     "irc_scan_topk_workspace": (I64, [I64, I64, I64, I64]),
     "irc_scan_topk": (I32, [P, P, I64, I64, I64, I64, I64, P, I64, P, P, P]),
+    "irc_scan_topk_many": (I32, [P, I64, P, I64, I64, I64, I64, I64, P, I64, I64, P, P, P, P]),
     "irc_corpus_pack": (I32, [P, P, I64, I64, P, P, P]),
     "irc_pair_sample": (I32, [P, P, P, P, I64, P, P]),
     "irc_pair_batch": (I32, [P, P, P, I64, I64, I64, I64, I64, P, P, P]),

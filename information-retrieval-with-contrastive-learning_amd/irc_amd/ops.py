@@ -202,10 +202,13 @@ def qkv_perm_index(H: int, device=None) -> torch.Tensor:
 
 
 # The L the frozen encoder sends to the fused kernel: a sequence takes a 64-row (L <= 64)
-# or 128-row (L <= 128) slot of the QKV GEMM, so below the slot size the slot's extra
-# rows are extra QKV work, against the separate attention launch and the QKV
-# activation's HBM round trip the fusion saves.
-QKV_ATTN_FUSED_L = ((48, 64), (112, 128))
+# or 128-row (L <= 128) slot of the QKV GEMM, or 256 // L sequences share a packed tile, so
+# the slot's or tile's unused rows are extra QKV work, against the separate attention
+# launch and the QKV activation's HBM round trip the fusion saves.  Measured at B = 512
+# (a C2 / C4 micro-batch), us per layer fused vs two-launch (profiles/r06_k/): L = 30-36:
+# 77-92 vs 85-97; 40: 113 vs 98; 44-64: 116-125 vs 120-146; 65-76: 222-225 vs 180-220;
+# 80: 224-225 vs 225-226; 85: 225 vs 237; 88-128: 240-263 vs 253-413.
+QKV_ATTN_FUSED_L = ((29, 36), (44, 64), (80, 128))
 
 
 def qkv_attention_supported(L: int, H: int, heads: int, ranges=((1, 128),)) -> bool:

@@ -13,6 +13,7 @@ per-shard top-k lists and merges them with the same exact rule.
 """
 from __future__ import annotations
 
+import ctypes
 import itertools
 
 import torch
@@ -43,6 +44,35 @@ def scan_topk(queries: torch.Tensor, docs: torch.Tensor, k: int, doc_offset: int
     _lib.call("irc_scan_topk", ptr(q), ptr(d), Q, N, D, k, doc_offset, ptr(ws), ws.numel(),
               ptr(out_s), ptr(out_i), stream_ptr(q.device))
     return out_s, out_i
+
+
+def scan_topk_many(batches, docs: torch.Tensor, k: int, doc_offset: int, streams,
+                   ws_tag: str = "scan"):
+    """scan_topk over query batches of one shape [Q, D], len(streams) of them in flight
+    (batch b on streams[b % depth], each stream with its own workspace), in ONE native
+    call (irc_scan_topk_many): the streams wait for the current stream first and the
+    current stream waits for all of them after.  Returns [(scores, idx)] per batch, views
+    of two [len(batches), Q, k] tensors; identical to scan_topk per batch."""
+    qs = [contig(q, torch.bfloat16) for q in batches]
+    d = contig(docs, torch.bfloat16)
+    require_hip(d, *qs)
+    Q, D = qs[0].shape
+    N = d.shape[0]
+    if d.shape[1] != D or any(q.shape != qs[0].shape for q in qs):
+        raise ValueError("scan_topk_many: every batch [Q, D] with the docs' D")
+    nb, depth = len(qs), len(streams)
+    out_s = torch.empty((nb, Q, k), dtype=torch.float32, device=d.device)
+    out_i = torch.empty((nb, Q, k), dtype=torch.int64, device=d.device)
+    if nb == 0:
+        return []
+    nbytes = int(_lib.fn("irc_scan_topk_workspace")(Q, N, D, k))
+    wss = [workspace(nbytes, d.device, f"{ws_tag}{j}") for j in range(depth)]
+    qp = (ctypes.c_void_p * nb)(*[q.data_ptr() for q in qs])
+    wp = (ctypes.c_void_p * depth)(*[w.data_ptr() for w in wss])
+    sp = (ctypes.c_void_p * depth)(*[s.cuda_stream for s in streams])
+    _lib.call("irc_scan_topk_many", qp, nb, ptr(d), Q, N, D, k, doc_offset, wp, nbytes, depth,
+              ptr(out_s), ptr(out_i), sp, stream_ptr(d.device))
+    return list(zip(out_s.unbind(0), out_i.unbind(0)))
 
 
 def scan_scores(queries: torch.Tensor, docs: torch.Tensor) -> torch.Tensor:
@@ -294,13 +324,16 @@ class ShardedDenseIndex:
         """search() over a sequence of query batches with up to ``depth`` batches
         in flight on as many HIP streams (each with its own scan workspace): one
         batch's latency-bound selects overlap the next batch's HBM-bound filter.
-        ``graphs`` (single process, every batch of one shape): each stream replays a
-        HIP graph of the whole local search captured once, so the host issues a copy,
-        a replay and two result copies per batch instead of the call's individual
-        launches -- measured slower than direct launches at C2 (Q = 256: 86.4 vs 81.1
-        us a batch at depth 2, 76.0 vs 71.9 at depth 3; depth 4 slower again,
-        profiles/r05_zd_scan_depth.txt).  Results are identical to calling search()
-        per batch; returned in order, usable on the current stream."""
+        Single process, bf16, batches of one shape: the whole loop is one native call
+        (irc_scan_topk_many: the host issues a C2 batch in 13-17 us against 39-43 us for
+        search() per batch, so the loop stays GPU-bound -- 60.6 us a batch at depth 3 on
+        a box where the Python loop also kept up, profiles/r06_i_scan_depth.log; the C2
+        leg on boxes since: 3.97-4.09M queries/s, profiles/r06_m/, against 3.27M with the
+        Python loop in profiles/r06_fin1_bench.log).  ``graphs`` (single process, every batch of one
+        shape): each stream replays a HIP graph of the whole local search captured once
+        -- measured slower than direct launches at C2 (77-80 us a batch at depth 3).
+        Results are identical to calling search() per batch; returned in order, usable
+        on the current stream."""
         import torch.distributed as dist
 
         batches = list(batches)
@@ -311,6 +344,11 @@ class ShardedDenseIndex:
             dist.get_world_size(self.group) == 1
         if graphs and not single:
             raise ValueError("graphed search_many needs a single-process index")
+        if single and not graphs and self.dtype == "bf16" and batches and \
+                all(q.shape == batches[0].shape for q in batches):
+            # the whole loop in one native call (irc_scan_topk_many): the per-batch Python
+            # of search() paced a C2 batch's ~70 us of GPU work
+            return scan_topk_many(batches, self.docs, k, self.doc_offset, streams)
         slots = self._graph_slots(batches[0], k, depth, streams) if (graphs and batches) else None
         out = []
         for n, q in enumerate(batches):

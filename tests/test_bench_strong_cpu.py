@@ -50,7 +50,7 @@ def _double_index(n_total, dim, rank, world, dev, group):
 def _args():
     import argparse
 
-    return argparse.Namespace(steps=2, warmup=1)
+    return argparse.Namespace(steps=2, warmup=1, scan_depth=2)
 
 
 def _worker(rank, port, out_dir, world):

@@ -62,11 +62,15 @@ def test_perm_index():
 
 @pytest.mark.parametrize("masked,L", [(True, 64), (False, 64), (True, 63), (True, 57),
                                       (False, 61), (True, 40), (True, 72), (True, 100),
-                                      (False, 128), (True, 128)])
+                                      (False, 128), (True, 128), (True, 32), (True, 48),
+                                      (False, 51), (True, 65), (True, 80), (False, 85),
+                                      (True, 29), (False, 31)])
 def test_bit_exact_on_big_tile_shape(gpu, masked, L):
     """B x L ~ 32k rows, where the unfused QKV GEMM runs on the big-tile main loop
-    (L <= 64: 64-row slots, four sequences a tile; L in (64, 128]: 128-row slots, two)."""
-    B = {40: 800, 72: 448, 100: 320, 128: 256}.get(L, 512)
+    (L <= 64: 64-row slots, four sequences a tile; L in (64, 128]: 128-row slots, two;
+    packed tiles of 256 // L sequences, staged a head at a time, where they take fewer
+    waves: e.g. L = 40 / 48 / 65 / 72 / 80 / 85 here)."""
+    B = {40: 800, 72: 448, 100: 320, 128: 256}.get(L, 512 if 52 <= L <= 64 else 32768 // L)
     H, heads = 768, 12
     x, w, b, mask = _inputs(gpu, B, L, H, 5, masked)
     cf = _fused(x, w, b, mask, B, L, H, heads)
@@ -80,11 +84,14 @@ def test_bit_exact_on_big_tile_shape(gpu, masked, L):
                                          (37, 768, 12, 40), (5, 768, 12, 1), (64, 1024, 16, 50),
                                          (300, 768, 12, 48), (9, 768, 12, 17),
                                          (37, 768, 12, 72), (3, 768, 12, 100),
-                                         (33, 1024, 16, 128), (7, 768, 12, 65)])
+                                         (33, 1024, 16, 128), (7, 768, 12, 65),
+                                         (5, 768, 12, 85), (11, 1024, 16, 33),
+                                         (37, 768, 12, 30), (3, 1024, 16, 32)])
 def test_against_reference(gpu, B, H, heads, L):
     """Ragged last tile (B = 37: 2368 rows), a single partial tile, BERT-large width;
     L < 64 (slots with repeated last tokens: B = 37 at L = 40 leaves a 1-sequence last
-    tile, L = 1 a single key)."""
+    tile, L = 1 a single key); packed tiles (B = 37 at L = 30: eight sequences a tile, five
+    in the last; B = 3 at L = 32: one partial tile)."""
     x, w, b, mask = _inputs(gpu, B, L, H, B + H)
     cf = _fused(x, w, b, mask, B, L, H, heads).float()
     cu = _unfused(x, w, b, mask, B, L, H, heads).float()
@@ -106,11 +113,11 @@ def test_rejects_unsupported(gpu):
         ops.qkv_attention(x.float(), w, b, mask, 4, 64, 768, 12)
 
 
-@pytest.mark.parametrize("L", [64, 61, 120])
+@pytest.mark.parametrize("L", [64, 61, 120, 32, 80])
 def test_encoder_fused_matches_unfused(gpu, L):
     """The frozen encoder with the fused launch equals the two-launch encoder bit for bit
-    at B = 512 (every QKV GEMM on the big-tile main loop), at L = 64 and at a joint
-    padding of 61 (slots)."""
+    where every unfused QKV GEMM runs on the big-tile main loop: L = 64 and a joint padding
+    of 61 (slots), L = 120 at B = 256 (128-row slots), L = 32 and 80 at B = 512 (packed)."""
     import dataclasses
 
     from irc_amd.bert import BERT_BASE, BertModel

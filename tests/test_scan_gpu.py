@@ -296,6 +296,25 @@ def test_search_many_equals_serial_search(gpu):
             assert torch.equal(s, s0) and torch.equal(i, i0)
 
 
+@pytest.mark.parametrize("q,nb,depth", [(256, 7, 3), (64, 5, 2), (1, 4, 3), (200, 2, 3),
+                                        (300, 1, 3)])
+def test_native_search_many_equals_serial_search(gpu, q, nb, depth):
+    """Batches of one shape take the one-call loop (irc_scan_topk_many): the GEMM filter
+    (Q >= 192), the single pass (Q <= 64), fewer batches than streams; exactly what serial
+    search() calls return, and ready on the current stream."""
+    from irc_amd import retrieval
+
+    rng = np.random.default_rng(q + nb)
+    d = _dev(_grid(rng, (30000, 256), 3), gpu)
+    index = retrieval.ShardedDenseIndex(d, doc_offset=11)
+    batches = [_dev(_grid(rng, (q, 256), 3), gpu) for _ in range(nb)]
+    many = index.search_many(batches, 50, depth=depth)
+    assert len(many) == nb
+    for qb, (s, i) in zip(batches, many):
+        s0, i0 = index.search(qb, 50)
+        assert torch.equal(s, s0) and torch.equal(i, i0)
+
+
 def test_graphed_search_many_equals_serial_search(gpu):
     """HIP-graph replays of the whole local search (one graph per stream) return
     exactly what serial search() calls return, for bf16 and fp8 shards."""

@@ -1,7 +1,7 @@
 """QKV projection + attention: one fused launch (irc_qkv_attention) against the two-launch
 form (irc_gemm EPI_BIAS + irc_attention) at the frozen encoder's shapes, interleaved.
 
-    python tools/qkv_attn_bench.py [--iters 20] [--h 768] [--lens 64,57,72,100,128]
+    python tools/qkv_attn_bench.py [--iters 20] [--h 768] [--b B] [--lens 64,57,72,100,128]
 
 Prints us per layer (HIP events on the launch stream) for each form, twice.
 """
@@ -19,14 +19,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--h", type=int, default=768)
-    ap.add_argument("--b", type=int, default=512)
-    ap.add_argument("--lens", default="64", help="sequence lengths (B = 32768 // L tokens ~ 32k)")
+    ap.add_argument("--b", type=int, default=0,
+                    help="sequences (default: 512 at L = 64, else 32768 // L: ~32k tokens)")
+    ap.add_argument("--lens", default="64", help="sequence lengths")
     a = ap.parse_args()
     from irc_amd import ops
 
     dev = torch.device("cuda:0")
     for L in (int(v) for v in a.lens.split(",")):
-        run_len(a, ops, dev, L, a.b if a.lens == "64" else max(1, 32768 // L))
+        run_len(a, ops, dev, L, a.b or (512 if L == 64 else max(1, 32768 // L)))
 
 
 def run_len(a, ops, dev, L, B):
