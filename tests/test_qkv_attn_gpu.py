@@ -64,7 +64,7 @@ def test_perm_index():
                                       (False, 61), (True, 40), (True, 72), (True, 100),
                                       (False, 128), (True, 128), (True, 32), (True, 48),
                                       (False, 51), (True, 65), (True, 80), (False, 85),
-                                      (True, 29), (False, 31)])
+                                      (True, 29), (False, 31), (True, 96)])
 def test_bit_exact_on_big_tile_shape(gpu, masked, L):
     """B x L ~ 32k rows, where the unfused QKV GEMM runs on the big-tile main loop
     (L <= 64: 64-row slots, four sequences a tile; L in (64, 128]: 128-row slots, two;
