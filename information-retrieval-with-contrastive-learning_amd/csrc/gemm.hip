@@ -1089,7 +1089,8 @@ struct QaArgs {
   int M, K, H;
   int64_t ldx, ldc;
   float scale;
-  int L;                    // sequence length, 1..64 (one 64-row slot per sequence)
+  int L;                    // sequence length, 1..128
+  int group_m;              // grouped tile order (grouped_tile; 0 = row-major)
 };
 
 //
@@ -1125,7 +1126,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
   }
   int tm, tn;
-  grouped_tile(bid, tiles_m, tiles_n, IRC_GEMM_GROUP_M, tm, tn);
+  grouped_tile(bid, tiles_m, tiles_n, g.group_m, tm, tn);
   // packed: first token row of the tile's first sequence; slots: first slot row
   const int m0 = PACK ? tm * spt * g.L : tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63;
@@ -1649,7 +1650,10 @@ extern "C" int irc_qkv_attention(int64_t M, int64_t H, int64_t heads, int64_t L,
   IRC_REQUIRE(bias_perm != nullptr, "qkv_attention: bias required");
   QaArgs a{static_cast<const unsigned short*>(x), static_cast<const unsigned short*>(wqkv_perm),
            bias_perm, mask, static_cast<unsigned short*>(ctx), (int)M, (int)H, (int)H, ldx, ldc,
-           0.125f, (int)L};
+           0.125f, (int)L, IRC_GEMM_GROUP_M};
+  // Row-major tile order here even where Wqkv exceeds an XCD's 4 MB L2 (C4: 6 MB): grouped
+  // (8 rows) measured 11.35-11.39k against 11.38-11.43k pairs/s on the C4 leg, GEMM traffic
+  // 407 vs 415 MB per launch (profiles/r06_n/)
   hipStream_t st = as_stream(stream);
   // Sequences per 256-row tile: 64- or 128-row slots, or packed (256 / L) where that takes
   // fewer waves of tiles over the CUs.  Packed tiles pay an attention round per 8 (sequence,
