@@ -466,8 +466,12 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
   const int b = active ? (int)(item / NJ / heads) : 0;
   const int64_t ld3 = 3LL * H;
   const unsigned short* base = qkv + (int64_t)b * Lr * ld3 + a * DH;  // + j*ld3: Q | +H: K | +2H: V
+  // key blocks through the sequence's last visible key (visible_key_blocks: the rest add
+  // exactly zero); V^T is staged for those only
+  int nkb = NJ;
   if (active) {
-    for (int p = lane; p < (L / 2) * 8; p += 64) {
+    nkb = visible_key_blocks(mask ? mask + (int64_t)b * Lr : nullptr, Lr, NJ, lane);
+    for (int p = lane; p < nkb * 128; p += 64) {
       const int dc = p & 7, j = (p >> 3) * 2;  // 8-wide d chunk, key pair (j, j+1)
       const u16x8 v0 = j < Lr ? *reinterpret_cast<const u16x8*>(base + (int64_t)j * ld3 + 2 * H + dc * 8)
                               : (u16x8)0;
@@ -494,6 +498,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
   f32x16 s[NJ];
 #pragma unroll
   for (int jb = 0; jb < NJ; ++jb) {
+    if (jb >= nkb) break;
     s[jb] = (f32x16)0.f;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -504,7 +509,8 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
   }
   float mx = -INFINITY;
 #pragma unroll
-  for (int jb = 0; jb < NJ; ++jb)
+  for (int jb = 0; jb < NJ; ++jb) {
+    if (jb >= nkb) break;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const f32x4 bias = *reinterpret_cast<const f32x4*>(&mb[wv][32 * jb + 8 * q + 4 * h]);
@@ -515,22 +521,26 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
         mx = fmaxf(mx, v);
       }
     }
+  }
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float sum = 0.f;
 #pragma unroll
-  for (int jb = 0; jb < NJ; ++jb)
+  for (int jb = 0; jb < NJ; ++jb) {
+    if (jb >= nkb) break;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const float p = __expf(s[jb][e] - mx);
       s[jb][e] = p;
       sum += p;
     }
+  }
   sum += __shfl_xor(sum, 32, 64);
   const float inv = 1.f / sum;
 
   f32x16 o[2] = {(f32x16)0.f, (f32x16)0.f};
 #pragma unroll
-  for (int jb = 0; jb < NJ; ++jb)
+  for (int jb = 0; jb < NJ; ++jb) {
+    if (jb >= nkb) break;
 #pragma unroll
     for (int k2 = 0; k2 < 2; ++k2) {
       bf16x8 pa;
@@ -547,6 +557,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
                                                         0, 0, 0);
       }
     }
+  }
   // O C layout: col = d (lane), row = query 32ib + (e&3) + 8(e>>2) + 4h
   if constexpr (MXO) {
     // O (bf16-rounded like the bf16 path's ctx) goes through this wave's V^T slot,

@@ -1203,6 +1203,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
         for (int j = lane; j < 128; j += 64)
           mb[j] = j >= g.L ? -3e30f
                            : ((g.mask == nullptr || g.mask[r0 + j] != 0) ? 0.f : -1e30f);
+        const int nkb = visible_key_blocks(g.mask ? g.mask + r0 : nullptr, g.L, nj, lane);
         __builtin_amdgcn_wave_barrier();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const unsigned short* Q = Tq;
@@ -1218,7 +1219,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
 #pragma unroll
         for (int jb = 0; jb < NJM; ++jb) {
           sc[jb] = (f32x16)0.f;
-          if (jb < nj) {
+          if (jb < nkb) {
             const int kr = min(t0 + 32 * jb + r32, BM - 1);
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
@@ -1230,7 +1231,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
         float mx = -INFINITY;
 #pragma unroll
         for (int jb = 0; jb < NJM; ++jb) {
-          if (jb >= nj) break;
+          if (jb >= nkb) break;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const f32x4 bias = *reinterpret_cast<const f32x4*>(&mb[32 * jb + 8 * q + 4 * h]);
@@ -1246,7 +1247,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
         float sum = 0.f;
 #pragma unroll
         for (int jb = 0; jb < NJM; ++jb) {
-          if (jb >= nj) break;
+          if (jb >= nkb) break;
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const float p = __expf(sc[jb][e] - mx);
@@ -1259,7 +1260,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
         f32x16 o[2] = {(f32x16)0.f, (f32x16)0.f};
 #pragma unroll
         for (int jb = 0; jb < NJM; ++jb) {
-          if (jb >= nj) break;
+          if (jb >= nkb) break;
 #pragma unroll
           for (int k2 = 0; k2 < 2; ++k2) {
             bf16x8 pa;
@@ -1326,6 +1327,8 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
       for (int j = lane; j < SL; j += 64)
         mbw[j] = j >= g.L ? -3e30f
                           : ((g.mask == nullptr || g.mask[r0 + j] != 0) ? 0.f : -1e30f);
+      // key blocks through the sequence's last visible key (the rest add exactly zero)
+      const int nkb = visible_key_blocks(g.mask ? g.mask + r0 : nullptr, g.L, nj, lane);
       __builtin_amdgcn_wave_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       const unsigned short* Ts = T + 64 * sl * TP;
@@ -1343,7 +1346,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
 #pragma unroll
         for (int jb = 0; jb < NJM; ++jb) {
           sc[jb] = (f32x16)0.f;
-          if (jb < nj) {
+          if (jb < nkb) {
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
               const bf16x8 kf =
@@ -1355,7 +1358,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
         float mx = -INFINITY;
 #pragma unroll
         for (int jb = 0; jb < NJM; ++jb) {
-          if (jb >= nj) break;
+          if (jb >= nkb) break;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const f32x4 bias = *reinterpret_cast<const f32x4*>(&mbw[32 * jb + 8 * q + 4 * h]);
@@ -1371,7 +1374,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
         float sum = 0.f;
 #pragma unroll
         for (int jb = 0; jb < NJM; ++jb) {
-          if (jb >= nj) break;
+          if (jb >= nkb) break;
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const float p = __expf(sc[jb][e] - mx);
@@ -1384,7 +1387,7 @@ __global__ __launch_bounds__(big::NT, 1) void qkv_attn_kernel(QaArgs g) {
         f32x16 o[2] = {(f32x16)0.f, (f32x16)0.f};
 #pragma unroll
         for (int jb = 0; jb < NJM; ++jb) {
-          if (jb >= nj) break;
+          if (jb >= nkb) break;
 #pragma unroll
           for (int k2 = 0; k2 < 2; ++k2) {
             bf16x8 pa;

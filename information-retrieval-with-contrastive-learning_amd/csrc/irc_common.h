@@ -226,6 +226,31 @@ __device__ __forceinline__ float warp_sum(float v) {
   return v;
 }
 
+// Key blocks of 32 that the attention rows of one sequence must visit: through the block
+// holding its last visible key.  Every key past it is masked (-1e30) or past L (-3e30), so
+// its probability is exactly 0 and its block adds exactly nothing to the row maximum, the
+// sum or P.V: skipping those blocks leaves the context bit-identical.  With no visible key
+// at all the row averages every key, so all nj blocks stay.  mask_row: the sequence's L
+// mask words (nonzero = visible), or null (all visible).  Called by all 64 lanes of a wave;
+// the result is wave-uniform.
+__device__ __forceinline__ int visible_key_blocks(const int64_t* mask_row, int L, int nj,
+                                                  int lane) {
+#ifdef IRC_ATTN_NO_SKIP  // A/B build: every key block
+  return nj;
+#endif
+  if (mask_row == nullptr) return nj;
+  int last = -1;
+  for (int j = lane; j < L; j += 64)
+    if (mask_row[j] != 0) last = j;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int t = __shfl_xor(last, o, 64);
+    last = t > last ? t : last;
+  }
+  last = __builtin_amdgcn_readfirstlane(last);
+  return last < 0 ? nj : last / 32 + 1;
+}
+
 __device__ __forceinline__ float warp_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -99,3 +99,48 @@ def test_attention_long_rows_all_masked_and_single_key(gpu):
     e = bf16_ulps(out.float().cpu().numpy(), ref.numpy(), ATT_FLOOR)
     print(f"long rows: {e:.2f} bf16 ulps")
     assert e <= ATT_ULPS, f"{e:.2f} bf16 ulps"
+
+
+@pytest.mark.parametrize("L", [64, 72, 96, 128])
+def test_attention_masks_with_holes(gpu, L):
+    """Key blocks past a sequence's last visible key are skipped (encoder.hip
+    visible_key_blocks): rows whose only visible keys sit late after masked ones, a
+    visible key alone in the last block, one alone at position 0, an all-masked row
+    (every block kept: the uniform average) -- all against the fp32 reference."""
+    from irc_amd import ops
+
+    B, H, heads = 6, 768, 12
+    g = torch.Generator().manual_seed(100 + L)
+    qkv = torch.randn((B * L, 3 * H), generator=g).bfloat16()
+    mask = torch.zeros(B, L, dtype=torch.int64)
+    mask[0] = 1                      # all visible
+    mask[1, 0] = 1                   # only the first key
+    mask[2, L - 1] = 1               # only the last key (last block)
+    mask[3, ::5] = 1                 # holes in every block
+    mask[4, 3:40] = 1                # a window straddling blocks 0 and 1
+    # row 5 all masked
+    out = ops.attention(qkv.to(gpu), mask.to(gpu), B, L, H, heads)
+    ref = _ref(qkv, mask, B, L, H, heads)
+    e = bf16_ulps(out.float().cpu().numpy(), ref.numpy(), ATT_FLOOR)
+    print(f"L={L} holes: {e:.2f} bf16 ulps")
+    assert e <= ATT_ULPS, f"{e:.2f} bf16 ulps"
+
+
+def test_attention_skipped_blocks_bit_identical(gpu):
+    """Sequences whose visible keys all lie in the first 32: their first 32 context rows
+    at L = 64 (the second key block skipped) equal those at L = 32 bit for bit -- the
+    skipped block would have added exact zeros -- as they do at L = 96 and 128."""
+    from irc_amd import ops
+
+    B, H, heads = 9, 768, 12
+    g = torch.Generator().manual_seed(7)
+    qkv = torch.randn((B, 128, 3 * H), generator=g).bfloat16()
+    lens = torch.randint(1, 33, (B,), generator=g)
+    mask = (torch.arange(128)[None, :] < lens[:, None]).long()
+    outs = {}
+    for L in (32, 64, 96, 128):
+        q = qkv[:, :L].reshape(B * L, 3 * H).contiguous().to(gpu)
+        m = mask[:, :L].contiguous().to(gpu)
+        outs[L] = ops.attention(q, m, B, L, H, heads).view(B, L, H)[:, :32].cpu()
+    for L in (64, 96, 128):
+        assert torch.equal(outs[L], outs[32]), L

@@ -136,3 +136,25 @@ def test_encoder_fused_matches_unfused(gpu, L):
     m.fused_attention = True
     y1 = m.encode(ids, mask)
     assert torch.equal(y0, y1)
+
+
+@pytest.mark.parametrize("L", [64, 32, 80, 120])
+def test_bit_exact_masks_with_holes(gpu, L):
+    """Masks with holes, a lone late key, a lone first key and all-masked rows (the
+    epilogue skips key blocks past a sequence's last visible key, as irc_attention
+    does): fused equals two-launch bit for bit (slots at 64 / 120, packed at 32 / 80)."""
+    B = {64: 512, 120: 256}.get(L, 32768 // L)
+    H, heads = 768, 12
+    x, w, b, _ = _inputs(gpu, B, L, H, 9, masked=False)
+    g = torch.Generator().manual_seed(L)
+    kind = torch.randint(0, 5, (B,), generator=g)
+    lens = torch.randint(1, L + 1, (B,), generator=g)
+    pos = torch.arange(L)[None, :]
+    mask = torch.where((kind == 0)[:, None], (pos < lens[:, None]), torch.zeros(1, L, dtype=torch.bool))
+    mask |= (kind == 1)[:, None] & ((pos % 7) == (lens[:, None] % 7))   # holes
+    mask |= (kind == 2)[:, None] & (pos == L - 1)                         # lone last key
+    mask |= (kind == 3)[:, None] & (pos == 0)                             # lone first key
+    mask = mask.to(torch.int64).to(gpu)                                    # kind 4: all masked
+    cf = _fused(x, w, b, mask, B, L, H, heads)
+    cu = _unfused(x, w, b, mask, B, L, H, heads)
+    assert torch.equal(cf, cu)

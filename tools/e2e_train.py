@@ -162,6 +162,8 @@ def main():
         f"{k} {np.median(v[w:]) * 1e3:.2f}" for k, v in spent.items()) +
         f"; whole run {tot * 1e3 / len(stamps):.2f} per step (incl. startup); padded L mean "
         f"{np.mean(lens):.1f} (bench.py's synthetic batch: L = 64)")
+    vals, cnt = np.unique(np.asarray(lens), return_counts=True)
+    print("padded L histogram: " + ", ".join(f"{v}: {c}" for v, c in zip(vals, cnt)))
 
 
 if __name__ == "__main__":
