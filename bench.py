@@ -842,11 +842,21 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # IRC_DIST_BACKEND=gloo (as main.py): a rehearsal of the N-rank path where RCCL cannot
+    # run it, e.g. N ranks sharing a 1-GPU box (ranks beyond the visible devices wrap
+    # round them); the default is RCCL with one rank per GPU
+    backend = os.environ.get("IRC_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "gloo" and ndev and local >= ndev:
+        local %= ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     train = scan = None
     model = None
@@ -945,6 +955,8 @@ def main():
                        "parallelism": f"dp{world} (train) / corpus-sharded x{world} (scan)"},
             "roofline": head["roofline"], "cpu_baseline": head["cpu_baseline"],
         }
+        if world > 1:
+            line["config"]["backend"] = dist.get_backend()  # "gloo": a rehearsal, not RCCL
         if train is not None:
             line["train"] = {k: train[k] for k in ("pairs_per_s", "ms_per_step", "step_tflops",
                                                    "flops_per_pair", "loss_last", "roofline")}
