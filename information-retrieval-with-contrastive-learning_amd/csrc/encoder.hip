@@ -425,8 +425,11 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ qk
 }
 
 // MFMA attention, bf16, head dim 64, L <= 32*NJ (NJ <= 4, any L: the joint
-// padding of a batch gives e.g. L = 72): one wave per (sequence, head, block of
-// 32 queries).  Key rows past L are read clamped and carry a -3e30 bias (below a
+// padding of a batch gives e.g. L = 72): one workgroup per (sequence, head), one wave
+// per block of 32 queries, the NJ waves sharing one V^T image and key-bias row in LDS
+// (staged once per (sequence, head); the round-5 form gave each wave its own copy, so
+// at NJ = 3 a workgroup of 4 unrelated waves held 53 KB and a CU 12 waves).  Key rows
+// past L are read clamped and carry a -3e30 bias (below a
 // masked key's -1e30, so an all-masked row still averages its L keys), V rows
 // past L are zero in LDS, query rows past L are never stored.
 //  * S^T[j][i] = K[j] . Q[i] on v_mfma_f32_32x32x16_bf16 (A = K rows, B = Q rows,
@@ -451,44 +454,35 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
                                                             unsigned char* __restrict__ ctx8 = nullptr,
                                                             unsigned char* __restrict__ cs = nullptr,
                                                             int64_t mpad = 0, int Lr = 32 * NJ) {
-  constexpr int L = 32 * NJ, DH = 64;
-  // V^T row pitch (u16): 8-byte aligned, conflict-free b64 reads (MXO at L = 32: 68,
-  // so the slot also holds the 32 x 68-float O staging)
-  constexpr int VP = (MXO && L + 4 < 68) ? 68 : L + 4;
-  __shared__ __attribute__((aligned(16))) unsigned short vt[4][DH][VP];
-  __shared__ __attribute__((aligned(16))) float mb[4][L];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int h = lane >> 5, r32 = lane & 31;
-  const int64_t item = (int64_t)blockIdx.x * 4 + wv;  // (b, head, ib)
-  const bool active = item < (int64_t)B * heads * NJ;
-  const int ib = active ? (int)(item % NJ) : 0;
-  const int a = active ? (int)(item / NJ % heads) : 0;
-  const int b = active ? (int)(item / NJ / heads) : 0;
+  constexpr int L = 32 * NJ, DH = 64, NT = 64 * NJ;
+  // V^T row pitch (u16): 8-byte aligned, conflict-free b64 reads
+  constexpr int VP = L + 4;
+  constexpr int OP = 68;  // MXO: row pitch (floats) of a wave's 32-row O staging
+  __shared__ __attribute__((aligned(16))) unsigned short vt[DH][VP];
+  __shared__ __attribute__((aligned(16))) float mb[L];
+  __shared__ __attribute__((aligned(16))) float ost[MXO ? NJ : 1][MXO ? 32 * OP : 1];
+  const int lane = threadIdx.x & 63, h = lane >> 5, r32 = lane & 31;
+  const int ib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // query block
+  const int a = (int)(blockIdx.x % heads), b = (int)(blockIdx.x / heads);
   const int64_t ld3 = 3LL * H;
   const unsigned short* base = qkv + (int64_t)b * Lr * ld3 + a * DH;  // + j*ld3: Q | +H: K | +2H: V
   // key blocks through the sequence's last visible key (visible_key_blocks: the rest add
-  // exactly zero); V^T is staged for those only
-  int nkb = NJ;
-  if (active) {
-    nkb = visible_key_blocks(mask ? mask + (int64_t)b * Lr : nullptr, Lr, NJ, lane);
-    for (int p = lane; p < nkb * 128; p += 64) {
-      const int dc = p & 7, j = (p >> 3) * 2;  // 8-wide d chunk, key pair (j, j+1)
-      const u16x8 v0 = j < Lr ? *reinterpret_cast<const u16x8*>(base + (int64_t)j * ld3 + 2 * H + dc * 8)
-                              : (u16x8)0;
-      const u16x8 v1 =
-          j + 1 < Lr ? *reinterpret_cast<const u16x8*>(base + (int64_t)(j + 1) * ld3 + 2 * H + dc * 8)
-                     : (u16x8)0;
+  // exactly zero; every wave finds the same count); V^T is staged for those only, once
+  const int nkb = visible_key_blocks(mask ? mask + (int64_t)b * Lr : nullptr, Lr, NJ, lane);
+  for (int p = threadIdx.x; p < nkb * 128; p += NT) {
+    const int dc = p & 7, j = (p >> 3) * 2;  // 8-wide d chunk, key pair (j, j+1)
+    const u16x8 v0 = j < Lr ? *reinterpret_cast<const u16x8*>(base + (int64_t)j * ld3 + 2 * H + dc * 8)
+                            : (u16x8)0;
+    const u16x8 v1 =
+        j + 1 < Lr ? *reinterpret_cast<const u16x8*>(base + (int64_t)(j + 1) * ld3 + 2 * H + dc * 8)
+                   : (u16x8)0;
 #pragma unroll
-      for (int dd = 0; dd < 8; ++dd)
-        *reinterpret_cast<uint32_t*>(&vt[wv][dc * 8 + dd][j]) =
-            (uint32_t)v0[dd] | ((uint32_t)v1[dd] << 16);
-    }
-    for (int j = lane; j < L; j += 64)
-      mb[wv][j] = j >= Lr ? -3e30f
-                          : ((mask == nullptr || mask[(int64_t)b * Lr + j] != 0) ? 0.f : -1e30f);
+    for (int dd = 0; dd < 8; ++dd)
+      *reinterpret_cast<uint32_t*>(&vt[dc * 8 + dd][j]) = (uint32_t)v0[dd] | ((uint32_t)v1[dd] << 16);
   }
+  for (int j = threadIdx.x; j < L; j += NT)
+    mb[j] = j >= Lr ? -3e30f : ((mask == nullptr || mask[(int64_t)b * Lr + j] != 0) ? 0.f : -1e30f);
   __syncthreads();
-  if (!active) return;  // past the only barrier
 
   bf16x8 qf[4];
 #pragma unroll
@@ -513,7 +507,7 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
     if (jb >= nkb) break;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const f32x4 bias = *reinterpret_cast<const f32x4*>(&mb[wv][32 * jb + 8 * q + 4 * h]);
+      const f32x4 bias = *reinterpret_cast<const f32x4*>(&mb[32 * jb + 8 * q + 4 * h]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float v = s[jb][4 * q + r] * scale + bias[r];
@@ -550,8 +544,8 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
         const int d = 32 * db + r32;
-        const u16x4 lo = *reinterpret_cast<const u16x4*>(&vt[wv][d][j0]);
-        const u16x4 hi = *reinterpret_cast<const u16x4*>(&vt[wv][d][j0 + 8]);
+        const u16x4 lo = *reinterpret_cast<const u16x4*>(&vt[d][j0]);
+        const u16x4 hi = *reinterpret_cast<const u16x4*>(&vt[d][j0 + 8]);
         const u16x8 vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(bf16x8, vv), o[db],
                                                         0, 0, 0);
@@ -560,15 +554,11 @@ __global__ __launch_bounds__(256) void attention_mfma_kernel(const unsigned shor
   }
   // O C layout: col = d (lane), row = query 32ib + (e&3) + 8(e>>2) + 4h
   if constexpr (MXO) {
-    // O (bf16-rounded like the bf16 path's ctx) goes through this wave's V^T slot,
-    // free once the P.V reads have returned, as [32 rows][OP floats]; each lane
-    // then owns one MX block (row lane >> 1, 32 columns): lane-local block max,
-    // 32 codes in two 16-byte stores, one scale byte.
-    constexpr int OP = 68;  // row pitch (floats): 16-byte rows, h halves 16 banks apart
-    static_assert(32 * OP * 4 <= (int)sizeof(vt[0]), "O staging fits the V^T slot");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    float* os = reinterpret_cast<float*>(&vt[wv][0][0]);
+    // O (bf16-rounded like the bf16 path's ctx) goes through the wave's own slot of ost
+    // as [32 rows][OP floats] (16-byte rows, h halves 16 banks apart); each lane then
+    // owns one MX block (row lane >> 1, 32 columns): lane-local block max, 32 codes in
+    // two 16-byte stores, one scale byte.
+    float* os = &ost[MXO ? ib : 0][0];
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -896,7 +886,8 @@ extern "C" int irc_attention_mx(const void* qkv, const int64_t* mask, void* ctx8
   switch ((L + 31) / 32) {
 #define IRC_ATTX(NJ)                                                                             \
   case NJ:                                                                                       \
-    hipLaunchKernelGGL((enc::attention_mfma_kernel<NJ, true>), grid, dim3(256), 0, st,          \
+    hipLaunchKernelGGL((enc::attention_mfma_kernel<NJ, true>), dim3((unsigned)(B * heads)),    \
+                       dim3(64 * NJ), 0, st,                                                     \
                        (const unsigned short*)qkv, mask, (unsigned short*)nullptr, (int)B, (int)H, \
                        (int)heads, sc, c8, css, mpad, (int)L);                                   \
     break;
@@ -979,7 +970,8 @@ extern "C" int irc_attention(int dtype, const void* qkv, const int64_t* mask, vo
     switch ((L + 31) / 32) {
 #define IRC_ATTB(NJ)                                                                             \
   case NJ:                                                                                       \
-    hipLaunchKernelGGL(enc::attention_mfma_kernel<NJ>, grid, dim3(256), 0, st,                   \
+    hipLaunchKernelGGL(enc::attention_mfma_kernel<NJ>, dim3((unsigned)(B * heads)), dim3(64 * NJ), \
+                       0, st,                                                                    \
                        (const unsigned short*)qkv, mask, (unsigned short*)ctx, (int)B, (int)H,   \
                        (int)heads, sc, (unsigned char*)nullptr, (unsigned char*)nullptr,         \
                        (int64_t)0, (int)L);                                                      \
