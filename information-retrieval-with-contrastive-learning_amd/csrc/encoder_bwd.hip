@@ -419,16 +419,18 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const T* __restrict__ qkv
 // the odd lane those of row r + 1 -- half the store instructions of per-element 2-byte
 // stores, same bytes.  row_r points at row r's element of column 0 of the lane's column
 // block; ld is the row stride.
+// rows_left: rows r, r + 1, ... that exist (Lr - r); a lane whose row does not is not stored
+// (the exchange itself needs every lane).
 __device__ __forceinline__ void store_row_pair(unsigned short* row_r, int64_t ld, int c, float v0,
-                                               float v1, int lane) {
+                                               float v1, int lane, int rows_left = 2) {
   const uint32_t w = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
   const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)w, 0xB1, 0xF, 0xF, false);
   const int odd = lane & 1;
   const uint32_t v = odd ? ((x >> 16) | (w & 0xFFFF0000u)) : ((w & 0xFFFFu) | (x << 16));
-  *reinterpret_cast<uint32_t*>(row_r + odd * ld + c - odd) = v;
+  if (odd < rows_left) *reinterpret_cast<uint32_t*>(row_r + odd * ld + c - odd) = v;
 }
 
-// MFMA (bf16, DH = 64, L = 32*NJ): one workgroup of NJ waves per (sequence, head).
+// MFMA (bf16, DH = 64, L <= 32*NJ): one workgroup of NJ waves per (sequence, head).
 // The 32x32x16 C layout of X^T (rows j, lanes = columns i) is, with the k order
 // permuted, the A operand of X (rows i, k over j) -- the forward's P.V trick --
 // so the backward needs both orientations:
@@ -438,11 +440,11 @@ __device__ __forceinline__ void store_row_pair(unsigned short* row_r, int64_t ld
 //  phase B, wave = key block (lanes = keys): S = Q K^T, P from the saved row
 //    statistics, dP = dO V^T, dS, dV = P^T dO and dK = scale dS^T Q (dO^T, Q^T
 //    from LDS).
-template <int NJ>
+template <int NJ, bool PART = false>  // PART: L not a multiple of 32 (rows past Lr)
 __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
     const unsigned short* __restrict__ qkv, const int64_t* __restrict__ mask,
     const unsigned short* __restrict__ ctx, const unsigned short* __restrict__ dctx,
-    unsigned short* __restrict__ dqkv, int H, int heads, float scale) {
+    unsigned short* __restrict__ dqkv, int H, int heads, float scale, int Lr = 32 * NJ) {
   constexpr int L = 32 * NJ, DH = 64;
   constexpr int VP = L + 4;  // transposed-tile row pitch (u16)
   __shared__ __attribute__((aligned(16))) unsigned short kT[DH][VP];
@@ -456,19 +458,31 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
   const int h = lane >> 5, r32 = lane & 31;
   const int b = blockIdx.x / heads, a = blockIdx.x % heads;
   const int64_t ld3 = 3LL * H;
-  const unsigned short* base = qkv + (int64_t)b * L * ld3 + a * DH;  // Q | +H: K | +2H: V
-  const unsigned short* dob = dctx + (int64_t)b * L * H + a * DH;
-  const unsigned short* ob = ctx + (int64_t)b * L * H + a * DH;
-  unsigned short* gb = dqkv + (int64_t)b * L * ld3 + a * DH;
+  // Lr <= L rows per sequence (a batch padded to L not a multiple of 32): rows past Lr read
+  // as zeros -- keys past Lr carry the -3e30 bias (P = 0), query rows past Lr have dO = 0,
+  // so they add exactly nothing to dK / dV -- and are never stored
+  const unsigned short* base = qkv + (int64_t)b * Lr * ld3 + a * DH;  // Q | +H: K | +2H: V
+  const unsigned short* dob = dctx + (int64_t)b * Lr * H + a * DH;
+  const unsigned short* ob = ctx + (int64_t)b * Lr * H + a * DH;
+  unsigned short* gb = dqkv + (int64_t)b * Lr * ld3 + a * DH;
+  const auto ld8 = [&](const unsigned short* p, int row) {
+    if constexpr (PART) return row < Lr ? *reinterpret_cast<const u16x8*>(p) : (u16x8)0;
+    return *reinterpret_cast<const u16x8*>(p);
+  };
+  const auto ldf = [&](const unsigned short* p, int row) {
+    if constexpr (PART) return row < Lr ? *reinterpret_cast<const bf16x8*>(p) : (bf16x8)0;
+    return *reinterpret_cast<const bf16x8*>(p);
+  };
+  const auto left = [&](int row) { return PART ? Lr - row : 2; };  // store_row_pair rows
 
   for (int p = threadIdx.x; p < (L / 2) * 8; p += 64 * NJ) {
     const int dc = p & 7, j = (p >> 3) * 2;
-    const u16x8 k0 = *reinterpret_cast<const u16x8*>(base + (int64_t)j * ld3 + H + dc * 8);
-    const u16x8 k1 = *reinterpret_cast<const u16x8*>(base + (int64_t)(j + 1) * ld3 + H + dc * 8);
-    const u16x8 q0 = *reinterpret_cast<const u16x8*>(base + (int64_t)j * ld3 + dc * 8);
-    const u16x8 q1 = *reinterpret_cast<const u16x8*>(base + (int64_t)(j + 1) * ld3 + dc * 8);
-    const u16x8 o0 = *reinterpret_cast<const u16x8*>(dob + (int64_t)j * H + dc * 8);
-    const u16x8 o1 = *reinterpret_cast<const u16x8*>(dob + (int64_t)(j + 1) * H + dc * 8);
+    const u16x8 k0 = ld8(base + (int64_t)j * ld3 + H + dc * 8, j);
+    const u16x8 k1 = ld8(base + (int64_t)(j + 1) * ld3 + H + dc * 8, j + 1);
+    const u16x8 q0 = ld8(base + (int64_t)j * ld3 + dc * 8, j);
+    const u16x8 q1 = ld8(base + (int64_t)(j + 1) * ld3 + dc * 8, j + 1);
+    const u16x8 o0 = ld8(dob + (int64_t)j * H + dc * 8, j);
+    const u16x8 o1 = ld8(dob + (int64_t)(j + 1) * H + dc * 8, j + 1);
 #pragma unroll
     for (int dd = 0; dd < 8; ++dd) {
       *reinterpret_cast<uint32_t*>(&kT[dc * 8 + dd][j]) = (uint32_t)k0[dd] | ((uint32_t)k1[dd] << 16);
@@ -477,7 +491,7 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
     }
   }
   for (int j = threadIdx.x; j < L; j += 64 * NJ)
-    mb[j] = (mask == nullptr || mask[(int64_t)b * L + j] != 0) ? 0.f : -1e30f;
+    mb[j] = j >= Lr ? -3e30f : ((mask == nullptr || mask[(int64_t)b * Lr + j] != 0) ? 0.f : -1e30f);
   __syncthreads();
 
   // ---------------- phase A: this wave's 32 queries
@@ -487,14 +501,14 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
     bf16x8 qf[4], df[4];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      qf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)i * ld3 + 16 * kk + 8 * h);
-      df[kk] = *reinterpret_cast<const bf16x8*>(dob + (int64_t)i * H + 16 * kk + 8 * h);
+      qf[kk] = ldf(base + (int64_t)i * ld3 + 16 * kk + 8 * h, i);
+      df[kk] = ldf(dob + (int64_t)i * H + 16 * kk + 8 * h, i);
     }
     float dsum = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const u16x8 o8 = *reinterpret_cast<const u16x8*>(ob + (int64_t)i * H + 32 * h + 8 * c);
-      const u16x8 d8 = *reinterpret_cast<const u16x8*>(dob + (int64_t)i * H + 32 * h + 8 * c);
+      const u16x8 o8 = ld8(ob + (int64_t)i * H + 32 * h + 8 * c, i);
+      const u16x8 d8 = ld8(dob + (int64_t)i * H + 32 * h + 8 * c, i);
 #pragma unroll
       for (int t = 0; t < 8; ++t) dsum += bf16_to_f32(o8[t]) * bf16_to_f32(d8[t]);
     }
@@ -505,8 +519,8 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
       s[jb] = (f32x16)0.f;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(base + (int64_t)(32 * jb + r32) * ld3 +
-                                                           H + 16 * kk + 8 * h);
+        const bf16x8 kf = ldf(base + (int64_t)(32 * jb + r32) * ld3 + H + 16 * kk + 8 * h,
+                              32 * jb + r32);
         s[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], s[jb], 0, 0, 0);
       }
     }
@@ -546,8 +560,8 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
       f32x16 dp = (f32x16)0.f;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(base + (int64_t)(32 * jb + r32) * ld3 +
-                                                           2 * H + 16 * kk + 8 * h);
+        const bf16x8 vf = ldf(base + (int64_t)(32 * jb + r32) * ld3 + 2 * H + 16 * kk + 8 * h,
+                              32 * jb + r32);
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, df[kk], dp, 0, 0, 0);
       }
 #pragma unroll
@@ -579,7 +593,7 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
       for (int e = 0; e < 16; e += 2) {  // rows ii, ii + 1 (e even): one paired store
         const int ii = 32 * ib + (e & 3) + 8 * (e >> 2) + 4 * h;
         store_row_pair(gb + (int64_t)ii * ld3, ld3, 32 * db + r32, o[db][e] * scale,
-                       o[db][e + 1] * scale, lane);
+                       o[db][e + 1] * scale, lane, left(ii));
       }
   }
   __syncthreads();
@@ -591,8 +605,8 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
     bf16x8 kf[4], vf[4];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
-      kf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)j * ld3 + H + 16 * kk + 8 * h);
-      vf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)j * ld3 + 2 * H + 16 * kk + 8 * h);
+      kf[kk] = ldf(base + (int64_t)j * ld3 + H + 16 * kk + 8 * h, j);
+      vf[kk] = ldf(base + (int64_t)j * ld3 + 2 * H + 16 * kk + 8 * h, j);
     }
     const float bj = mb[j];
     f32x16 dv[2] = {(f32x16)0.f, (f32x16)0.f};
@@ -602,10 +616,10 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
       f32x16 sc = (f32x16)0.f, dp = (f32x16)0.f;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(base + (int64_t)(32 * ib + r32) * ld3 +
-                                                           16 * kk + 8 * h);
-        const bf16x8 da = *reinterpret_cast<const bf16x8*>(dob + (int64_t)(32 * ib + r32) * H +
-                                                           16 * kk + 8 * h);
+        const bf16x8 qa = ldf(base + (int64_t)(32 * ib + r32) * ld3 + 16 * kk + 8 * h,
+                              32 * ib + r32);
+        const bf16x8 da = ldf(dob + (int64_t)(32 * ib + r32) * H + 16 * kk + 8 * h,
+                              32 * ib + r32);
         sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[kk], sc, 0, 0, 0);
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[kk], dp, 0, 0, 0);
       }
@@ -654,15 +668,15 @@ __global__ __launch_bounds__(64 * NJ) void attn_bwd_mfma_kernel(
       for (int e = 0; e < 16; e += 2) {
         const int jj = 32 * jb + (e & 3) + 8 * (e >> 2) + 4 * h;
         store_row_pair(gb + (int64_t)jj * ld3 + H, ld3, 32 * db + r32, dk[db][e] * scale,
-                       dk[db][e + 1] * scale, lane);
+                       dk[db][e + 1] * scale, lane, left(jj));
         store_row_pair(gb + (int64_t)jj * ld3 + 2 * H, ld3, 32 * db + r32, dv[db][e],
-                       dv[db][e + 1], lane);
+                       dv[db][e + 1], lane, left(jj));
       }
   }
 }
 
 // MFMA (bf16, DH = 64, any L <= 512: the joint padding of a batch, e.g. L = 72 or 300;
-// attn_bwd_mfma_kernel takes L = 32, 64, 96, 128): one workgroup of NW waves per
+// attn_bwd_mfma_kernel takes L <= 128): one workgroup of NW waves per
 // (sequence, head), the same two phases with loops over 32-row blocks.  Dynamic LDS:
 // the key bias and the per-query statistics [Lp] (Lp = L rounded up to 32), then one
 // or two transposed [64][Lp + 4] bf16 images: K^T in phase A, Q^T and dO^T in phase B
@@ -1047,40 +1061,36 @@ extern "C" int irc_attention_bwd(int dtype, const void* qkv, const int64_t* mask
   if (B == 0 || L == 0) return IRC_OK;
   hipStream_t st = as_stream(stream);
   using u16 = unsigned short;
-  if (dtype == 0 && dh == 64 && (L % 32 != 0 || L > 128)) {
+  if (dtype == 0 && dh == 64 && L > 128) {
     IRC_REQUIRE(L <= 512, "attention_bwd: L=%lld > 512 (BERT's position table)", (long long)L);
     const size_t lds = encb::attn_bwd_long_lds(L);
     const dim3 grid((unsigned)(B * heads));
     prof_begin(st);
-    if (L <= 128)
-      hipLaunchKernelGGL(encb::attn_bwd_long_kernel<4>, grid, dim3(256), lds, st, (const u16*)qkv,
-                         mask, (const u16*)ctx, (const u16*)dctx, (u16*)dqkv, (int)L, (int)H,
-                         (int)heads, 0.125f);
-    else
-      hipLaunchKernelGGL(encb::attn_bwd_long_kernel<8>, grid, dim3(512), lds, st, (const u16*)qkv,
-                         mask, (const u16*)ctx, (const u16*)dctx, (u16*)dqkv, (int)L, (int)H,
-                         (int)heads, 0.125f);
+    hipLaunchKernelGGL(encb::attn_bwd_long_kernel<8>, grid, dim3(512), lds, st, (const u16*)qkv,
+                       mask, (const u16*)ctx, (const u16*)dctx, (u16*)dqkv, (int)L, (int)H,
+                       (int)heads, 0.125f);
     prof_end("attention_bwd", st, (double)B * L * (3 * H + 2 * H + 3 * H) * 2.0);
     return check_launch("attention_bwd_long_kernel");
   }
-  if (dtype == 0 && dh == 64) {  // L = 32, 64, 96, 128
+  // L <= 128: whole rows in registers, L rounded up to 32-row blocks (rows past L read as
+  // zeros, never stored).  At L = 65 / 72 (32k tokens) 419 / 400 us in the blocked long
+  // kernel this replaced there, against 169 / 185 us at 64 / 96 (profiles/r06_u/).
+  if (dtype == 0 && dh == 64) {
     const float sc = 0.125f;
     const dim3 grid((unsigned)(B * heads));
     prof_begin(st);
-    switch (L / 32) {
-      case 1: hipLaunchKernelGGL(encb::attn_bwd_mfma_kernel<1>, grid, dim3(64), 0, st,
-                                 (const u16*)qkv, mask, (const u16*)ctx, (const u16*)dctx,
-                                 (u16*)dqkv, (int)H, (int)heads, sc); break;
-      case 2: hipLaunchKernelGGL(encb::attn_bwd_mfma_kernel<2>, grid, dim3(128), 0, st,
-                                 (const u16*)qkv, mask, (const u16*)ctx, (const u16*)dctx,
-                                 (u16*)dqkv, (int)H, (int)heads, sc); break;
-      case 3: hipLaunchKernelGGL(encb::attn_bwd_mfma_kernel<3>, grid, dim3(192), 0, st,
-                                 (const u16*)qkv, mask, (const u16*)ctx, (const u16*)dctx,
-                                 (u16*)dqkv, (int)H, (int)heads, sc); break;
-      default: hipLaunchKernelGGL(encb::attn_bwd_mfma_kernel<4>, grid, dim3(256), 0, st,
-                                  (const u16*)qkv, mask, (const u16*)ctx, (const u16*)dctx,
-                                  (u16*)dqkv, (int)H, (int)heads, sc); break;
+#define IRC_ABW(NJ, P)                                                                        \
+  hipLaunchKernelGGL((encb::attn_bwd_mfma_kernel<NJ, P>), grid, dim3(64 * NJ), 0, st,            \
+                     (const u16*)qkv, mask, (const u16*)ctx, (const u16*)dctx, (u16*)dqkv, (int)H, \
+                     (int)heads, sc, (int)L)
+    const bool part = L % 32 != 0;
+    switch ((L + 31) / 32) {
+      case 1: if (part) IRC_ABW(1, true); else IRC_ABW(1, false); break;
+      case 2: if (part) IRC_ABW(2, true); else IRC_ABW(2, false); break;
+      case 3: if (part) IRC_ABW(3, true); else IRC_ABW(3, false); break;
+      default: if (part) IRC_ABW(4, true); else IRC_ABW(4, false); break;
     }
+#undef IRC_ABW
     // algorithmic bytes: QKV, ctx, dctx read, dQKV written
     prof_end("attention_bwd", st, (double)B * L * (3 * H + 2 * H + 3 * H) * 2.0);
     return check_launch("attention_bwd_mfma_kernel");

@@ -57,7 +57,12 @@ def _attn_ref(qkv, mask, B, L, H, heads):
                                              (torch.bfloat16, 400, 128, 2),
                                              (torch.bfloat16, 512, 768, 12),
                                              (torch.float32, 300, 128, 2),
-                                             (torch.float32, 512, 32, 2)])
+                                             (torch.float32, 512, 32, 2),
+                                             (torch.bfloat16, 65, 768, 12),
+                                             (torch.bfloat16, 72, 256, 4),
+                                             (torch.bfloat16, 2, 128, 2),
+                                             (torch.bfloat16, 17, 256, 4),
+                                             (torch.bfloat16, 127, 256, 4)])
 def test_attention_bwd(gpu, dtype, L, H, heads):
     from irc_amd import ops
 
